@@ -1,0 +1,68 @@
+"""Shared pytest setup: the `gpu` marker and import paths.
+
+`-m "not gpu"` tests run here on CPU (oracle vs golden vectors, host logic, C-ABI exports,
+multi-rank gloo paths); `-m gpu` tests are the parity tests proper and need a MI355X.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "dbscan-on-spark_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+EPS_03F = float(np.float32(0.3))  # Scala `eps = 0.3F` widened to Double (SURVEY key fact 4b)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def labeled_data():
+    import oracle as O
+
+    return O.load_labeled_csv(os.path.join(GOLDEN, "labeled_data.csv"))
+
+
+@pytest.fixture(scope="session")
+def labeled_expected():
+    a = np.loadtxt(os.path.join(GOLDEN, "labeled_expected.csv"), delimiter=",", dtype=np.int64)
+    return dict(flag_naive=a[:, 1], cluster_naive=a[:, 2], flag_archery=a[:, 3],
+                cluster_archery=a[:, 4])
+
+
+def load_edge_cases():
+    with open(os.path.join(GOLDEN, "edge_cases.json")) as f:
+        recs = json.load(f)
+    for r in recs:
+        r["x"] = np.array([float.fromhex(v) for v in r["x"]], np.float64)
+        r["y"] = np.array([float.fromhex(v) for v in r["y"]], np.float64)
+        r["eps"] = float.fromhex(r["eps"])
+        r["cluster"] = np.array(r["cluster"], np.int32)
+        r["flag"] = np.array(r["flag"], np.uint8)
+    return recs
+
+
+def gen_blobs(n, noise=0.0, dense=1.0, seed=1, k=32):
+    """Host copy of the SURVEY §8d generator G(n, noise, dense, seed) (numpy RNG; used for
+    parity inputs -- the bench uses the device generator, whose values differ bitwise)."""
+    rng = np.random.default_rng(seed)
+    s = np.sqrt(n / 1e6)
+    n_noise = int(round(n * noise))
+    n_blob = n - n_noise
+    centres = rng.uniform(-1000 * s, 1000 * s, size=(k, 2))
+    sig = rng.uniform(20 * s, 60 * s, size=k)
+    sig[:4] /= dense
+    lab = rng.integers(0, k, size=n_blob)
+    pts = centres[lab] + rng.normal(size=(n_blob, 2)) * sig[lab, None]
+    nz = rng.uniform(-1100 * s, 1100 * s, size=(n_noise, 2))
+    allp = np.concatenate([pts, nz])
+    perm = rng.permutation(n)
+    allp = allp[perm]
+    return allp[:, 0].copy(), allp[:, 1].copy()
