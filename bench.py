@@ -1,0 +1,197 @@
+"""Benchmark: points clustered/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): G(n = 10^7 x N, 32 Gaussian blobs, no noise,
+seed 1), eps = 2.55 (k_bar ~ 49), minPoints = 10, LocalDBSCANNaive semantics, visit order =
+generation order (i.i.d. draws).  A step = one full local fit of the resident points (HBM in ->
+labels in HBM).  N = 1: one dbscan_fit_device per step.  N > 1: the slab-sharded node path
+(dbscan_amd/node.py): per-GPU slab fits with 2*eps halos + RCCL all-gathers of the boundary
+records + global union-find + relabel; per-GPU work is fixed (weak scaling).
+
+roofline: the dominant kernel of the timed region, timed with HIP events on the library's own
+stream; achieved = SURVEY §8d algorithmic bytes/point for that stage x points / avg duration.
+cpu_baseline (rank 0, N = 1): the oracle's restatement of the reference path -- the
+EvenSplitPartitioner (maxPointsPerPartition = 8192) + LocalDBSCANNaive.fit O(m^2) per partition
+(oracle/reference_pipeline.c), on host threads, for a bounded time on the same points.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
+
+METRIC = "points clustered/sec (whole node) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# SURVEY.md §8d algorithmic bytes per point, by pipeline stage (each array crosses HBM once).
+ALG_BYTES = {
+    "bbox": 16, "bin": 20, "sort_upsweep": 4, "sort_scan": 0, "sort_downsweep": 16,
+    "gather": 36, "cells": 8, "segs": 0, "count": 17, "union": 21, "final": 13, "rank": 5,
+    "output": 30,
+}
+PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--points-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--eps", type=float, default=2.55)
+    ap.add_argument("--min-points", type=int, default=10)
+    ap.add_argument("--noise", type=float, default=0.0)
+    ap.add_argument("--dense", type=float, default=1.0)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no per-stage events")
+    return ap.parse_args()
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(x, y, eps, min_points, budget, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # CPU baseline leg only
+
+    rects, counts = O.ref_partition(x, y, eps, 8192)
+    r = O.ref_fit_partitions_timed(x, y, eps, min_points, rects, counts, threads, budget)
+    return {
+        "value": r["main_points"] / r["seconds"] if r["seconds"] > 0 else None,
+        "unit": "points/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"reference path restated in C (oracle/reference_pipeline.c): "
+                   f"EvenSplitPartitioner(maxPointsPerPartition=8192) over the same {x.size} "
+                   f"points -> {len(counts)} partitions; LocalDBSCANNaive.fit O(m^2) on the first "
+                   f"{r['parts']} partitions ({r['main_points']} main / {r['outer_points']} "
+                   f"points incl. eps halos) in {r['seconds']:.2f} s on {threads} threads; "
+                   f"merge not timed"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    import dbscan_amd
+    from dbscan_amd import device as D
+
+    h = dbscan_amd.Handle(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    n_total = args.points_per_gpu * world
+    if world == 1:
+        x, y = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
+        cl = torch.empty(n_total, dtype=torch.int32, device="cuda")
+        fl = torch.empty(n_total, dtype=torch.uint8, device="cuda")
+
+        def step():
+            return D.fit_tensors(x, y, args.eps, args.min_points, 0, h, cl, fl)[2]
+    else:
+        from dbscan_amd import node
+
+        job = node.NodeJob.synthetic(n_total, args.noise, args.dense, args.seed, args.eps,
+                                     args.min_points, h, dist)
+
+        def step():
+            return job.run()
+
+    for _ in range(args.warmup):
+        k = step()
+    if not args.no_profile:
+        h.profile(True)
+        h.profile_reset()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        k = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    prof = h.profile_read() if not args.no_profile else {}
+    h.profile(False)
+    stats = h.stats()
+
+    ms_per_step = el / args.steps * 1e3
+    value = n_total * args.steps / el
+    stages = {k2: v["ms"] / max(1, args.steps) for k2, v in prof.items()}
+    roof = None
+    if prof:
+        dom = max(prof, key=lambda s: prof[s]["ms"])
+        avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])
+        pts = stats.get("n", args.points_per_gpu)
+        launches_per_step = prof[dom]["launches"] / max(1, args.steps)
+        alg = ALG_BYTES.get(dom, 0) * pts / max(1.0, launches_per_step)
+        achieved = alg / (avg_ms * 1e-3) / 1e9
+        traffic = load_traffic(dom)
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
+                "alg_bytes_per_point": ALG_BYTES.get(dom, 0),
+                "pipeline_frac": round(PIPELINE_ALG_BYTES * pts / (ms_per_step * 1e-3) / 1e9
+                                       / HBM_PEAK_GBS, 5)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sx, sy = x.cpu().numpy(), y.cpu().numpy()
+        cpu = cpu_baseline(sx, sy, args.eps, args.min_points, args.cpu_budget, args.cpu_threads)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "points/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (device generator G(n, noise, dense, seed), SURVEY §8d)",
+            "config": {
+                "workload": (f"G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
+                             f"dense={args.dense}, seed={args.seed}), eps={args.eps}, "
+                             f"minPoints={args.min_points}, LocalDBSCANNaive semantics"),
+                "n_points": n_total, "eps": args.eps, "min_points": args.min_points,
+                "parallelism": "single GPU" if world == 1 else f"slab x{world} + RCCL merge",
+                "clusters": k, "core_points": stats.get("core"),
+                "occupied_cells": stats.get("cells")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages_ms_per_step": {k2: round(v, 4) for k2, v in stages.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,424 @@
+// capi.hip -- the C-ABI of libdbscan_hip.so (declared in include/dbscan_hip.h): handles,
+// error reporting, host<->device staging, profiling and the synthetic generator.
+//
+// Boundary replaced: `new LocalDBSCANNaive(eps, minPoints).fit(points)` at DBSCAN.scala:153-154
+// (LocalDBSCANNaive.scala:31,37; LocalDBSCANArchery.scala:32,36).  Return codes and ownership
+// follow SURVEY.md §8b: the caller owns host arrays, the handle owns grow-only device buffers,
+// no pointer is retained past a call, errors go to a thread-local dbscan_last_error().
+#include "../../include/dbscan_hip.h"
+#include "internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+
+namespace dbscan {
+
+HipError::HipError(hipError_t e, const char* expr, const char* file, int line) : err(e) {
+    char buf[512];
+    snprintf(buf, sizeof(buf), "HIP error %d (%s) at %s:%d: %s", (int)e, hipGetErrorString(e),
+             file, line, expr);
+    what = buf;
+}
+
+void* DevBuf::ensure(size_t need) {
+    if (need == 0) need = 16;
+    if (need <= bytes) return p;
+    release();
+    size_t cap = need + need / 8;  // grow-only with headroom
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        bytes = 0;
+        throw HipError(e, "hipMalloc (workspace)", __FILE__, __LINE__);
+    }
+    bytes = cap;
+    return p;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+hipEvent_t Profiler::take() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    DBSCAN_HIP_CHECK(hipEventCreate(&e));
+    return e;
+}
+
+int Profiler::stage_index(const char* name) {
+    for (size_t i = 0; i < stages.size(); ++i)
+        if (stages[i].name == name) return (int)i;
+    stages.push_back(Stage{name, 0.0, 0});
+    return (int)stages.size() - 1;
+}
+
+void Profiler::flush() {
+    for (auto& pe : pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            stages[pe.stage].ms += ms;
+            stages[pe.stage].launches += 1;
+        }
+        pool.push_back(pe.a);
+        pool.push_back(pe.b);
+    }
+    pending.clear();
+}
+
+void Profiler::destroy() {
+    for (auto& pe : pending) {
+        pool.push_back(pe.a);
+        pool.push_back(pe.b);
+    }
+    pending.clear();
+    for (auto e : pool) (void)hipEventDestroy(e);
+    pool.clear();
+}
+
+StageTimer::StageTimer(Profiler* p, hipStream_t st, const char* name) : prof(p), s(st) {
+    if (!prof || !prof->on) {
+        prof = nullptr;
+        return;
+    }
+    stage = prof->stage_index(name);
+    a = prof->take();
+    DBSCAN_HIP_CHECK(hipEventRecord(a, s));
+}
+
+StageTimer::~StageTimer() {
+    if (!prof) return;
+    hipEvent_t b = prof->take();
+    if (hipEventRecord(b, s) == hipSuccess) prof->pending.push_back({stage, a, b});
+}
+
+// ------------------------------------ generator -----------------------------------------
+
+namespace {
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t& st) {
+    uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline double u01_open(uint64_t v) {  // (0, 1]
+    return ((double)(v >> 11) + 1.0) * 0x1p-53;
+}
+
+constexpr int kBlobs = 32;
+struct BlobParams {
+    double cx[kBlobs], cy[kBlobs], sigma[kBlobs];
+    double noise_half;  // noise over [-noise_half, noise_half]^2
+    double noise_frac;
+    uint64_t seed;
+};
+
+__global__ __launch_bounds__(256) void gen_blobs_kernel(BlobParams bp, int64_t n, double* x,
+                                                        double* y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st = bp.seed ^ ((uint64_t)i * 0xD1B54A32D192ED03ull);
+    (void)splitmix64(st);
+    const double u0 = u01_open(splitmix64(st));
+    const uint64_t r1 = splitmix64(st);
+    const double u2 = u01_open(splitmix64(st));
+    const double u3 = u01_open(splitmix64(st));
+    if (u0 <= bp.noise_frac) {
+        x[i] = (2.0 * u2 - 1.0) * bp.noise_half;
+        y[i] = (2.0 * u3 - 1.0) * bp.noise_half;
+    } else {
+        const int b = (int)(r1 % kBlobs);
+        const double rad = sqrt(-2.0 * log(u2));
+        const double th = 6.283185307179586 * u3;
+        x[i] = bp.cx[b] + bp.sigma[b] * rad * cos(th);
+        y[i] = bp.cy[b] + bp.sigma[b] * rad * sin(th);
+    }
+}
+
+}  // namespace
+}  // namespace dbscan
+
+// ------------------------------------ handle --------------------------------------------
+
+struct dbscan_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    dbscan::Workspace ws;
+    dbscan::Profiler prof;
+    dbscan::FitStats stats;
+    dbscan::DevBuf hx, hy, hcl, hfl;  // staging for the host-array entry points
+    std::mutex mu;                    // one fit at a time per handle
+};
+
+namespace {
+
+thread_local std::string g_err;
+thread_local std::unique_ptr<dbscan_handle, void (*)(dbscan_handle*)> g_tls_handle(
+    nullptr, dbscan_destroy);
+
+void set_err(const std::string& s) { g_err = s; }
+
+template <class F>
+int32_t guarded(dbscan_handle* h, F&& f) {
+    g_err.clear();
+    try {
+        if (h) {
+            hipError_t e = hipSetDevice(h->device);
+            if (e != hipSuccess) throw dbscan::HipError(e, "hipSetDevice", __FILE__, __LINE__);
+        }
+        return f();
+    } catch (const dbscan::ArgError& e) {
+        set_err(e.what);
+        return DBSCAN_EARG;
+    } catch (const dbscan::HipError& e) {
+        set_err(e.what);
+        return (e.err == hipErrorOutOfMemory || e.err == hipErrorMemoryAllocation) ? DBSCAN_EOOM
+                                                                                    : DBSCAN_EHIP;
+    } catch (const std::bad_alloc&) {
+        set_err("host allocation failed");
+        return DBSCAN_EOOM;
+    } catch (...) {
+        set_err("unknown error");
+        return DBSCAN_EHIP;
+    }
+}
+
+void check_fit_args(int64_t n, double eps, int32_t mode, const void* a, const void* b,
+                    const void* c, const void* d) {
+    (void)eps;
+    if (n < 0) throw dbscan::ArgError{"n < 0"};
+    if (n > DBSCAN_MAX_POINTS) throw dbscan::ArgError{"n exceeds DBSCAN_MAX_POINTS"};
+    if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
+        throw dbscan::ArgError{"mode must be DBSCAN_MODE_NAIVE or DBSCAN_MODE_ARCHERY"};
+    if (n > 0 && (!a || !b || !c || !d)) throw dbscan::ArgError{"NULL array pointer"};
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dbscan_last_error(void) { return g_err.c_str(); }
+
+int32_t dbscan_version(void) { return 100; }
+
+int32_t dbscan_device_count(void) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return c;
+}
+
+dbscan_handle* dbscan_create(int32_t device) {
+    g_err.clear();
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_err("no HIP device visible");
+        return nullptr;
+    }
+    if (device < 0 || device >= count) {
+        set_err("device index out of range");
+        return nullptr;
+    }
+    dbscan_handle* h = new (std::nothrow) dbscan_handle();
+    if (!h) {
+        set_err("host allocation failed");
+        return nullptr;
+    }
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        set_err(std::string("hipStreamCreate failed: ") + hipGetErrorString(e));
+        delete h;
+        return nullptr;
+    }
+    return h;
+}
+
+void dbscan_destroy(dbscan_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->prof.destroy();
+    h->ws.release();
+    h->hx.release();
+    h->hy.release();
+    h->hcl.release();
+    h->hfl.release();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+void* dbscan_stream(dbscan_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
+                          double eps, int32_t min_points, int32_t mode, int32_t* d_cluster,
+                          uint8_t* d_flag, int32_t* n_clusters_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
+        dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
+                          nullptr, nullptr, nullptr};
+        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+        h->prof.flush();
+        if (n_clusters_out) *n_clusters_out = (int32_t)k;
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t n, double eps,
+                     int32_t min_points, int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                     int32_t* n_clusters_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, mode, x, y, cluster_out, flag_out);
+        if (n == 0) {
+            if (n_clusters_out) *n_clusters_out = 0;
+            h->stats = dbscan::FitStats();
+            return DBSCAN_OK;
+        }
+        double* dx = static_cast<double*>(h->hx.ensure(n * sizeof(double)));
+        double* dy = static_cast<double*>(h->hy.ensure(n * sizeof(double)));
+        int32_t* dcl = static_cast<int32_t*>(h->hcl.ensure(n * sizeof(int32_t)));
+        uint8_t* dfl = static_cast<uint8_t*>(h->hfl.ensure(n));
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl,
+                          nullptr, nullptr, nullptr};
+        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
+                                        hipMemcpyDeviceToHost, h->stream));
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(flag_out, dfl, n, hipMemcpyDeviceToHost, h->stream));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->prof.flush();
+        if (n_clusters_out) *n_clusters_out = (int32_t)k;
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_fit(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
+                   int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                   int32_t* n_clusters_out) {
+    if (!g_tls_handle) {
+        dbscan_handle* h = dbscan_create(0);
+        if (!h) return DBSCAN_EHIP;
+        g_tls_handle.reset(h);
+    }
+    return dbscan_fit_h(g_tls_handle.get(), x, y, n, eps, min_points, mode, cluster_out,
+                        flag_out, n_clusters_out);
+}
+
+int32_t dbscan_fit_slab_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                               const uint8_t* d_zone, int64_t n, double eps,
+                               int32_t min_points, uint8_t* d_core, int32_t* d_root,
+                               int32_t* d_bmin) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, DBSCAN_MODE_NAIVE, d_x, d_y, d_core, d_root);
+        if (n > 0 && (!d_zone || !d_bmin)) throw dbscan::ArgError{"NULL array pointer"};
+        dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
+                          nullptr, d_core, d_root, d_bmin};
+        dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+        h->prof.flush();
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {
+    if (!h || !out) return DBSCAN_EARG;
+    const int64_t v[9] = {h->stats.n,  h->stats.nf,  h->stats.ncells,
+                          h->stats.ncore, h->stats.nclusters, h->stats.nx,
+                          h->stats.ny, h->stats.bits, h->stats.grid_mode};
+    int k = 0;
+    for (; k < max && k < 9; ++k) out[k] = v[k];
+    return k;
+}
+
+int32_t dbscan_profile_enable(dbscan_handle* h, int32_t on) {
+    if (!h) return DBSCAN_EARG;
+    h->prof.on = on != 0;
+    return DBSCAN_OK;
+}
+
+int32_t dbscan_profile_reset(dbscan_handle* h) {
+    if (!h) return DBSCAN_EARG;
+    h->prof.stages.clear();
+    return DBSCAN_OK;
+}
+
+int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, double* total_ms,
+                            int64_t* launches, int32_t max) {
+    if (!h) return DBSCAN_EARG;
+    int32_t k = 0, off = 0;
+    for (auto& st : h->prof.stages) {
+        if (k >= max) break;
+        const int len = (int)st.name.size() + 1;
+        if (names) {
+            if (off + len > names_cap) break;
+            memcpy(names + off, st.name.c_str(), (size_t)len);
+        }
+        off += len;
+        if (total_ms) total_ms[k] = st.ms;
+        if (launches) launches[k] = st.launches;
+        ++k;
+    }
+    return k;
+}
+
+int32_t dbscan_generate_blobs_device(dbscan_handle* h, double* d_x, double* d_y, int64_t n,
+                                     double noise_frac, double dense, uint64_t seed) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        if (n < 0 || (n > 0 && (!d_x || !d_y))) throw dbscan::ArgError{"bad generator args"};
+        if (n == 0) return DBSCAN_OK;
+        dbscan::BlobParams bp;
+        const double s = std::sqrt((double)n / 1e6);  // SURVEY §8d scale-invariant generator
+        uint64_t st = seed * 0x2545F4914F6CDD1Dull + 0x1234567ull;
+        for (int b = 0; b < dbscan::kBlobs; ++b) {
+            bp.cx[b] = (2.0 * dbscan::u01_open(dbscan::splitmix64(st)) - 1.0) * 1000.0 * s;
+            bp.cy[b] = (2.0 * dbscan::u01_open(dbscan::splitmix64(st)) - 1.0) * 1000.0 * s;
+            bp.sigma[b] = (20.0 + 40.0 * dbscan::u01_open(dbscan::splitmix64(st))) * s;
+            if (b < 4 && dense > 0) bp.sigma[b] /= dense;
+        }
+        bp.noise_half = 1100.0 * s;
+        bp.noise_frac = noise_frac;
+        bp.seed = seed;
+        hipLaunchKernelGGL(dbscan::gen_blobs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                           0, h->stream, bp, n, d_x, d_y);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        return DBSCAN_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,577 @@
+// fit.hip -- the local DBSCAN fit on gfx950: eps grid, neighbour counts, lock-free
+// union-find, border/noise labelling and cluster numbering.
+//
+// Reference semantics restated here (src/main/scala/org/apache/spark/mllib/clustering/dbscan/):
+//   DBSCANPoint.scala:26-30           the fp64 predicate dx*dx + dy*dy <= eps*eps, no FMA
+//   LocalDBSCANNaive.scala:37-118     order-dependent fit, as its closed form:
+//     core(p) <=> |N(p)| >= minPoints (N includes p);  clusters = components of the core-core
+//     eps graph;  s(K) = smallest visit index of a core in K;  cluster id = rank of s(K);
+//     non-core b with adjacent clusters A and m = min s(K) over A:
+//       Naive  : Border of the cluster with s = m if A != {} and m < index(b), else Noise
+//       Archery: Border of the cluster with s = m if A != {}, else Noise
+//                                                    (LocalDBSCANArchery.scala:103-106 re-claim)
+//
+// Kernels, in pipeline order (one HIP stream per handle; see DESIGN.md for the rooflines):
+//   bin        key = cy*nx + cx (u32) per point, perm = input index
+//   [radix sort (primitives.hip)]
+//   gather     sorted double2 coordinates (AoS) -- one global_load_dwordx4 per candidate test
+//   cells      occupied cells from the key head flags (scan) -> ckey, cstart, cell-of-slot
+//   segs       per cell: slot ranges of the 3 stencil rows (row-major keys make the 3 cells of a
+//              stencil row one contiguous slot range)
+//   count      thread per slot: candidate loop with early exit at minPoints -> core flag
+//   union      thread per core slot: candidates with smaller slot only (rows cy-1 and the
+//              head of row cy); lock-free union-find hooking the root with the larger visit
+//              index under the smaller (CAS, agent scope), so every root is s(K) directly
+//   final      root of every core -> lab = visit index of its root; roots flagged in input order
+//   [scan of root flags in input order -> rank = cluster id - 1]
+//   output     cores: rank[lab]+1; non-cores: min lab over core neighbours + Naive/Archery rule;
+//              written in input order
+#include "internal.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace dbscan {
+
+enum GridMode { kGridEps = 0, kGridAllPairs = 1, kGridNoPairs = 2 };
+
+struct GridParams {
+    double xmin2, ymin2, invx, invy;  // cell = floor((v*0.5 - vmin*0.5) * inv)
+    uint32_t nx, ny;
+};
+
+namespace {
+
+// DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
+// two rounded multiplies, one rounded add, <=.  The whole library is built with
+// -ffp-contract=off; the pragma pins it here as well.
+__device__ __forceinline__ bool within_eps(double px, double py, double ox, double oy,
+                                           double eps2) {
+#pragma clang fp contract(off)
+    const double dx = ox - px;
+    const double dy = oy - py;
+    const double a = dx * dx;
+    const double b = dy * dy;
+    return (a + b) <= eps2;
+}
+
+struct Seg {  // 32 B: rows dy = -1, 0, +1 as [b, e) slot ranges
+    int b0, e0, b1, e1, b2, e2, pad0, pad1;
+};
+
+__device__ __forceinline__ Seg load_seg(const Seg* seg, int c) {
+    const int4* p = reinterpret_cast<const int4*>(seg + c);
+    const int4 u = p[0];
+    const int4 v = p[1];
+    Seg s;
+    s.b0 = u.x; s.e0 = u.y; s.b1 = u.z; s.e1 = u.w; s.b2 = v.x; s.e2 = v.y;
+    s.pad0 = 0; s.pad1 = 0;
+    return s;
+}
+
+// Candidate iteration over up to three slot ranges [b0,e0) [b1,e1) [b2,e2) (the stencil rows).
+// f(j) returns false to stop early.
+template <class F>
+__device__ __forceinline__ void for_candidates(const Seg& s, F f) {
+    const int b[3] = {s.b0, s.b1, s.b2};
+    const int e[3] = {s.e0, s.e1, s.e2};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        for (int j = b[r]; j < e[r]; ++j)
+            if (!f(j)) return;
+}
+
+__global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ x,
+                                                     const double* __restrict__ y, int64_t n,
+                                                     GridParams g, uint32_t* __restrict__ key,
+                                                     int32_t* __restrict__ perm) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double a = x[i], b = y[i];
+    uint32_t k = kSentinelKey;
+    if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
+        double fx = floor((a * 0.5 - g.xmin2) * g.invx);
+        double fy = floor((b * 0.5 - g.ymin2) * g.invy);
+        fx = fx < 0 ? 0 : (fx > (double)(g.nx - 1) ? (double)(g.nx - 1) : fx);
+        fy = fy < 0 ? 0 : (fy > (double)(g.ny - 1) ? (double)(g.ny - 1) : fy);
+        k = (uint32_t)((uint64_t)fy * g.nx + (uint64_t)fx);
+    }
+    key[i] = k;
+    perm[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void iota_key_kernel(int64_t n, uint32_t kval,
+                                                          uint32_t* __restrict__ key,
+                                                          int32_t* __restrict__ perm) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    key[i] = kval;
+    perm[i] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict__ x,
+                                                        const double* __restrict__ y, int64_t nf,
+                                                        const int32_t* __restrict__ perm,
+                                                        double2* __restrict__ xy) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nf) return;
+    const int32_t o = perm[p];
+    xy[p] = make_double2(x[o], y[o]);
+}
+
+// cell[p] holds the exclusive scan of head flags on entry; converted to the cell index.
+__global__ __launch_bounds__(kBlock) void cells_kernel(const uint32_t* __restrict__ key,
+                                                       int64_t nf, int32_t* __restrict__ cell,
+                                                       uint32_t* __restrict__ ckey,
+                                                       int32_t* __restrict__ cstart,
+                                                       const int32_t* __restrict__ ncells) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nf) {
+        if (p == nf) cstart[*ncells] = (int32_t)nf;
+        return;
+    }
+    const int32_t ex = cell[p];
+    const bool head = (p == 0) || key[p] != key[p - 1];
+    if (head) {
+        ckey[ex] = key[p];
+        cstart[ex] = (int32_t)p;
+    }
+    cell[p] = ex + (head ? 1 : 0) - 1;
+}
+
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t k) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = lo + ((hi - lo) >> 1);
+        if (a[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict__ ckey,
+                                                      const int32_t* __restrict__ cstart,
+                                                      const int32_t* __restrict__ ncells_p,
+                                                      GridParams g, Seg* __restrict__ seg) {
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    const int C = *ncells_p;
+    if (c >= C) return;
+    const uint32_t key = ckey[c];
+    const uint32_t cy = key / g.nx, cx = key - cy * g.nx;
+    const uint32_t lox = cx > 0 ? cx - 1 : cx;
+    const uint32_t hix = cx + 1 < g.nx ? cx + 1 : cx;
+    int rb[3], re[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        rb[r] = 0;
+        re[r] = 0;
+        const int64_t ry = (int64_t)cy + r - 1;
+        if (ry < 0 || ry >= (int64_t)g.ny) continue;
+        const uint32_t klo = (uint32_t)ry * g.nx + lox, khi = (uint32_t)ry * g.nx + hix;
+        int a, z;
+        if (r == 1) {  // own row: neighbours are adjacent entries of ckey
+            a = (c > 0 && ckey[c - 1] == klo && lox != cx) ? c - 1 : c;
+            z = (c + 1 < C && ckey[c + 1] == khi && hix != cx) ? c + 2 : c + 1;
+        } else {
+            a = lower_bound_u32(ckey, C, klo);
+            z = a;
+            while (z < C && ckey[z] <= khi) ++z;
+        }
+        rb[r] = cstart[a];
+        re[r] = cstart[z];
+    }
+    Seg s;
+    s.b0 = rb[0]; s.e0 = re[0]; s.b1 = rb[1]; s.e1 = re[1]; s.b2 = rb[2]; s.e2 = re[2];
+    s.pad0 = 0; s.pad1 = 0;
+    seg[c] = s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Neighbour counts -> core flags (LocalDBSCANNaive.scala:52-54, :99-101), with early exit
+// once minPoints neighbours are seen (the count itself is never an output).
+// zone (optional, slab fits): zone-2 points are halo-only candidates -> never core.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict__ xy,
+                                                       const int32_t* __restrict__ cell,
+                                                       const Seg* __restrict__ seg, int64_t n,
+                                                       int64_t nf, double eps2,
+                                                       int32_t min_points,
+                                                       const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ zone,
+                                                       uint8_t* __restrict__ core,
+                                                       int32_t* __restrict__ parent,
+                                                       int32_t* __restrict__ ncore) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t nact = __ballot(p < n);
+    if (p >= n) return;
+    parent[p] = (int32_t)p;
+    bool is_core;
+    if (zone && zone[perm[p]] == 2) {
+        is_core = false;
+    } else if (min_points <= 0) {
+        is_core = true;
+    } else if (p >= nf) {
+        is_core = false;  // outside the grid: no neighbours, not even itself
+    } else {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int cnt = 0;
+        for_candidates(s, [&](int j) {
+            const double2 q = xy[j];
+            cnt += within_eps(me.x, me.y, q.x, q.y, eps2) ? 1 : 0;
+            return cnt < min_points;
+        });
+        is_core = cnt >= min_points;
+    }
+    core[p] = is_core ? 1 : 0;
+    const uint64_t cm = __ballot(is_core);
+    if (__lane_id() == (int)__ffsll((unsigned long long)nact) - 1 && cm)
+        atomicAdd(ncore, (int32_t)__popcll(cm));
+}
+
+// ---------------------------------------------------------------------------------------
+// Lock-free union-find over slots.  parent pointers always lead to a strictly smaller visit
+// index (perm), so there are no cycles and a root is the minimum-index core of its set.
+// Loads/stores are agent-scope relaxed atomics (L1-bypassing), hooks are CAS on roots only;
+// stale reads only ever show an older ancestor, which is still an ancestor.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int ld_par(int* par, int i) {
+    return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_par(int* par, int i, int v) {
+    __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ int uf_find(int* par, int x) {
+    int cur = ld_par(par, x);
+    if (cur == x) return x;
+    int prev = x;
+    for (;;) {
+        const int next = ld_par(par, cur);
+        if (next == cur) return cur;
+        st_par(par, prev, next);  // path halving (prev is a non-root: only ancestors stored)
+        prev = cur;
+        cur = next;
+    }
+}
+
+// Merge the sets of believed roots ra, rb; returns the believed root of the union.
+__device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra, int rb) {
+    while (ra != rb) {
+        const bool swap = prio[ra] < prio[rb];
+        const int hi = swap ? rb : ra;  // larger visit index: hooked
+        const int lo = swap ? ra : rb;
+        int expected = hi;
+        if (__hip_atomic_compare_exchange_strong(par + hi, &expected, lo, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return lo;
+        ra = uf_find(par, expected);  // hi was hooked meanwhile: continue from its new parent
+        rb = uf_find(par, lo);
+    }
+    return ra;
+}
+
+__global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict__ xy,
+                                                       const int32_t* __restrict__ cell,
+                                                       const Seg* __restrict__ seg, int64_t nf,
+                                                       double eps2,
+                                                       const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ core,
+                                                       int32_t* __restrict__ parent) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nf || !core[p]) return;
+    const double2 me = xy[p];
+    Seg s = load_seg(seg, cell[p]);
+    // only slots < p: row cy-1 entirely, row cy up to p, row cy+1 never
+    s.e1 = (int)p;
+    s.b2 = 0;
+    s.e2 = 0;
+    int rp = uf_find(parent, (int)p);
+    for_candidates(s, [&](int j) {
+        const double2 q = xy[j];
+        if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
+            const int rj = uf_find(parent, j);
+            if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
+        }
+        return true;
+    });
+}
+
+__global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
+                                                       const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ core,
+                                                       const int32_t* __restrict__ parent,
+                                                       int32_t* __restrict__ lab,
+                                                       uint8_t* __restrict__ is_root) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    if (!core[p]) {
+        lab[p] = -1;
+        return;
+    }
+    int r = (int)p;
+    for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
+    lab[p] = perm[r];
+    if (r == (int)p && is_root) is_root[perm[p]] = 1;
+}
+
+// Border / noise rule + cluster numbering, written in input order.
+__global__ __launch_bounds__(kBlock) void output_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2, int32_t mode,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    const int32_t* __restrict__ lab, const int32_t* __restrict__ rank,
+    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const int32_t o = perm[p];
+    int32_t cl = 0;
+    uint8_t fl = 2;  // Noise
+    if (core[p]) {
+        cl = rank[lab[p]] + 1;
+        fl = 1;  // Core
+    } else if (p < nf) {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int32_t m = 0x7FFFFFFF;
+        for_candidates(s, [&](int j) {
+            const double2 q = xy[j];
+            if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
+                const int32_t lj = lab[j];
+                m = lj < m ? lj : m;
+            }
+            return true;
+        });
+        if (m != 0x7FFFFFFF && (mode != 0 || m < o)) {
+            cl = rank[m] + 1;
+            fl = 0;  // Border
+        }
+    }
+    cluster_out[o] = cl;
+    flag_out[o] = fl;
+}
+
+// Slab fit output (multi-GPU): core flag, local root (slab index), border minimum root.
+__global__ __launch_bounds__(kBlock) void slab_output_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
+    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
+    uint8_t* __restrict__ core_out, int32_t* __restrict__ root_out,
+    int32_t* __restrict__ bmin_out) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const int32_t o = perm[p];
+    int32_t m = -1;
+    if (!core[p] && p < nf && zone[o] == 0) {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int32_t best = 0x7FFFFFFF;
+        for_candidates(s, [&](int j) {
+            const double2 q = xy[j];
+            if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
+                const int32_t lj = lab[j];
+                best = lj < best ? lj : best;
+            }
+            return true;
+        });
+        m = best == 0x7FFFFFFF ? -1 : best;
+    }
+    core_out[o] = core[p];
+    root_out[o] = core[p] ? lab[p] : -1;
+    bmin_out[o] = m;
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------------------
+
+// Grid sizing on the host (see DESIGN.md "grid soundness"): cell side >= R*(1+2^-16) with
+// R = max(|eps|*(1+2^-40), 2^-500) bounds |x'-x| for every pair the fp64 predicate accepts;
+// cells per axis <= 2^31 and nx*ny <= 2^31 (u32 keys with a sentinel), growing the side
+// (never shrinking it) when the extent would need more cells.
+static bool make_grid(const double bb[5], double eps, GridParams* g) {
+    const double xmin = bb[0], xmax = bb[1], ymin = bb[2], ymax = bb[3];
+    double R = std::fabs(eps) * (1.0 + 0x1p-40);
+    if (R < 0x1p-500) R = 0x1p-500;
+    double hx = R * (1.0 + 0x1p-16), hy = hx;
+    const double limit = 2147483648.0;  // 2^31 cells
+    auto cells = [](double vmax, double vmin, double h) {
+        const double t = (vmax * 0.5 - vmin * 0.5) * (2.0 / h);
+        return std::floor(t) + 1.0;  // may be +inf for absurd extents
+    };
+    for (int it = 0; it < 4096; ++it) {
+        const double cx = cells(xmax, xmin, hx), cy = cells(ymax, ymin, hy);
+        if (cx <= limit && cy <= limit && cx * cy <= limit) {
+            g->invx = 2.0 / hx;
+            g->invy = 2.0 / hy;
+            g->xmin2 = xmin * 0.5;
+            g->ymin2 = ymin * 0.5;
+            g->nx = (uint32_t)cx;
+            g->ny = (uint32_t)cy;
+            return true;
+        }
+        if (cx >= cy) hx *= 2.0; else hy *= 2.0;
+    }
+    return false;
+}
+
+int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st) {
+    const int64_t n = a.n;
+    FitStats stats;
+    stats.n = n;
+    if (n == 0) {
+        if (st) *st = stats;
+        return 0;
+    }
+    const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
+    int mode = std::isnan(eps2) ? kGridNoPairs : (std::isinf(eps2) ? kGridAllPairs : kGridEps);
+
+    uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
+    uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
+    int32_t* perm = static_cast<int32_t*>(ws.perm.ensure(n * sizeof(int32_t)));
+    int32_t* perm2 = static_cast<int32_t*>(ws.perm2.ensure(n * sizeof(int32_t)));
+    double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
+    int32_t* misc_i = reinterpret_cast<int32_t*>(misc + 16);  // [0] ncells, [1] nclusters
+
+    DBSCAN_HIP_CHECK(hipMemsetAsync(misc_i, 0, 4 * sizeof(int32_t), s));
+    GridParams g{0, 0, 0, 0, 1, 1};
+    int64_t nf = 0;
+    int bits = 0;
+    if (mode == kGridEps) {
+        double bb[5];
+        {
+            StageTimer t(prof, s, "bbox");
+            bbox_finite(s, a.x, a.y, n, misc, ws.scan_tmp);
+        }
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(bb, misc, sizeof(bb), hipMemcpyDeviceToHost, s));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        nf = (int64_t)bb[4];
+        if (nf > 0 && !make_grid(bb, a.eps, &g)) throw ArgError{"cannot size the eps grid"};
+        if (nf == 0) mode = kGridNoPairs;
+    } else if (mode == kGridAllPairs) {
+        nf = n;  // one cell holding every point; the predicate decides (incl. non-finite)
+    }
+    stats.grid_mode = mode;
+    stats.nf = nf;
+    stats.nx = g.nx;
+    stats.ny = g.ny;
+
+    if (mode == kGridEps) {
+        {
+            StageTimer t(prof, s, "bin");
+            hipLaunchKernelGGL(bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, g, key,
+                               perm);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        const uint64_t cells = (uint64_t)g.nx * g.ny;  // valid keys < cells <= 2^31
+        bits = 1;
+        while (bits < 32 && (1ull << bits) <= cells) ++bits;  // keys < 2^bits - 1 (sentinel)
+        radix_sort_pairs(s, key, perm, key2, perm2, n, bits, ws.hist, ws.scan_tmp, prof);
+    } else {
+        StageTimer t(prof, s, "bin");
+        hipLaunchKernelGGL(iota_key_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
+                           mode == kGridAllPairs ? 0u : kSentinelKey, key, perm);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+    stats.bits = bits;
+
+    const int64_t nfa = nf > 0 ? nf : 1;
+    double2* xy = static_cast<double2*>(ws.xy.ensure(nfa * sizeof(double2)));
+    int32_t* cell = static_cast<int32_t*>(ws.cell.ensure(nfa * sizeof(int32_t)));
+    uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(nfa * sizeof(uint32_t)));
+    int32_t* cstart = static_cast<int32_t*>(ws.cstart.ensure((nfa + 1) * sizeof(int32_t)));
+    Seg* seg = static_cast<Seg*>(ws.seg.ensure(nfa * sizeof(Seg)));
+    uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
+    int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
+    int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
+
+    if (nf > 0) {
+        {
+            StageTimer t(prof, s, "gather");
+            hipLaunchKernelGGL(gather_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, a.x, a.y, nf,
+                               perm, xy);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer t(prof, s, "cells");
+            exclusive_scan(s, 2, key, cell, nf, &misc_i[0], ws.scan_tmp);
+            hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, nf,
+                               cell, ckey, cstart, &misc_i[0]);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer t(prof, s, "segs");
+            hipLaunchKernelGGL(segs_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, ckey, cstart,
+                               &misc_i[0], g, seg);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+    }
+    {
+        StageTimer t(prof, s, "count");
+        hipLaunchKernelGGL(count_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, n, nf,
+                           eps2, a.min_points, perm, a.zone, core, parent, &misc_i[2]);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+    if (nf > 0) {
+        StageTimer t(prof, s, "union");
+        hipLaunchKernelGGL(union_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, nf,
+                           eps2, perm, core, parent);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+    int64_t k = 0;
+    if (!a.zone) {
+        uint8_t* is_root = static_cast<uint8_t*>(ws.is_root.ensure(n));
+        int32_t* rank = static_cast<int32_t*>(ws.rank.ensure(n * sizeof(int32_t)));
+        {
+            StageTimer t(prof, s, "final");
+            DBSCAN_HIP_CHECK(hipMemsetAsync(is_root, 0, n, s));
+            hipLaunchKernelGGL(final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
+                               parent, lab, is_root);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer t(prof, s, "rank");
+            exclusive_scan(s, 1, is_root, rank, n, &misc_i[1], ws.scan_tmp);
+        }
+        {
+            StageTimer t(prof, s, "output");
+            hipLaunchKernelGGL(output_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, n,
+                               nf, eps2, a.mode, perm, core, lab, rank, a.cluster, a.flag);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        int32_t hv[3];
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        k = hv[1];
+        stats.ncells = nf > 0 ? hv[0] : 0;
+        stats.ncore = hv[2];
+    } else {
+        {
+            StageTimer t(prof, s, "final");
+            hipLaunchKernelGGL(final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
+                               parent, lab, (uint8_t*)nullptr);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer t(prof, s, "output");
+            hipLaunchKernelGGL(slab_output_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell,
+                               seg, n, nf, eps2, perm, a.zone, core, lab, a.core_out, a.root_out,
+                               a.bmin_out);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        int32_t hv[3];
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        stats.ncells = nf > 0 ? hv[0] : 0;
+        stats.ncore = hv[2];
+    }
+    stats.nclusters = k;
+    if (st) *st = stats;
+    return k;
+}
+
+}  // namespace dbscan

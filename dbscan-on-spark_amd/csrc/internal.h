@@ -1,0 +1,137 @@
+// internal.h -- shared declarations of libdbscan_hip.so (gfx950 only).
+//
+// Device data layout (one fit, n points, nf finite points in the eps grid):
+//   key[n]   u32 cell key cy*nx+cx (0xFFFFFFFF for points outside the grid)   -> radix sorted
+//   perm[n]  i32 input index of each sorted slot (the reference's visit index)
+//   xy[nf]   double2 sorted coordinates, SoA->AoS so one 16-B load feeds a candidate test
+//   cell[nf] i32 occupied-cell index of each sorted slot
+//   ckey[C], cstart[C+1]  occupied cells (sorted keys) and their first slot
+//   seg[C]   int8 (b0,e0,b1,e1,b2,e2,-,-): slot ranges of the 3 rows of the 3x3 stencil
+//   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
+//   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace dbscan {
+
+constexpr uint32_t kSentinelKey = 0xFFFFFFFFu;
+constexpr int kBlock = 256;
+
+#define DBSCAN_HIP_CHECK(expr)                                                              \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) throw ::dbscan::HipError(_e, #expr, __FILE__, __LINE__);     \
+    } while (0)
+
+struct HipError {
+    hipError_t err;
+    std::string what;
+    HipError(hipError_t e, const char* expr, const char* file, int line);
+};
+
+struct ArgError {
+    std::string what;
+};
+
+// Grow-only device buffer (owned by one handle; never copied).
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    void* ensure(size_t need);
+    void release();
+    ~DevBuf() { release(); }
+};
+
+// Stage timing with events on the fit stream.
+struct Profiler {
+    bool on = false;
+    struct Stage {
+        std::string name;
+        double ms = 0;
+        int64_t launches = 0;
+    };
+    std::vector<Stage> stages;
+    struct Pending {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t take();
+    int stage_index(const char* name);
+    void flush();  // after the stream is synchronized: accumulate and recycle events
+    void destroy();
+};
+
+// RAII bracket around one stage's launches.
+struct StageTimer {
+    Profiler* prof;
+    hipStream_t s;
+    int stage = -1;
+    hipEvent_t a = nullptr;
+    StageTimer(Profiler* p, hipStream_t st, const char* name);
+    ~StageTimer();
+};
+
+struct Workspace {
+    DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
+        is_root, rank, misc;
+    void release() {
+        for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
+                          &seg, &core, &parent, &lab, &is_root, &rank, &misc})
+            b->release();
+    }
+};
+
+struct FitStats {
+    int64_t n = 0, nf = 0, ncells = 0, ncore = 0, nclusters = 0, nx = 0, ny = 0, bits = 0,
+            grid_mode = 0;
+};
+
+// One fit.  Full fits (zone == nullptr) write cluster/flag in input order and return the
+// cluster count; slab fits (zone != nullptr) write core_out/root_out/bmin_out.
+struct FitArgs {
+    const double* x;
+    const double* y;
+    const uint8_t* zone;
+    int64_t n;
+    double eps;
+    int32_t min_points;
+    int32_t mode;
+    int32_t* cluster;
+    uint8_t* flag;
+    uint8_t* core_out;
+    int32_t* root_out;
+    int32_t* bmin_out;
+};
+
+int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st);
+
+// ---- primitives (primitives.hip) ----
+// Exclusive scan of int32 values produced by `mode`:
+//   0: in = const int32_t* values
+//   1: in = const uint8_t* flags (0/1)
+//   2: head flags of a sorted u32 key array: v[i] = (i == 0 || key[i] != key[i-1])
+// Writes out[0..n) and, if total_dev != nullptr, the total at *total_dev.
+void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
+                    int32_t* total_dev, DevBuf& tmp);
+
+// LSD radix sort of (key, val) pairs on the low `bits` bits; results end in key/val
+// (ping-pong through key2/val2).  Stable.
+void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
+                      int32_t*& val2, int64_t n, int bits, DevBuf& hist, DevBuf& scan_tmp,
+                      Profiler* prof);
+
+// Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
+void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
+                 DevBuf& tmp);
+
+}  // namespace dbscan

@@ -1,0 +1,382 @@
+// primitives.hip -- hand-written device-wide primitives for the fit pipeline (gfx950).
+//
+//   exclusive_scan     reduce-then-scan over 4096-element tiles (256 threads x 16 rounds),
+//                      wave64 shuffle scans, recursive over the tile sums
+//   radix_sort_pairs   stable LSD radix sort, 8-bit digits, 4096-key tiles:
+//                      upsweep (per-wave LDS histograms) -> scan -> downsweep that ranks keys
+//                      with 64-bit wave ballots (match-any over the 8 digit bits), scans the
+//                      per-(round,wave,digit) counts in LDS, sorts the tile in LDS and writes
+//                      each digit run contiguously (coalesced) to its global offset
+//   bbox_finite        min/max of finite coordinates + finite count (grid sizing)
+#include "internal.h"
+
+#include <cmath>
+#include <cstdio>
+
+namespace dbscan {
+
+namespace {
+
+constexpr int kItems = 16;                  // rounds per tile
+constexpr int kTile = kBlock * kItems;      // 4096
+constexpr int kWaves = kBlock / 64;         // 4
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int MODE>
+__device__ __forceinline__ int scan_value(const void* in, int64_t i, int64_t n) {
+    if (i >= n) return 0;
+    if constexpr (MODE == 0) {
+        return static_cast<const int32_t*>(in)[i];
+    } else if constexpr (MODE == 1) {
+        return static_cast<const uint8_t*>(in)[i] ? 1 : 0;
+    } else {
+        const uint32_t* k = static_cast<const uint32_t*>(in);
+        return (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const void* in, int64_t n,
+                                                             int32_t* partial) {
+    __shared__ int ws[kWaves];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    int acc = 0;
+#pragma unroll 4
+    for (int r = 0; r < kItems; ++r) acc += scan_value<MODE>(in, base + r * kBlock + threadIdx.x, n);
+    acc = wave_sum(acc);
+    if (lane_id() == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int w = 0; w < kWaves; ++w) s += ws[w];
+        partial[blockIdx.x] = s;
+    }
+}
+
+// Exclusive scan of one tile per block, offset by the scanned tile sums (or 0).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void scan_down_kernel(const void* in, int64_t n,
+                                                           const int32_t* tile_offset,
+                                                           int32_t* out, int32_t* total) {
+    __shared__ int ws[2][kWaves];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    int carry = tile_offset ? tile_offset[blockIdx.x] : 0;
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + r * kBlock + threadIdx.x;
+        const int v = scan_value<MODE>(in, i, n);
+        const int incl = wave_incl_scan(v);
+        if (lane == 63) ws[r & 1][w] = incl;
+        __syncthreads();
+        int woff = 0, btot = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) {
+            const int t = ws[r & 1][k];
+            woff += (k < w) ? t : 0;
+            btot += t;
+        }
+        if (i < n) out[i] = carry + woff + incl - v;
+        carry += btot;
+    }
+    if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = carry;
+}
+
+template <int MODE>
+__global__ void scan_total_kernel(const void* in, const int32_t* out, int64_t n, int32_t* tot) {
+    *tot = out[n - 1] + scan_value<MODE>(in, n - 1, n);
+}
+
+template <int MODE>
+void scan_impl(hipStream_t s, const void* in, int32_t* out, int64_t n, int32_t* total_dev,
+               int32_t* tmp, size_t tmp_elems) {
+    const int64_t nb = (n + kTile - 1) / kTile;
+    if (nb <= 1) {
+        hipLaunchKernelGGL(scan_down_kernel<MODE>, dim3(1), dim3(kBlock), 0, s, in, n, nullptr,
+                           out, total_dev);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    if ((size_t)nb > tmp_elems) throw ArgError{"scan workspace too small"};
+    int32_t* partial = tmp;
+    hipLaunchKernelGGL(scan_reduce_kernel<MODE>, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n,
+                       partial);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    // exclusive scan of the tile sums in place (recursion on a smaller problem)
+    scan_impl<0>(s, partial, partial, nb, nullptr, tmp + nb, tmp_elems - (size_t)nb);
+    hipLaunchKernelGGL(scan_down_kernel<MODE>, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n,
+                       partial, out, nullptr);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    if (total_dev) {
+        // total = last exclusive value + last input value
+        hipLaunchKernelGGL(scan_total_kernel<MODE>, dim3(1), dim3(1), 0, s, in, out, n,
+                           total_dev);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+}
+
+size_t scan_tmp_elems(int64_t n) {
+    size_t need = 0;
+    int64_t m = n;
+    while (m > kTile) {
+        m = (m + kTile - 1) / kTile;
+        need += (size_t)m;
+    }
+    return need + 16;
+}
+
+// ------------------------------------ radix sort ------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* __restrict__ key,
+                                                               int64_t n, int shift,
+                                                               int64_t nblocks,
+                                                               int32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kWaves][256];
+    const int w = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < kWaves * 256; d += kBlock) (&h[0][0])[d] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll 4
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + r * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[w][(key[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const int d = threadIdx.x;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) c += h[k][d];
+    hist[(int64_t)d * nblocks + blockIdx.x] = (int32_t)c;
+}
+
+struct DownsweepSmem {
+    uint16_t wcnt[kItems * kWaves][256];  // per (round, wave) digit counts -> prefixes
+    uint32_t keys[kTile];
+    int32_t vals[kTile];
+    int32_t tile_start[256];
+    int32_t gofs[256];
+    int32_t wsum[kWaves];
+};
+
+__global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
+    uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, int64_t n, int shift,
+    int64_t nblocks, const int32_t* __restrict__ hist_scanned) {
+    __shared__ DownsweepSmem sm;
+    const int t = threadIdx.x, w = t >> 6, lane = lane_id();
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+
+    {  // zero the count table (32 KB): 8 x 16 B per thread
+        uint4* z = reinterpret_cast<uint4*>(&sm.wcnt[0][0]);
+        for (int k = t; k < (int)(sizeof(sm.wcnt) / 16); k += kBlock) z[k] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+
+    uint32_t k_r[kItems];
+    int32_t v_r[kItems];
+    uint32_t dr[kItems];  // digit | (rank_in_wave << 16); digit 256 = invalid
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + r * kBlock + t;
+        const bool valid = i < n;
+        const uint32_t k = valid ? key[i] : kSentinelKey;
+        const int32_t v = valid ? val[i] : 0;
+        const uint32_t d = (k >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rk = (uint32_t)__popcll(peers & lt_mask);
+        if (valid && rk == 0) sm.wcnt[r * kWaves + w][d] = (uint16_t)__popcll(peers);
+        k_r[r] = k;
+        v_r[r] = v;
+        dr[r] = valid ? (d | (rk << 16)) : 256u;
+    }
+    __syncthreads();
+    {  // per digit: exclusive prefix over (round, wave) slots in tile order
+        int running = 0;
+        for (int sidx = 0; sidx < kItems * kWaves; ++sidx) {
+            const int c = sm.wcnt[sidx][t];
+            sm.wcnt[sidx][t] = (uint16_t)running;
+            running += c;
+        }
+        // block exclusive scan of the tile digit counts -> tile_start
+        const int incl = wave_incl_scan(running);
+        if (lane == 63) sm.wsum[w] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int q = 0; q < w; ++q) woff += sm.wsum[q];
+        sm.tile_start[t] = woff + incl - running;
+        sm.gofs[t] = hist_scanned[(int64_t)t * nblocks + blockIdx.x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const uint32_t d = dr[r] & 0xFFFFu;
+        if (d < 256u) {
+            const int lpos = sm.tile_start[d] + sm.wcnt[r * kWaves + w][d] + (int)(dr[r] >> 16);
+            sm.keys[lpos] = k_r[r];
+            sm.vals[lpos] = v_r[r];
+        }
+    }
+    __syncthreads();
+    for (int j = t; j < tile_n; j += kBlock) {
+        const uint32_t k = sm.keys[j];
+        const uint32_t d = (k >> shift) & 255u;
+        const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
+        key_out[g] = k;
+        val_out[g] = sm.vals[j];
+    }
+}
+
+// ------------------------------------ bbox -----------------------------------------------
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __restrict__ x,
+                                                              const double* __restrict__ y,
+                                                              int64_t n, double* partial) {
+    __shared__ double sm[kWaves][5];
+    double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, cnt = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const double a = x[i], b = y[i];
+        if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
+            xmin = fmin(xmin, a);
+            xmax = fmax(xmax, a);
+            ymin = fmin(ymin, b);
+            ymax = fmax(ymax, b);
+            cnt += 1.0;
+        }
+    }
+    xmin = wave_min(xmin);
+    xmax = wave_max(xmax);
+    ymin = wave_min(ymin);
+    ymax = wave_max(ymax);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        sm[w][0] = xmin;
+        sm[w][1] = xmax;
+        sm[w][2] = ymin;
+        sm[w][3] = ymax;
+        sm[w][4] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kWaves; ++k) {
+            sm[0][0] = fmin(sm[0][0], sm[k][0]);
+            sm[0][1] = fmax(sm[0][1], sm[k][1]);
+            sm[0][2] = fmin(sm[0][2], sm[k][2]);
+            sm[0][3] = fmax(sm[0][3], sm[k][3]);
+            sm[0][4] += sm[k][4];
+        }
+        for (int c = 0; c < 5; ++c) partial[blockIdx.x * 5 + c] = sm[0][c];
+    }
+}
+
+__global__ void bbox_final_kernel(const double* partial, int nb, double* out) {
+    if (threadIdx.x != 0) return;
+    double r[5] = {INFINITY, -INFINITY, INFINITY, -INFINITY, 0};
+    for (int b = 0; b < nb; ++b) {
+        r[0] = fmin(r[0], partial[b * 5 + 0]);
+        r[1] = fmax(r[1], partial[b * 5 + 1]);
+        r[2] = fmin(r[2], partial[b * 5 + 2]);
+        r[3] = fmax(r[3], partial[b * 5 + 3]);
+        r[4] += partial[b * 5 + 4];
+    }
+    for (int c = 0; c < 5; ++c) out[c] = r[c];
+}
+
+}  // namespace
+
+void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
+                    int32_t* total_dev, DevBuf& tmp) {
+    if (n <= 0) {
+        if (total_dev) DBSCAN_HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(int32_t), s));
+        return;
+    }
+    const size_t need = scan_tmp_elems(n);
+    int32_t* t = static_cast<int32_t*>(tmp.ensure(need * sizeof(int32_t)));
+    switch (mode) {
+        case 0: scan_impl<0>(s, in, out, n, total_dev, t, need); break;
+        case 1: scan_impl<1>(s, in, out, n, total_dev, t, need); break;
+        default: scan_impl<2>(s, in, out, n, total_dev, t, need); break;
+    }
+}
+
+void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
+                      int32_t*& val2, int64_t n, int bits, DevBuf& hist, DevBuf& scan_tmp,
+                      Profiler* prof) {
+    if (n <= 1 || bits <= 0) return;
+    const int64_t nb = (n + kTile - 1) / kTile;
+    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
+    for (int shift = 0; shift < bits; shift += 8) {
+        {
+            StageTimer st(prof, s, "sort_upsweep");
+            hipLaunchKernelGGL(radix_upsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, key,
+                               n, shift, nb, h);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer st(prof, s, "sort_scan");
+            exclusive_scan(s, 0, h, h, nb * 256, nullptr, scan_tmp);
+        }
+        {
+            StageTimer st(prof, s, "sort_downsweep");
+            hipLaunchKernelGGL(radix_downsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s,
+                               key, val, key2, val2, n, shift, nb, h);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        uint32_t* tk = key;
+        key = key2;
+        key2 = tk;
+        int32_t* tv = val;
+        val = val2;
+        val2 = tv;
+    }
+}
+
+void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
+                 DevBuf& tmp) {
+    int nb = (int)((n + kBlock - 1) / kBlock);
+    if (nb > 1024) nb = 1024;
+    if (nb < 1) nb = 1;
+    double* partial = static_cast<double*>(tmp.ensure((size_t)nb * 5 * sizeof(double)));
+    hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, s, x, y, n, partial);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(64), 0, s, partial, nb, out_dev);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dbscan

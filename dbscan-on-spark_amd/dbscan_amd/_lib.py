@@ -1,0 +1,135 @@
+"""ctypes binding of libdbscan_hip.so (the C-ABI declared in include/dbscan_hip.h).
+
+There is deliberately no CPU fallback: if the HIP library is missing or no GPU is visible the
+calls raise, so a test that passes has run the gfx950 kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libdbscan_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "dbscan_hip.h")
+
+DBSCAN_OK, DBSCAN_EARG, DBSCAN_EHIP, DBSCAN_EOOM = 0, -1, -2, -3
+MODE_NAIVE, MODE_ARCHERY = 0, 1
+
+# (name, restype, argtypes) for every symbol include/dbscan_hip.h declares.
+_vp, _i32, _i64, _d, _u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, \
+    ctypes.c_uint64
+SIGNATURES = [
+    ("dbscan_last_error", ctypes.c_char_p, []),
+    ("dbscan_version", _i32, []),
+    ("dbscan_device_count", _i32, []),
+    ("dbscan_create", _vp, [_i32]),
+    ("dbscan_destroy", None, [_vp]),
+    ("dbscan_fit", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_fit_h", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_fit_device", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_stream", _vp, [_vp]),
+    ("dbscan_last_stats", _i32, [_vp, _vp, _i32]),
+    ("dbscan_profile_enable", _i32, [_vp, _i32]),
+    ("dbscan_profile_reset", _i32, [_vp]),
+    ("dbscan_profile_read", _i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
+    ("dbscan_fit_slab_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp, _vp]),
+    ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class DBSCANError(RuntimeError):
+    pass
+
+
+def _adopt_torch_runtime() -> None:
+    """torch (ROCm wheel) bundles its own libamdhip64.so / libhsa-runtime64.so with the same
+    SONAMEs as /opt/rocm's.  Two HIP runtimes in one process cannot share the GPU, so when torch
+    is importable we load it first: the dynamic linker then binds our DT_NEEDED
+    libamdhip64.so.7 / libhsa-runtime64.so.1 to torch's already-loaded copies."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libdbscan_hip.so (raises if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            _adopt_torch_runtime()
+            if not os.path.exists(LIB_PATH):
+                raise DBSCANError(
+                    f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                    "g.build()'` (hipcc --offload-arch=gfx950)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != DBSCAN_OK:
+        msg = load().dbscan_last_error()
+        raise DBSCANError(f"libdbscan_hip error {rc}: {msg.decode() if msg else ''}")
+
+
+class Handle:
+    """Owns a dbscan_handle (one HIP stream + grow-only device buffers on one GPU)."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        h = L.dbscan_create(int(device))
+        if not h:
+            raise DBSCANError(f"dbscan_create({device}) failed: {L.dbscan_last_error().decode()}")
+        self._h = ctypes.c_void_p(h)
+        self.device = int(device)
+
+    @property
+    def ptr(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            load().dbscan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(load().dbscan_stream(self._h) or 0)
+
+    def stats(self) -> dict:
+        buf = (ctypes.c_int64 * 9)()
+        k = load().dbscan_last_stats(self._h, buf, 9)
+        keys = ["n", "finite", "cells", "core", "clusters", "nx", "ny", "key_bits", "grid_mode"]
+        return {keys[i]: int(buf[i]) for i in range(k)}
+
+    def profile(self, on: bool = True) -> None:
+        check(load().dbscan_profile_enable(self._h, 1 if on else 0))
+
+    def profile_reset(self) -> None:
+        check(load().dbscan_profile_reset(self._h))
+
+    def profile_read(self) -> dict:
+        names = ctypes.create_string_buffer(4096)
+        ms = (ctypes.c_double * 64)()
+        ln = (ctypes.c_int64 * 64)()
+        k = load().dbscan_profile_read(self._h, names, 4096, ms, ln, 64)
+        out, parts = {}, names.raw.split(b"\0")
+        for i in range(k):
+            out[parts[i].decode()] = dict(ms=float(ms[i]), launches=int(ln[i]))
+        return out

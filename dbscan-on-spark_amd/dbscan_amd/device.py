@@ -1,0 +1,61 @@
+"""Device-resident entry points (torch tensors in HBM -> labels in HBM).
+
+torch is plumbing here (allocation, streams); all compute is libdbscan_hip.so."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _p(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def fit_tensors(x: torch.Tensor, y: torch.Tensor, eps: float, min_points: int, mode: int,
+                handle: _lib.Handle, cluster: torch.Tensor = None, flag: torch.Tensor = None):
+    """Fit device float64 tensors; returns (cluster int32, flag uint8, n_clusters).
+
+    The caller's pending torch work on x/y must be complete: we synchronize torch's current
+    stream before handing the pointers to the library's own stream."""
+    assert x.is_cuda and y.is_cuda and x.dtype == torch.float64 and y.dtype == torch.float64
+    assert x.shape == y.shape and x.dim() == 1 and x.is_contiguous() and y.is_contiguous()
+    n = x.numel()
+    if cluster is None:
+        cluster = torch.empty(n, dtype=torch.int32, device=x.device)
+    if flag is None:
+        flag = torch.empty(n, dtype=torch.uint8, device=x.device)
+    torch.cuda.current_stream(x.device).synchronize()
+    k = ctypes.c_int32(0)
+    _lib.check(_lib.load().dbscan_fit_device(handle.ptr, _p(x), _p(y), n, float(eps),
+                                             int(min_points), int(mode), _p(cluster), _p(flag),
+                                             ctypes.byref(k)))
+    return cluster, flag, int(k.value)
+
+
+def generate_blobs(n: int, noise: float, dense: float, seed: int, handle: _lib.Handle,
+                   device=None):
+    """SURVEY §8d generator on the device (no PCIe): returns (x, y) float64 tensors."""
+    dev = device if device is not None else torch.device("cuda", handle.device)
+    x = torch.empty(n, dtype=torch.float64, device=dev)
+    y = torch.empty(n, dtype=torch.float64, device=dev)
+    torch.cuda.current_stream(dev).synchronize()
+    _lib.check(_lib.load().dbscan_generate_blobs_device(handle.ptr, _p(x), _p(y), n,
+                                                        float(noise), float(dense), int(seed)))
+    return x, y
+
+
+def slab_fit(x: torch.Tensor, y: torch.Tensor, zone: torch.Tensor, eps: float, min_points: int,
+             handle: _lib.Handle):
+    """Slab fit for the node path: returns (core uint8, root int32, bmin int32) device tensors."""
+    n = x.numel()
+    core = torch.empty(n, dtype=torch.uint8, device=x.device)
+    root = torch.empty(n, dtype=torch.int32, device=x.device)
+    bmin = torch.empty(n, dtype=torch.int32, device=x.device)
+    torch.cuda.current_stream(x.device).synchronize()
+    _lib.check(_lib.load().dbscan_fit_slab_device(handle.ptr, _p(x), _p(y), _p(zone), n,
+                                                  float(eps), int(min_points), _p(core),
+                                                  _p(root), _p(bmin)))
+    return core, root, bmin

@@ -1,0 +1,142 @@
+"""Host-side mirror of the reference's local-fit interface, backed by libdbscan_hip.so.
+
+Mirrors (src/main/scala/org/apache/spark/mllib/clustering/dbscan/):
+  DBSCANPoint              DBSCANPoint.scala:21-32   (x = vector(0), y = vector(1), distanceSquared)
+  DBSCANLabeledPoint/Flag  DBSCANLabeledPoint.scala:24-47 (Unknown = 0, Flag ordinals, toString)
+  LocalDBSCANNaive         LocalDBSCANNaive.scala:31-120  (fit in input order, Naive noise rule)
+  LocalDBSCANArchery       LocalDBSCANArchery.scala:32-126 (fit, Noise re-claimed as Border)
+Same names, argument meaning and error behaviour: a vector with fewer than two coordinates
+raises IndexError (the reference throws IndexOutOfBounds from vector(1)); `fit` never raises on
+valid input and returns fresh labeled points in input order with visited = True.
+Everything is computed by the gfx950 kernels; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+
+Unknown = 0  # DBSCANLabeledPoint.scala:26
+
+
+class Flag(enum.IntEnum):  # DBSCANLabeledPoint.scala:28-31
+    Border = 0
+    Core = 1
+    Noise = 2
+    NotFlagged = 3
+
+
+class DBSCANPoint:
+    """case class DBSCANPoint(vector: Vector) -- equality/hash on the whole vector."""
+
+    __slots__ = ("vector",)
+
+    def __init__(self, vector: Sequence[float]):
+        self.vector = tuple(float(v) for v in vector)
+
+    @property
+    def x(self) -> float:
+        return self.vector[0]
+
+    @property
+    def y(self) -> float:
+        return self.vector[1]
+
+    def distanceSquared(self, other: "DBSCANPoint") -> float:  # DBSCANPoint.scala:26-30
+        dx = other.x - self.x
+        dy = other.y - self.y
+        return (dx * dx) + (dy * dy)
+
+    def __eq__(self, other):
+        return isinstance(other, DBSCANPoint) and self.vector == other.vector
+
+    def __hash__(self):
+        return hash(self.vector)
+
+    def __repr__(self):
+        return f"DBSCANPoint([{','.join(repr(v) for v in self.vector)}])"
+
+
+class DBSCANLabeledPoint(DBSCANPoint):
+    __slots__ = ("flag", "cluster", "visited")
+
+    def __init__(self, vector: Sequence[float]):
+        super().__init__(vector.vector if isinstance(vector, DBSCANPoint) else vector)
+        self.flag = Flag.NotFlagged
+        self.cluster = Unknown
+        self.visited = False
+
+    def __str__(self):  # DBSCANLabeledPoint.scala:43-45: s"$vector,$cluster,$flag"
+        return f"[{','.join(repr(v) for v in self.vector)}],{self.cluster},{self.flag.name}"
+
+
+_tls_handles = {}
+
+
+def default_handle(device: int = 0) -> _lib.Handle:
+    h = _tls_handles.get(device)
+    if h is None:
+        h = _lib.Handle(device)
+        _tls_handles[device] = h
+    return h
+
+
+def fit_arrays(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
+               handle: Optional[_lib.Handle] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Fit host arrays (input order = visit order). Returns (cluster int32, flag uint8, k)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    if x.shape != y.shape or x.ndim != 1:
+        raise ValueError("x and y must be 1-D arrays of equal length")
+    n = x.size
+    cl = np.zeros(n, np.int32)
+    fl = np.zeros(n, np.uint8)
+    k = ctypes.c_int32(0)
+    h = handle or default_handle()
+    _lib.check(_lib.load().dbscan_fit_h(
+        h.ptr, x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p), n,
+        float(eps), int(min_points), int(mode), cl.ctypes.data_as(ctypes.c_void_p),
+        fl.ctypes.data_as(ctypes.c_void_p), ctypes.byref(k)))
+    return cl, fl, int(k.value)
+
+
+class _LocalDBSCAN:
+    _mode = _lib.MODE_NAIVE
+
+    def __init__(self, eps: float, minPoints: int, handle: Optional[_lib.Handle] = None):
+        self.eps = float(eps)
+        self.minPoints = int(minPoints)
+        self.minDistanceSquared = self.eps * self.eps  # LocalDBSCANNaive.scala:33
+        self._handle = handle
+
+    def fit(self, points: Iterable[DBSCANPoint]) -> List[DBSCANLabeledPoint]:
+        pts = list(points)
+        vecs = [p.vector if isinstance(p, DBSCANPoint) else tuple(p) for p in pts]
+        x = np.fromiter((v[0] for v in vecs), np.float64, len(vecs))
+        y = np.fromiter((v[1] for v in vecs), np.float64, len(vecs))  # IndexError if < 2 dims
+        cl, fl, _ = fit_arrays(x, y, self.eps, self.minPoints, self._mode, self._handle)
+        out = []
+        for v, c, f in zip(vecs, cl.tolist(), fl.tolist()):
+            lp = DBSCANLabeledPoint(v)
+            lp.cluster = c
+            lp.flag = Flag(f)
+            lp.visited = True
+            out.append(lp)
+        return out
+
+
+class LocalDBSCANNaive(_LocalDBSCAN):
+    """LocalDBSCANNaive(eps, minPoints).fit(points) -- the one DBSCAN.train uses."""
+
+    _mode = _lib.MODE_NAIVE
+
+
+class LocalDBSCANArchery(_LocalDBSCAN):
+    """LocalDBSCANArchery(eps, minPoints).fit(points).  Visit order = input order (archery's
+    R-tree entry order is not reproducible; its labels match up to permutation)."""
+
+    _mode = _lib.MODE_ARCHERY

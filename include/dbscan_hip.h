@@ -1,0 +1,135 @@
+/*
+ * dbscan_hip.h -- C-ABI of libdbscan_hip.so, the MI355X (gfx950) local DBSCAN fit.
+ *
+ * The reference has no FFI: its seam is the Scala expression
+ *     new LocalDBSCANNaive(eps, minPoints).fit(points)           DBSCAN.scala:153-154
+ * with  fit(points: Iterable[DBSCANPoint]): Iterable[DBSCANLabeledPoint]
+ *                                                                 LocalDBSCANNaive.scala:37
+ * and its variant LocalDBSCANArchery(eps, minPoints).fit          LocalDBSCANArchery.scala:36
+ * (paths relative to src/main/scala/org/apache/spark/mllib/clustering/dbscan/).  Every entry
+ * point below is what a JNI binding of that seam binds (INTEGRATION.md shows the JNI stub and
+ * the Scala `LocalDBSCANHip` wrapper).  Plain pointers and sizes only; no torch types.
+ *
+ * Semantics (bit-exact with the reference for mode NAIVE, visit order = array order):
+ *   neighbour(p, o)  <=>  dx = o.x - p.x; dy = o.y - p.y; dx*dx + dy*dy <= eps*eps   in fp64,
+ *                        never fused into FMA                       DBSCANPoint.scala:26-30,
+ *                                                                   LocalDBSCANNaive.scala:33,77
+ *   |N(p)| counts p itself; core <=> |N(p)| >= min_points          LocalDBSCANNaive.scala:54,101
+ *   clusters are numbered 1..k in the order the reference's outer loop would open them
+ *   (rank of the smallest core index of each core-core component)  LocalDBSCANNaive.scala:45-64
+ *   NAIVE:   a non-core point is Border of the first-opened adjacent cluster if that cluster
+ *            opens before the point's own index, else Noise           LocalDBSCANNaive.scala:94
+ *   ARCHERY: a non-core point with any core neighbour is Border of the first-opened adjacent
+ *            cluster (Noise re-claimed)                              LocalDBSCANArchery.scala:103-106
+ *            (archery visits in R-tree entry order; callers pass the order they want as the
+ *            array order -- raw archery numbering is not reproducible)
+ * Outputs are in INPUT order: cluster (0 = Unknown/Noise) and flag (Flag ordinals below).
+ * Non-finite coordinates are never anyone's neighbour (not even their own) while eps*eps is
+ * finite; eps*eps = +inf makes every pair whose d2 is not NaN a neighbour (all-pairs, O(n^2));
+ * eps*eps = NaN has no pairs.
+ */
+#ifndef DBSCAN_HIP_H
+#define DBSCAN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* DBSCANLabeledPoint.Flag ordinals, DBSCANLabeledPoint.scala:28-31 */
+#define DBSCAN_FLAG_BORDER 0
+#define DBSCAN_FLAG_CORE 1
+#define DBSCAN_FLAG_NOISE 2
+#define DBSCAN_FLAG_NOT_FLAGGED 3
+
+#define DBSCAN_MODE_NAIVE 0   /* LocalDBSCANNaive   (used by DBSCAN.train, DBSCAN.scala:154) */
+#define DBSCAN_MODE_ARCHERY 1 /* LocalDBSCANArchery (LocalDBSCANArcherySuite)               */
+
+/* return codes */
+#define DBSCAN_OK 0
+#define DBSCAN_EARG (-1) /* bad argument: n < 0, n > DBSCAN_MAX_POINTS, NULL pointer, bad mode */
+#define DBSCAN_EHIP (-2) /* HIP runtime error (details in dbscan_last_error) */
+#define DBSCAN_EOOM (-3) /* device allocation failed */
+
+#define DBSCAN_MAX_POINTS 2147483000LL /* int32 point indices on device */
+
+typedef struct dbscan_handle dbscan_handle;
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* dbscan_last_error(void);
+/* ABI version (major*100 + minor). */
+int32_t dbscan_version(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int32_t dbscan_device_count(void);
+
+/* A handle owns one HIP stream and grow-only device work buffers on `device`; one handle per
+ * thread (Spark local[N] runs N concurrent fits).  NULL on failure (see dbscan_last_error). */
+dbscan_handle* dbscan_create(int32_t device);
+void dbscan_destroy(dbscan_handle* h);
+
+/* Host arrays in, host arrays out (input order).  Replaces LocalDBSCANNaive.fit /
+ * LocalDBSCANArchery.fit (LocalDBSCANNaive.scala:37, LocalDBSCANArchery.scala:36).
+ * n == 0 returns DBSCAN_OK with *n_clusters_out = 0.  The handle-less form uses a
+ * thread-local handle on device 0. */
+int32_t dbscan_fit(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
+                   int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                   int32_t* n_clusters_out);
+int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t n, double eps,
+                     int32_t min_points, int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                     int32_t* n_clusters_out);
+
+/* Device-resident form: d_x, d_y, d_cluster, d_flag are device pointers on the handle's
+ * device.  All work is enqueued on the handle's stream; the call returns after the stream has
+ * drained (the cluster count is read back).  This is the form bench.py times. */
+int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
+                          double eps, int32_t min_points, int32_t mode, int32_t* d_cluster,
+                          uint8_t* d_flag, int32_t* n_clusters_out);
+
+/* The handle's hipStream_t (as void*), for callers that order their own work around it. */
+void* dbscan_stream(dbscan_handle* h);
+
+/* Statistics of the handle's last fit:
+ *   [0] n  [1] finite points in the grid  [2] occupied cells  [3] core points
+ *   [4] clusters  [5] grid nx  [6] grid ny  [7] radix key bits  [8] grid mode
+ *   (0 = eps grid, 1 = all pairs, 2 = no pairs)                                */
+int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max);
+
+/* Per-kernel timing with HIP events on the handle's stream.  When enabled, every pipeline
+ * stage of each fit is bracketed by events; read accumulates (name, total ms, launches).
+ * `names` receives NUL-separated stage names.  Returns the number of stages written. */
+int32_t dbscan_profile_enable(dbscan_handle* h, int32_t on);
+int32_t dbscan_profile_reset(dbscan_handle* h);
+int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, double* total_ms,
+                            int64_t* launches, int32_t max);
+
+/* ---------------------------------------------------------------------------------------
+ * Slab fit for the multi-GPU node path.  The caller passes the points of one
+ * spatial slab grown by 2*eps halos, in increasing global visit order, with a zone per point:
+ *   0 = owned (inside this rank's main slab), 1 = inner halo (within eps of the slab),
+ *   2 = outer halo (only used as neighbour-count candidates).
+ * Counts are exact for zones 0 and 1.  The slab fit then unions core-core edges among zone
+ * 0/1 points and returns, per point, in slab order:
+ *   d_core[i]   1 if core (zones 0/1), else 0
+ *   d_root[i]   cores: slab index of the minimum-index core of the point's local component;
+ *               non-cores: -1
+ *   d_bmin[i]   zone-0 non-cores: slab index of the smallest root among adjacent cores'
+ *               components (or -1); others -1
+ * Global merge and relabel happen above this call (dbscan_amd/node.py, RCCL all-gather). */
+int32_t dbscan_fit_slab_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                               const uint8_t* d_zone, int64_t n, double eps,
+                               int32_t min_points, uint8_t* d_core, int32_t* d_root,
+                               int32_t* d_bmin);
+
+/* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
+ * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the
+ * visit order.  Writes d_x, d_y (device).  Used by bench.py so 10^7..10^9 points need no PCIe. */
+int32_t dbscan_generate_blobs_device(dbscan_handle* h, double* d_x, double* d_y, int64_t n,
+                                     double noise_frac, double dense, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DBSCAN_HIP_H */

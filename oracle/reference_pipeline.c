@@ -355,29 +355,93 @@ static void* fit_worker(void* arg) {
     return NULL;
 }
 
+static int cmp_i64(const void* a, const void* b) {
+    int64_t u = *(const int64_t*)a, v = *(const int64_t*)b;
+    return (u > v) - (u < v);
+}
+
 static void collect_members(fit_ctx* f) {
-    /* DBSCAN.scala:132-137: (id, point) for every margin whose outer contains the point */
-    f->members = (int64_t**)calloc((size_t)(f->nparts > 0 ? f->nparts : 1), sizeof(int64_t*));
-    f->msize = (int64_t*)calloc((size_t)(f->nparts > 0 ? f->nparts : 1), sizeof(int64_t));
-    int64_t* mcap = (int64_t*)calloc((size_t)(f->nparts > 0 ? f->nparts : 1), sizeof(int64_t));
-    for (int64_t i = 0; i < f->n; ++i)
-        for (int64_t p = 0; p < f->nparts; ++p) {
-            double outer[4];
-            shrink(&f->rects[4 * p], -f->eps, outer);
-            if (!rect_contains_pt(outer, f->x[i], f->y[i])) continue;
-            if (f->msize[p] == mcap[p]) {
-                mcap[p] = mcap[p] ? 2 * mcap[p] : 64;
-                f->members[p] = (int64_t*)realloc(f->members[p], sizeof(int64_t) * (size_t)mcap[p]);
-            }
-            f->members[p][f->msize[p]++] = i;
-        }
-    free(mcap);
-    f->cl = (int32_t**)calloc((size_t)(f->nparts > 0 ? f->nparts : 1), sizeof(int32_t*));
-    f->fl = (uint8_t**)calloc((size_t)(f->nparts > 0 ? f->nparts : 1), sizeof(uint8_t*));
-    for (int64_t p = 0; p < f->nparts; ++p) {
-        f->cl[p] = (int32_t*)malloc(sizeof(int32_t) * (size_t)(f->msize[p] + 1));
-        f->fl[p] = (uint8_t*)malloc((size_t)(f->msize[p] + 1));
+    /* DBSCAN.scala:132-137: (id, point) for every margin whose outer contains the point.
+     * Points are bucketed on the 2*eps cell grid (DBSCAN.scala:345-356) so each outer
+     * rectangle only tests points of the cells it overlaps (+1 cell of slack); membership is
+     * still decided by the exact inclusive contains (DBSCANRectangle.scala:34-37). */
+    const int64_t np = f->nparts > 0 ? f->nparts : 1;
+    f->members = (int64_t**)calloc((size_t)np, sizeof(int64_t*));
+    f->msize = (int64_t*)calloc((size_t)np, sizeof(int64_t));
+    f->cl = (int32_t**)calloc((size_t)np, sizeof(int32_t*));
+    f->fl = (uint8_t**)calloc((size_t)np, sizeof(uint8_t*));
+    const double mrs = 2 * f->eps;
+    int64_t n = f->n;
+    int64_t* ci = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t* cj = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t imin = INT64_MAX, imax = INT64_MIN, jmin = INT64_MAX, jmax = INT64_MIN;
+    for (int64_t p = 0; p < n; ++p) {
+        ci[p] = corner_index(f->x[p], mrs);
+        cj[p] = corner_index(f->y[p], mrs);
+        if (ci[p] < imin) imin = ci[p];
+        if (ci[p] > imax) imax = ci[p];
+        if (cj[p] < jmin) jmin = cj[p];
+        if (cj[p] > jmax) jmax = cj[p];
     }
+    int64_t W = n ? imax - imin + 1 : 1, H = n ? jmax - jmin + 1 : 1;
+    int dense = (double)W * (double)H <= 4e8;
+    int64_t* start = NULL;
+    int64_t* order = NULL;
+    if (dense && n) { /* counting sort of points by cell, stable (input order inside a cell) */
+        start = (int64_t*)calloc((size_t)(W * H + 1), sizeof(int64_t));
+        order = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+        for (int64_t p = 0; p < n; ++p) start[(cj[p] - jmin) * W + (ci[p] - imin) + 1]++;
+        for (int64_t c = 0; c < W * H; ++c) start[c + 1] += start[c];
+        int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(W * H));
+        memcpy(cur, start, sizeof(int64_t) * (size_t)(W * H));
+        for (int64_t p = 0; p < n; ++p) order[cur[(cj[p] - jmin) * W + (ci[p] - imin)]++] = p;
+        free(cur);
+    }
+    for (int64_t q = 0; q < f->nparts; ++q) {
+        double outer[4];
+        shrink(&f->rects[4 * q], -f->eps, outer);
+        int64_t cap = 0, m = 0;
+        int64_t* mem = NULL;
+        if (dense) {
+            int64_t i0 = corner_index(outer[0], mrs) - 1, i1 = corner_index(outer[2], mrs) + 1;
+            int64_t j0 = corner_index(outer[1], mrs) - 1, j1 = corner_index(outer[3], mrs) + 1;
+            if (i0 < imin) i0 = imin;
+            if (j0 < jmin) j0 = jmin;
+            if (i1 > imax) i1 = imax;
+            if (j1 > jmax) j1 = jmax;
+            for (int64_t j = j0; j <= j1; ++j)
+                for (int64_t i = i0; i <= i1; ++i) {
+                    int64_t c = (j - jmin) * W + (i - imin);
+                    for (int64_t t = start[c]; t < start[c + 1]; ++t) {
+                        int64_t p = order[t];
+                        if (!rect_contains_pt(outer, f->x[p], f->y[p])) continue;
+                        if (m == cap) {
+                            cap = cap ? 2 * cap : 64;
+                            mem = (int64_t*)realloc(mem, sizeof(int64_t) * (size_t)cap);
+                        }
+                        mem[m++] = p;
+                    }
+                }
+            qsort(mem, (size_t)m, sizeof(int64_t), cmp_i64); /* groupByKey order = input order */
+        } else {
+            for (int64_t p = 0; p < n; ++p) {
+                if (!rect_contains_pt(outer, f->x[p], f->y[p])) continue;
+                if (m == cap) {
+                    cap = cap ? 2 * cap : 64;
+                    mem = (int64_t*)realloc(mem, sizeof(int64_t) * (size_t)cap);
+                }
+                mem[m++] = p;
+            }
+        }
+        f->members[q] = mem;
+        f->msize[q] = m;
+        f->cl[q] = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m + 1));
+        f->fl[q] = (uint8_t*)malloc((size_t)(m + 1));
+    }
+    free(start);
+    free(order);
+    free(ci);
+    free(cj);
 }
 
 static void free_fit(fit_ctx* f) {

@@ -1,0 +1,99 @@
+"""CPU tests of the drop-in boundary: libdbscan_hip.so builds for gfx950, loads, exports every
+symbol include/dbscan_hip.h declares with the documented error behaviour -- no compute calls
+(there is no GPU here; the parity tests are in test_gpu_parity.py)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+import dbscan_amd
+from dbscan_amd import _lib
+
+
+def _header_symbols():
+    with open(_lib.HEADER_PATH) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dbscan_[a-z_]+)\s*\(", text)))
+
+
+def test_library_built_for_gfx950():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    text = out.stdout + out.stderr
+    if "gfx950" not in text:  # older objdump: look for the code object triple in the binary
+        with open(_lib.LIB_PATH, "rb") as f:
+            assert b"gfx950" in f.read()
+
+
+def test_exports_every_declared_symbol():
+    syms = _header_symbols()
+    assert len(syms) >= 14
+    L = _lib.load()
+    for s in syms:
+        assert hasattr(L, s), s
+    declared = {name for name, _, _ in _lib.SIGNATURES}
+    assert declared == set(syms), set(syms) ^ declared
+
+
+def test_nm_exports_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dbscan_[a-z_]+)\b", out))
+    assert set(_header_symbols()) <= exported
+
+
+def test_version_and_device_count_without_gpu():
+    L = _lib.load()
+    assert L.dbscan_version() == 100
+    assert L.dbscan_device_count() >= 0
+
+
+def test_null_handle_errors():
+    L = _lib.load()
+    k = ctypes.c_int32(0)
+    rc = L.dbscan_fit_h(None, None, None, 0, 0.3, 10, 0, None, None, ctypes.byref(k))
+    assert rc == _lib.DBSCAN_EARG
+    assert b"NULL handle" in L.dbscan_last_error()
+    rc = L.dbscan_fit_device(None, None, None, 0, 0.3, 10, 0, None, None, None)
+    assert rc == _lib.DBSCAN_EARG
+    assert L.dbscan_last_stats(None, None, 0) == _lib.DBSCAN_EARG
+
+
+@pytest.mark.skipif(_lib.load().dbscan_device_count() > 0, reason="GPU present")
+def test_create_without_gpu_fails_loudly():
+    L = _lib.load()
+    assert not L.dbscan_create(0)
+    assert L.dbscan_last_error()
+    with pytest.raises(dbscan_amd.DBSCANError):
+        dbscan_amd.fit_arrays([0.0], [0.0], 0.3, 1)
+
+
+def test_reference_interface_shapes():
+    from dbscan_amd import DBSCANLabeledPoint, DBSCANPoint, Flag, LocalDBSCANNaive
+
+    assert [f.value for f in Flag] == [0, 1, 2, 3]  # DBSCANLabeledPoint.scala:30
+    p, q = DBSCANPoint([0.0, 0.0, 1.0]), DBSCANPoint([0.3, 0.4])
+    assert q.distanceSquared(p) == 0.3 * 0.3 + 0.4 * 0.4
+    lp = DBSCANLabeledPoint(p)
+    assert (lp.flag, lp.cluster, lp.visited) == (Flag.NotFlagged, 0, False)
+    assert str(lp) == "[0.0,0.0,1.0],0,NotFlagged"
+    assert LocalDBSCANNaive(0.3, 10).minDistanceSquared == 0.3 * 0.3
+
+
+def test_cpp_mirror_compiles_against_the_library(tmp_path):
+    """include/dbscan_local.hpp (the C++ host mirror of the reference interface) compiles and
+    links against libdbscan_hip.so with plain g++ (no HIP headers needed by callers)."""
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "dbscan_local.hpp"\nint main(){ dbscan::LocalDBSCANNaive f(0.3, 10);'
+                   ' (void)f; return dbscan_version() == 100 ? 0 : 1; }\n')
+    exe = tmp_path / "t"
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                    str(exe), "-L", libdir, "-ldbscan_hip", f"-Wl,-rpath,{libdir}"], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0
