@@ -29,6 +29,8 @@
 #include "internal.h"
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace dbscan {
@@ -38,6 +40,7 @@ enum GridMode { kGridEps = 0, kGridAllPairs = 1, kGridNoPairs = 2 };
 struct GridParams {
     double xmin2, ymin2, invx, invy;  // cell = floor((v*0.5 - vmin*0.5) * inv)
     uint32_t nx, ny;
+    int clique;  // cell side <= eps*(1+2^-14): quarter cells are cliques of the predicate
 };
 
 namespace {
@@ -90,11 +93,15 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
     const double a = x[i], b = y[i];
     uint32_t k = kSentinelKey;
     if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
-        double fx = floor((a * 0.5 - g.xmin2) * g.invx);
-        double fy = floor((b * 0.5 - g.ymin2) * g.invy);
-        fx = fx < 0 ? 0 : (fx > (double)(g.nx - 1) ? (double)(g.nx - 1) : fx);
-        fy = fy < 0 ? 0 : (fy > (double)(g.ny - 1) ? (double)(g.ny - 1) : fy);
-        k = (uint32_t)((uint64_t)fy * g.nx + (uint64_t)fx);
+        // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
+        double fx = floor(2.0 * ((a * 0.5 - g.xmin2) * g.invx));
+        double fy = floor(2.0 * ((b * 0.5 - g.ymin2) * g.invy));
+        const double mx = 2.0 * (double)g.nx - 1.0, my = 2.0 * (double)g.ny - 1.0;
+        fx = fx < 0 ? 0 : (fx > mx ? mx : fx);
+        fy = fy < 0 ? 0 : (fy > my ? my : fy);
+        const uint32_t qx = (uint32_t)fx, qy = (uint32_t)fy;
+        const uint64_t cellk = (uint64_t)(qy >> 1) * g.nx + (qx >> 1);
+        k = (uint32_t)((cellk << 2) | ((qy & 1u) << 1) | (qx & 1u));
     }
     key[i] = k;
     perm[i] = (int32_t)i;
@@ -119,9 +126,11 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
     xy[p] = make_double2(x[o], y[o]);
 }
 
-// cell[p] holds the exclusive scan of head flags on entry; converted to the cell index.
+// cell[p] holds the exclusive scan of head flags on entry; converted to the group index.
+// shift = 2: eps cells (key >> 2); shift = 0: quarter cells (full key).
 __global__ __launch_bounds__(kBlock) void cells_kernel(const uint32_t* __restrict__ key,
-                                                       int64_t nf, int32_t* __restrict__ cell,
+                                                       int shift, int64_t nf,
+                                                       int32_t* __restrict__ cell,
                                                        uint32_t* __restrict__ ckey,
                                                        int32_t* __restrict__ cstart,
                                                        const int32_t* __restrict__ ncells) {
@@ -131,9 +140,9 @@ __global__ __launch_bounds__(kBlock) void cells_kernel(const uint32_t* __restric
         return;
     }
     const int32_t ex = cell[p];
-    const bool head = (p == 0) || key[p] != key[p - 1];
+    const bool head = (p == 0) || (key[p] >> shift) != (key[p - 1] >> shift);
     if (head) {
-        ckey[ex] = key[p];
+        ckey[ex] = key[p] >> shift;
         cstart[ex] = (int32_t)p;
     }
     cell[p] = ex + (head ? 1 : 0) - 1;
@@ -197,6 +206,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict
                                                        int32_t min_points,
                                                        const int32_t* __restrict__ perm,
                                                        const uint8_t* __restrict__ zone,
+                                                       const int32_t* __restrict__ qidx,
+                                                       const int32_t* __restrict__ qstart,
                                                        uint8_t* __restrict__ core,
                                                        int32_t* __restrict__ parent,
                                                        int32_t* __restrict__ ncore) {
@@ -211,6 +222,8 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict
         is_core = true;
     } else if (p >= nf) {
         is_core = false;  // outside the grid: no neighbours, not even itself
+    } else if (qidx && qstart[qidx[p] + 1] - qstart[qidx[p]] >= min_points) {
+        is_core = true;  // a clique quarter cell holding >= minPoints points (dense box)
     } else {
         const double2 me = xy[p];
         const Seg s = load_seg(seg, cell[p]);
@@ -234,38 +247,76 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict
 // Loads/stores are agent-scope relaxed atomics (L1-bypassing), hooks are CAS on roots only;
 // stale reads only ever show an older ancestor, which is still an ancestor.
 // ---------------------------------------------------------------------------------------
+// UF variant (template parameter V): 0 = agent-scope atomic loads (L1-bypassing) + path-halving
+// stores; 1 = plain loads, no stores (stale L1 copies are older ancestors: still correct);
+// 2 = atomic loads, no stores.
+__device__ unsigned long long g_uf_stats[8];  // debug variant 3: finds, hops, cas, cas_fail, pairs
+
+template <int V>
 __device__ __forceinline__ int ld_par(int* par, int i) {
-    return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (V == 3) atomicAdd(&g_uf_stats[1], 1ull);
+    if constexpr (V == 1 || V == 4) {
+        return par[i];  // plain (L1-cacheable) load
+    } else {
+        return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
+template <int V>
 __device__ __forceinline__ void st_par(int* par, int i, int v) {
-    __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (V == 4) {
+        par[i] = v;  // plain store: a hint only (any ancestor is a valid parent)
+    } else {
+        __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
+template <int V = 0>
 __device__ int uf_find(int* par, int x) {
-    int cur = ld_par(par, x);
+    if constexpr (V == 3) atomicAdd(&g_uf_stats[0], 1ull);
+    int cur = ld_par<V>(par, x);
     if (cur == x) return x;
     int prev = x;
     for (;;) {
-        const int next = ld_par(par, cur);
+        const int next = ld_par<V>(par, cur);
         if (next == cur) return cur;
-        st_par(par, prev, next);  // path halving (prev is a non-root: only ancestors stored)
+        if constexpr (V == 0 || V == 3 || V == 4) st_par<V>(par, prev, next);  // path halving
+        prev = cur;
+        cur = next;
+    }
+}
+
+// Walk x's chain; stop early (returning `target`) when the walk meets `target`, which then
+// need not be a root any more: the two are in one set.  Avoids re-reading a hot root's line.
+template <int V = 0>
+__device__ int uf_find_until(int* par, int x, int target) {
+    if (x == target) return target;
+    int cur = ld_par<V>(par, x);
+    if (cur == x || cur == target) return cur;
+    int prev = x;
+    for (;;) {
+        const int next = ld_par<V>(par, cur);
+        if (next == cur || next == target) return next;
+        if constexpr (V == 0 || V == 3 || V == 4) st_par<V>(par, prev, next);
         prev = cur;
         cur = next;
     }
 }
 
 // Merge the sets of believed roots ra, rb; returns the believed root of the union.
+template <int V = 0>
 __device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra, int rb) {
     while (ra != rb) {
         const bool swap = prio[ra] < prio[rb];
         const int hi = swap ? rb : ra;  // larger visit index: hooked
         const int lo = swap ? ra : rb;
         int expected = hi;
+        if constexpr (V == 3) atomicAdd(&g_uf_stats[2], 1ull);
         if (__hip_atomic_compare_exchange_strong(par + hi, &expected, lo, __ATOMIC_RELAXED,
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             return lo;
-        ra = uf_find(par, expected);  // hi was hooked meanwhile: continue from its new parent
-        rb = uf_find(par, lo);
+        if constexpr (V == 3) atomicAdd(&g_uf_stats[3], 1ull);
+        ra = uf_find<V>(par, expected);  // hi was hooked meanwhile: continue from its new parent
+        rb = uf_find<V>(par, lo);
     }
     return ra;
 }
@@ -294,6 +345,94 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
         }
         return true;
     });
+}
+
+// ---------------------------------------------------------------------------------------
+// Clique-quarter union (cell side <= eps*(1+2^-14)).  A quarter cell has side ~eps/2 and
+// diagonal ~0.71*eps, so any two of its points satisfy the fp64 predicate: its cores are one
+// connected set without a single distance test.  quarter_init points every core of a quarter at
+// the quarter's minimum-visit-index core (a valid union-find state: pointers go to a smaller
+// visit index); quarter_union then needs ONE core-core edge per pair of quarter cells within
+// reach (offsets <= 2 on the quarter grid, i.e. inside the 3x3 eps-cell stencil), examined once
+// by the later quarter in sorted order, and one union per connected pair.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void quarter_init_kernel(const int32_t* __restrict__ qstart,
+                                                              const int32_t* __restrict__ nq_p,
+                                                              const int32_t* __restrict__ perm,
+                                                              const uint8_t* __restrict__ core,
+                                                              int32_t* __restrict__ qrep,
+                                                              int32_t* __restrict__ parent) {
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= *nq_p) return;
+    const int b = qstart[q], e = qstart[q + 1];
+    int rep = -1, best = 0x7FFFFFFF;
+    for (int j = b; j < e; ++j)
+        if (core[j] && perm[j] < best) {
+            best = perm[j];
+            rep = j;
+        }
+    qrep[q] = rep;
+    if (rep < 0) return;
+    for (int j = b; j < e; ++j)
+        if (core[j]) parent[j] = rep;
+}
+
+__device__ __forceinline__ void quarter_xy(uint32_t key, uint32_t nx, int& gx, int& gy) {
+    const uint32_t ck = key >> 2;
+    const uint32_t cy = ck / nx, cx = ck - cy * nx;
+    gx = (int)(2 * cx + (key & 1u));
+    gy = (int)(2 * cy + ((key >> 1) & 1u));
+}
+
+template <int V>
+__global__ __launch_bounds__(kBlock) void quarter_union_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ qidx,
+    const uint32_t* __restrict__ qkey, const int32_t* __restrict__ qstart,
+    const int32_t* __restrict__ qrep, const int32_t* __restrict__ nq_p, GridParams g,
+    double eps2, const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    int32_t* __restrict__ parent) {
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= *nq_p) return;
+    const int rq = qrep[q];
+    if (rq < 0) return;
+    int gx, gy;
+    quarter_xy(qkey[q], g.nx, gx, gy);
+    const int qs = qstart[q], qe = qstart[q + 1];
+    const Seg s = load_seg(seg, cell[qs]);
+    int rp = uf_find<V>(parent, rq);
+    const int rb[2] = {s.b0, s.b1}, re[2] = {s.e0, s.e1};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {  // rows cy-1 and cy: every quarter there with a smaller key
+        if (rb[r] >= re[r]) continue;
+        const int q_lo = qidx[rb[r]], q_hi = qidx[re[r] - 1];
+        for (int q2 = q_lo; q2 <= q_hi && q2 < q; ++q2) {
+            const int r2 = qrep[q2];
+            if (r2 < 0) continue;
+            int gx2, gy2;
+            quarter_xy(qkey[q2], g.nx, gx2, gy2);
+            if (abs(gx2 - gx) > 2 || abs(gy2 - gy) > 2) continue;
+            int rr = uf_find_until<V>(parent, r2, rp);
+            if (rr == rp) continue;  // already one set: skip the pair test
+            if constexpr (V == 3) atomicAdd(&g_uf_stats[4], 1ull);
+            const int b2 = qstart[q2], e2 = qstart[q2 + 1];
+            bool found = false;
+            for (int a = qs; a < qe && !found; ++a) {
+                if (!core[a]) continue;
+                const double2 pa = xy[a];
+                for (int b = b2; b < e2; ++b) {
+                    if (!core[b]) continue;
+                    const double2 pb = xy[b];
+                    if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) {
+                        found = true;
+                        break;
+                    }
+                }
+            }
+            if (!found) continue;
+            rp = uf_unite_roots<V>(parent, perm, rp, rr);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
@@ -391,14 +530,15 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 
 // Grid sizing on the host (see DESIGN.md "grid soundness"): cell side >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500) bounds |x'-x| for every pair the fp64 predicate accepts;
-// cells per axis <= 2^31 and nx*ny <= 2^31 (u32 keys with a sentinel), growing the side
-// (never shrinking it) when the extent would need more cells.
+// nx*ny <= 2^29 (u32 keys = cell*4 + quadrant, below the sentinel), growing the side (never
+// shrinking it) when the extent would need more cells.  Quarter cells are cliques only while
+// the side was not grown: clique = side <= |eps|*(1+2^-14).
 static bool make_grid(const double bb[5], double eps, GridParams* g) {
     const double xmin = bb[0], xmax = bb[1], ymin = bb[2], ymax = bb[3];
     double R = std::fabs(eps) * (1.0 + 0x1p-40);
     if (R < 0x1p-500) R = 0x1p-500;
     double hx = R * (1.0 + 0x1p-16), hy = hx;
-    const double limit = 2147483648.0;  // 2^31 cells
+    const double limit = 536870912.0;  // 2^29 cells
     auto cells = [](double vmax, double vmin, double h) {
         const double t = (vmax * 0.5 - vmin * 0.5) * (2.0 / h);
         return std::floor(t) + 1.0;  // may be +inf for absurd extents
@@ -412,6 +552,8 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
             g->ymin2 = ymin * 0.5;
             g->nx = (uint32_t)cx;
             g->ny = (uint32_t)cy;
+            const double cl = std::fabs(eps) * (1.0 + 0x1p-14);
+            g->clique = (hx <= cl && hy <= cl) ? 1 : 0;
             return true;
         }
         if (cx >= cy) hx *= 2.0; else hy *= 2.0;
@@ -438,7 +580,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     int32_t* misc_i = reinterpret_cast<int32_t*>(misc + 16);  // [0] ncells, [1] nclusters
 
     DBSCAN_HIP_CHECK(hipMemsetAsync(misc_i, 0, 4 * sizeof(int32_t), s));
-    GridParams g{0, 0, 0, 0, 1, 1};
+    GridParams g{0, 0, 0, 0, 1, 1, 0};
     int64_t nf = 0;
     int bits = 0;
     if (mode == kGridEps) {
@@ -467,9 +609,9 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        const uint64_t cells = (uint64_t)g.nx * g.ny;  // valid keys < cells <= 2^31
+        const uint64_t qcells = 4ull * g.nx * g.ny;  // valid keys < qcells <= 2^31
         bits = 1;
-        while (bits < 32 && (1ull << bits) <= cells) ++bits;  // keys < 2^bits - 1 (sentinel)
+        while (bits < 32 && (1ull << bits) <= qcells) ++bits;  // keys < 2^bits - 1 (sentinel)
         radix_sort_pairs(s, key, perm, key2, perm2, n, bits, ws.hist, ws.scan_tmp, prof);
     } else {
         StageTimer t(prof, s, "bin");
@@ -488,6 +630,17 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
     int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
     int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
+    const bool clique = mode == kGridEps && g.clique;
+    int32_t* qidx = nullptr;
+    uint32_t* qkey = nullptr;
+    int32_t* qstart = nullptr;
+    int32_t* qrep = nullptr;
+    if (clique) {
+        qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
+        qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
+        qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
+        qrep = static_cast<int32_t*>(ws.qrep.ensure(nfa * sizeof(int32_t)));
+    }
 
     if (nf > 0) {
         {
@@ -498,10 +651,16 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "cells");
-            exclusive_scan(s, 2, key, cell, nf, &misc_i[0], ws.scan_tmp);
-            hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, nf,
+            exclusive_scan(s, 3, key, cell, nf, &misc_i[0], ws.scan_tmp);
+            hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 2, nf,
                                cell, ckey, cstart, &misc_i[0]);
             DBSCAN_HIP_CHECK(hipGetLastError());
+            if (clique) {
+                exclusive_scan(s, 2, key, qidx, nf, &misc_i[3], ws.scan_tmp);
+                hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 0,
+                                   nf, qidx, qkey, qstart, &misc_i[3]);
+                DBSCAN_HIP_CHECK(hipGetLastError());
+            }
         }
         {
             StageTimer t(prof, s, "segs");
@@ -513,10 +672,46 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     {
         StageTimer t(prof, s, "count");
         hipLaunchKernelGGL(count_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, n, nf,
-                           eps2, a.min_points, perm, a.zone, core, parent, &misc_i[2]);
+                           eps2, a.min_points, perm, a.zone, qidx, qstart, core, parent,
+                           &misc_i[2]);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
-    if (nf > 0) {
+    if (clique) {
+        {
+            StageTimer t(prof, s, "quarter_init");
+            hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qstart,
+                               &misc_i[3], perm, core, qrep, parent);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        StageTimer t(prof, s, "union");
+        static const int variant = [] {
+            const char* e = getenv("DBSCAN_UF_VARIANT");
+            return e ? atoi(e) : 1;
+        }();
+        auto* kq = variant == 0   ? quarter_union_kernel<0>
+                   : variant == 2 ? quarter_union_kernel<2>
+                   : variant == 3 ? quarter_union_kernel<3>
+                   : variant == 4 ? quarter_union_kernel<4>
+                                  : quarter_union_kernel<1>;
+        if (variant == 3) {
+            unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            DBSCAN_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_uf_stats), z, sizeof(z), 0,
+                                                    hipMemcpyHostToDevice, s));
+        }
+        hipLaunchKernelGGL(kq, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, qidx, qkey,
+                           qstart, qrep, &misc_i[3], g, eps2, perm, core, parent);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+        if (variant == 3) {
+            unsigned long long z[8];
+            int32_t nq = 0;
+            DBSCAN_HIP_CHECK(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_uf_stats), sizeof(z), 0,
+                                                      hipMemcpyDeviceToHost, s));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(&nq, &misc_i[3], 4, hipMemcpyDeviceToHost, s));
+            DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+            fprintf(stderr, "uf stats: quarters=%d finds=%llu hops=%llu cas=%llu cas_fail=%llu "
+                    "pair_tests=%llu\n", nq, z[0], z[1], z[2], z[3], z[4]);
+        }
+    } else if (nf > 0) {
         StageTimer t(prof, s, "union");
         hipLaunchKernelGGL(union_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, nf,
                            eps2, perm, core, parent);

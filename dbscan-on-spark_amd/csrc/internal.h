@@ -7,6 +7,9 @@
 //   cell[nf] i32 occupied-cell index of each sorted slot
 //   ckey[C], cstart[C+1]  occupied cells (sorted keys) and their first slot
 //   seg[C]   int8 (b0,e0,b1,e1,b2,e2,-,-): slot ranges of the 3 rows of the 3x3 stencil
+//   qidx[nf], qkey[Q], qstart[Q+1], qrep[Q]  quarter cells (2x2 per eps cell; key low 2 bits =
+//            quadrant): side ~eps/2, so each is a clique under the exact predicate; qrep =
+//            its minimum-visit-index core (or -1)
 //   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
 //   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
 #pragma once
@@ -83,10 +86,11 @@ struct StageTimer {
 
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
-        is_root, rank, misc;
+        is_root, rank, misc, qidx, qkey, qstart, qrep;
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
-                          &seg, &core, &parent, &lab, &is_root, &rank, &misc})
+                          &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
+                          &qstart, &qrep})
             b->release();
     }
 };
@@ -120,6 +124,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
 //   0: in = const int32_t* values
 //   1: in = const uint8_t* flags (0/1)
 //   2: head flags of a sorted u32 key array: v[i] = (i == 0 || key[i] != key[i-1])
+//   3: head flags of key >> 2 (the eps cell of a quarter-cell key)
 // Writes out[0..n) and, if total_dev != nullptr, the total at *total_dev.
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
                     int32_t* total_dev, DevBuf& tmp);

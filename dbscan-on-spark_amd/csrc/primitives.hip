@@ -46,9 +46,12 @@ __device__ __forceinline__ int scan_value(const void* in, int64_t i, int64_t n) 
         return static_cast<const int32_t*>(in)[i];
     } else if constexpr (MODE == 1) {
         return static_cast<const uint8_t*>(in)[i] ? 1 : 0;
-    } else {
+    } else if constexpr (MODE == 2) {
         const uint32_t* k = static_cast<const uint32_t*>(in);
         return (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
+    } else {  // head flags of key >> 2 (cell of a quarter-cell key)
+        const uint32_t* k = static_cast<const uint32_t*>(in);
+        return (i == 0 || (k[i] >> 2) != (k[i - 1] >> 2)) ? 1 : 0;
     }
 }
 
@@ -305,17 +308,41 @@ __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __re
     }
 }
 
-__global__ void bbox_final_kernel(const double* partial, int nb, double* out) {
-    if (threadIdx.x != 0) return;
-    double r[5] = {INFINITY, -INFINITY, INFINITY, -INFINITY, 0};
-    for (int b = 0; b < nb; ++b) {
-        r[0] = fmin(r[0], partial[b * 5 + 0]);
-        r[1] = fmax(r[1], partial[b * 5 + 1]);
-        r[2] = fmin(r[2], partial[b * 5 + 2]);
-        r[3] = fmax(r[3], partial[b * 5 + 3]);
-        r[4] += partial[b * 5 + 4];
+__global__ __launch_bounds__(kBlock) void bbox_final_kernel(const double* partial, int nb,
+                                                            double* out) {
+    __shared__ double sm[kWaves][5];
+    double r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY, r4 = 0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        r0 = fmin(r0, partial[b * 5 + 0]);
+        r1 = fmax(r1, partial[b * 5 + 1]);
+        r2 = fmin(r2, partial[b * 5 + 2]);
+        r3 = fmax(r3, partial[b * 5 + 3]);
+        r4 += partial[b * 5 + 4];
     }
-    for (int c = 0; c < 5; ++c) out[c] = r[c];
+    r0 = wave_min(r0);
+    r1 = wave_max(r1);
+    r2 = wave_min(r2);
+    r3 = wave_max(r3);
+    for (int o = 32; o > 0; o >>= 1) r4 += __shfl_xor(r4, o, 64);
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        sm[w][0] = r0;
+        sm[w][1] = r1;
+        sm[w][2] = r2;
+        sm[w][3] = r3;
+        sm[w][4] = r4;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kWaves; ++k) {
+            sm[0][0] = fmin(sm[0][0], sm[k][0]);
+            sm[0][1] = fmax(sm[0][1], sm[k][1]);
+            sm[0][2] = fmin(sm[0][2], sm[k][2]);
+            sm[0][3] = fmax(sm[0][3], sm[k][3]);
+            sm[0][4] += sm[k][4];
+        }
+        for (int c = 0; c < 5; ++c) out[c] = sm[0][c];
+    }
 }
 
 }  // namespace
@@ -331,7 +358,8 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
     switch (mode) {
         case 0: scan_impl<0>(s, in, out, n, total_dev, t, need); break;
         case 1: scan_impl<1>(s, in, out, n, total_dev, t, need); break;
-        default: scan_impl<2>(s, in, out, n, total_dev, t, need); break;
+        case 2: scan_impl<2>(s, in, out, n, total_dev, t, need); break;
+        default: scan_impl<3>(s, in, out, n, total_dev, t, need); break;
     }
 }
 
@@ -375,7 +403,7 @@ void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, dou
     double* partial = static_cast<double*>(tmp.ensure((size_t)nb * 5 * sizeof(double)));
     hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, s, x, y, n, partial);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(64), 0, s, partial, nb, out_dev);
+    hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(kBlock), 0, s, partial, nb, out_dev);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
