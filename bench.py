@@ -52,16 +52,22 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no per-stage events")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--node", action="store_true", help="use the node path even at N = 1")
     return ap.parse_args()
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
+def load_traffic(kernel, n_points):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/profile.sh + tools/pmc_summary.py), only if it was measured on this workload size."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("bytes_per_launch")
+        e = d.get(kernel, {})
+        if e.get("n_points", 10_000_000) != n_points:
+            return None
+        return e.get("bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -95,19 +101,23 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     import dbscan_amd
     from dbscan_amd import device as D
 
-    h = dbscan_amd.Handle(local_rank)
+    h = dbscan_amd.Handle(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
 
     n_total = args.points_per_gpu * world
-    if world == 1:
+    if world == 1 and not args.node:
         x, y = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
         cl = torch.empty(n_total, dtype=torch.int32, device="cuda")
         fl = torch.empty(n_total, dtype=torch.uint8, device="cuda")
@@ -139,7 +149,8 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     prof = h.profile_read() if not args.no_profile else {}
@@ -157,7 +168,7 @@ def main():
         launches_per_step = prof[dom]["launches"] / max(1, args.steps)
         alg = ALG_BYTES.get(dom, 0) * pts / max(1.0, launches_per_step)
         achieved = alg / (avg_ms * 1e-3) / 1e9
-        traffic = load_traffic(dom)
+        traffic = load_traffic(dom, pts) if (world == 1 and not args.node) else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
@@ -166,7 +177,7 @@ def main():
                                        / HBM_PEAK_GBS, 5)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.node:
         sx, sy = x.cpu().numpy(), y.cpu().numpy()
         cpu = cpu_baseline(sx, sy, args.eps, args.min_points, args.cpu_budget, args.cpu_threads)
 
@@ -181,7 +192,8 @@ def main():
                              f"dense={args.dense}, seed={args.seed}), eps={args.eps}, "
                              f"minPoints={args.min_points}, LocalDBSCANNaive semantics"),
                 "n_points": n_total, "eps": args.eps, "min_points": args.min_points,
-                "parallelism": "single GPU" if world == 1 else f"slab x{world} + RCCL merge",
+                "parallelism": ("single GPU" if world == 1 and not args.node else
+                                f"slab x{world} + {'RCCL' if args.backend == 'nccl' else args.backend} merge"),
                 "clusters": k, "core_points": stats.get("core"),
                 "occupied_cells": stats.get("cells")},
             "roofline": roof,

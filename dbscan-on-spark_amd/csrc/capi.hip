@@ -158,6 +158,7 @@ struct dbscan_handle {
     dbscan::Workspace ws;
     dbscan::Profiler prof;
     dbscan::FitStats stats;
+    dbscan::SlabState slab;
     dbscan::DevBuf hx, hy, hcl, hfl;  // staging for the host-array entry points
     std::mutex mu;                    // one fit at a time per handle
 };
@@ -277,8 +278,8 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
         std::lock_guard<std::mutex> lk(h->mu);
         check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
-                          nullptr, nullptr, nullptr};
-        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+                          nullptr, nullptr};
+        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
         if (n_clusters_out) *n_clusters_out = (int32_t)k;
         return DBSCAN_OK;
@@ -306,9 +307,8 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         uint8_t* dfl = static_cast<uint8_t*>(h->hfl.ensure(n));
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
-        dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl,
-                          nullptr, nullptr, nullptr};
-        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+        dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
+        int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
                                         hipMemcpyDeviceToHost, h->stream));
         DBSCAN_HIP_CHECK(hipMemcpyAsync(flag_out, dfl, n, hipMemcpyDeviceToHost, h->stream));
@@ -331,10 +331,9 @@ int32_t dbscan_fit(const double* x, const double* y, int64_t n, double eps, int3
                         flag_out, n_clusters_out);
 }
 
-int32_t dbscan_fit_slab_device(dbscan_handle* h, const double* d_x, const double* d_y,
+int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
-                               int32_t min_points, uint8_t* d_core, int32_t* d_root,
-                               int32_t* d_bmin) {
+                               int32_t min_points, uint8_t* d_core, int32_t* d_root) {
     if (!h) {
         set_err("NULL handle");
         return DBSCAN_EARG;
@@ -342,10 +341,31 @@ int32_t dbscan_fit_slab_device(dbscan_handle* h, const double* d_x, const double
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
         check_fit_args(n, eps, DBSCAN_MODE_NAIVE, d_x, d_y, d_core, d_root);
-        if (n > 0 && (!d_zone || !d_bmin)) throw dbscan::ArgError{"NULL array pointer"};
+        if (n > 0 && !d_zone) throw dbscan::ArgError{"NULL zone pointer"};
         dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
-                          nullptr, d_core, d_root, d_bmin};
-        dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats);
+                          nullptr, d_core, d_root};
+        dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
+        h->prof.flush();
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                                 const int64_t* d_gs_of_root, const int32_t* d_label_of_root,
+                                 int32_t mode, int32_t* d_cluster, uint8_t* d_flag) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
+            throw dbscan::ArgError{"bad mode"};
+        if (h->slab.n > 0 && (!d_zone || !d_gid || !d_gs_of_root || !d_label_of_root ||
+                              !d_cluster || !d_flag))
+            throw dbscan::ArgError{"NULL array pointer"};
+        dbscan::run_slab_label(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gid, d_gs_of_root,
+                               d_label_of_root, mode, d_cluster, d_flag);
         h->prof.flush();
         return DBSCAN_OK;
     });

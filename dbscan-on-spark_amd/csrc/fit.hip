@@ -489,35 +489,67 @@ __global__ __launch_bounds__(kBlock) void output_kernel(
     flag_out[o] = fl;
 }
 
-// Slab fit output (multi-GPU): core flag, local root (slab index), border minimum root.
-__global__ __launch_bounds__(kBlock) void slab_output_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
-    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
-    uint8_t* __restrict__ core_out, int32_t* __restrict__ root_out,
-    int32_t* __restrict__ bmin_out) {
+// Slab fit, phase 1 output (multi-GPU node path): core flag and local root (slab index of the
+// minimum-index core of the local component), in slab order.
+__global__ __launch_bounds__(kBlock) void slab_roots_kernel(int64_t n,
+                                                            const int32_t* __restrict__ perm,
+                                                            const uint8_t* __restrict__ core,
+                                                            const int32_t* __restrict__ lab,
+                                                            uint8_t* __restrict__ core_out,
+                                                            int32_t* __restrict__ root_out) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const int32_t o = perm[p];
-    int32_t m = -1;
-    if (!core[p] && p < nf && zone[o] == 0) {
+    core_out[o] = core[p];
+    root_out[o] = core[p] ? lab[p] : -1;
+}
+
+// Slab fit, phase 2 (after the global merge): labels of the owned (zone 0) points.
+//   gs_of_root[r]    global s(K) (a global visit index) of local root r (slab index)
+//   label_of_root[r] global cluster id of that component
+// Border rule on global visit indices: m = min over core neighbours of gs_of_root[root];
+// Naive: Border iff m < gid(b); Archery: Border iff a core neighbour exists.
+__global__ __launch_bounds__(kBlock) void slab_label_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2, int32_t mode,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
+    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
+    const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
+    const int32_t* __restrict__ label_of_root, int32_t* __restrict__ cluster_out,
+    uint8_t* __restrict__ flag_out) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const int32_t o = perm[p];
+    if (zone[o] != 0) return;
+    int32_t cl = 0;
+    uint8_t fl = 2;
+    if (core[p]) {
+        cl = label_of_root[lab[p]];
+        fl = 1;
+    } else if (p < nf) {
         const double2 me = xy[p];
         const Seg s = load_seg(seg, cell[p]);
-        int32_t best = 0x7FFFFFFF;
+        int64_t m = 0x7FFFFFFFFFFFFFFFll;
+        int32_t mr = -1;
         for_candidates(s, [&](int j) {
             const double2 q = xy[j];
             if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
-                const int32_t lj = lab[j];
-                best = lj < best ? lj : best;
+                const int32_t r = lab[j];
+                const int64_t v = gs_of_root[r];
+                if (v < m) {
+                    m = v;
+                    mr = r;
+                }
             }
             return true;
         });
-        m = best == 0x7FFFFFFF ? -1 : best;
+        if (mr >= 0 && (mode != 0 || m < gid[o])) {
+            cl = label_of_root[mr];
+            fl = 0;
+        }
     }
-    core_out[o] = core[p];
-    root_out[o] = core[p] ? lab[p] : -1;
-    bmin_out[o] = m;
+    cluster_out[o] = cl;
+    flag_out[o] = fl;
 }
 
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -561,12 +593,19 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
     return false;
 }
 
-int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st) {
+int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
+                SlabState* slab) {
+    if (slab) slab->valid = false;
     const int64_t n = a.n;
     FitStats stats;
     stats.n = n;
     if (n == 0) {
         if (st) *st = stats;
+        if (slab) {
+            slab->valid = a.zone != nullptr;
+            slab->n = 0;
+            slab->nf = 0;
+        }
         return 0;
     }
     const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
@@ -620,6 +659,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     stats.bits = bits;
+    ws.perm_sorted = perm;
 
     const int64_t nfa = nf > 0 ? nf : 1;
     double2* xy = static_cast<double2*>(ws.xy.ensure(nfa * sizeof(double2)));
@@ -753,9 +793,8 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "output");
-            hipLaunchKernelGGL(slab_output_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell,
-                               seg, n, nf, eps2, perm, a.zone, core, lab, a.core_out, a.root_out,
-                               a.bmin_out);
+            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
+                               core, lab, a.core_out, a.root_out);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         int32_t hv[3];
@@ -766,7 +805,31 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     }
     stats.nclusters = k;
     if (st) *st = stats;
+    if (slab) {
+        slab->valid = a.zone != nullptr;
+        slab->n = n;
+        slab->nf = nf;
+        slab->eps2 = eps2;
+    }
     return k;
+}
+
+void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
+                    const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
+                    const int32_t* label_of_root, int32_t mode, int32_t* cluster,
+                    uint8_t* flag) {
+    if (!st.valid) throw ArgError{"dbscan_slab_label_device: no slab fit on this handle"};
+    if (st.n == 0) return;
+    StageTimer t(prof, s, "slab_label");
+    hipLaunchKernelGGL(slab_label_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+                       static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
+                       static_cast<const Seg*>(ws.seg.p), st.n, st.nf, st.eps2, mode,
+                       static_cast<const int32_t*>(ws.perm_sorted),
+                       zone, static_cast<const uint8_t*>(ws.core.p),
+                       static_cast<const int32_t*>(ws.lab.p), gid, gs_of_root, label_of_root,
+                       cluster, flag);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace dbscan

@@ -87,6 +87,7 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep;
+    int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
@@ -101,7 +102,8 @@ struct FitStats {
 };
 
 // One fit.  Full fits (zone == nullptr) write cluster/flag in input order and return the
-// cluster count; slab fits (zone != nullptr) write core_out/root_out/bmin_out.
+// cluster count; slab fits (zone != nullptr) write core_out/root_out and keep their grid in the
+// workspace for run_slab_label.
 struct FitArgs {
     const double* x;
     const double* y;
@@ -114,10 +116,20 @@ struct FitArgs {
     uint8_t* flag;
     uint8_t* core_out;
     int32_t* root_out;
-    int32_t* bmin_out;
 };
 
-int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st);
+// What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).
+struct SlabState {
+    bool valid = false;
+    int64_t n = 0, nf = 0;
+    double eps2 = 0;
+};
+
+int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
+                SlabState* slab);
+void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
+                    const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
+                    const int32_t* label_of_root, int32_t mode, int32_t* cluster, uint8_t* flag);
 
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:

@@ -49,13 +49,29 @@ def generate_blobs(n: int, noise: float, dense: float, seed: int, handle: _lib.H
 
 def slab_fit(x: torch.Tensor, y: torch.Tensor, zone: torch.Tensor, eps: float, min_points: int,
              handle: _lib.Handle):
-    """Slab fit for the node path: returns (core uint8, root int32, bmin int32) device tensors."""
+    """Slab fit phase 1 (node path): returns (core uint8, root int32) device tensors."""
     n = x.numel()
     core = torch.empty(n, dtype=torch.uint8, device=x.device)
     root = torch.empty(n, dtype=torch.int32, device=x.device)
-    bmin = torch.empty(n, dtype=torch.int32, device=x.device)
     torch.cuda.current_stream(x.device).synchronize()
-    _lib.check(_lib.load().dbscan_fit_slab_device(handle.ptr, _p(x), _p(y), _p(zone), n,
+    _lib.check(_lib.load().dbscan_slab_fit_device(handle.ptr, _p(x), _p(y), _p(zone), n,
                                                   float(eps), int(min_points), _p(core),
-                                                  _p(root), _p(bmin)))
-    return core, root, bmin
+                                                  _p(root)))
+    return core, root
+
+
+def slab_label(zone: torch.Tensor, gid: torch.Tensor, gs_of_root: torch.Tensor,
+               label_of_root: torch.Tensor, mode: int, handle: _lib.Handle, cluster=None,
+               flag=None):
+    """Slab fit phase 2 (after the global merge): (cluster int32, flag uint8) in slab order;
+    only zone-0 entries are written."""
+    n = zone.numel()
+    if cluster is None:
+        cluster = torch.zeros(n, dtype=torch.int32, device=zone.device)
+    if flag is None:
+        flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
+    torch.cuda.current_stream(zone.device).synchronize()
+    _lib.check(_lib.load().dbscan_slab_label_device(handle.ptr, _p(zone), _p(gid),
+                                                    _p(gs_of_root), _p(label_of_root),
+                                                    int(mode), _p(cluster), _p(flag)))
+    return cluster, flag

@@ -1,0 +1,257 @@
+"""Whole-node DBSCAN over N GPUs: spatial slabs with eps halos, exact merge over RCCL.
+
+This is the MI355X restatement of the reference's distributed path:
+  DBSCAN.scala:105-137   partition the plane, grow each partition by eps, duplicate points
+  DBSCAN.scala:150-155   LocalDBSCANNaive.fit per partition            -> slab fit on one GPU
+  DBSCAN.scala:158-222   band points, findAdjacencies, DBSCANGraph, global ids
+                                                  -> all-gather of shared core points + merge
+  DBSCAN.scala:232-270   relabel inner/outer points                  -> slab label kernel
+One process per GPU; slabs are x-ranges at count quantiles snapped to the 2*eps grid
+(DBSCAN.scala:289 minimumRectangleSize), one slab per rank.
+
+Exactness (why the result equals ONE fit of the whole data set, bit for bit, including the
+Naive noise rule and the cluster numbering -- unlike the reference's merge):
+  * zone 0 = the rank's own slab; zone 1 = points within R = max|x'-x| of any accepted pair
+    (R >= eps) of the slab; zone 2 = within 2R.  Counts of zone 0/1 points are exact, so their
+    core flags are the global ones.
+  * every global core-core edge (p, q) has p owned by some rank g and q in g's zone 0/1, so it
+    is an edge of g's local graph: global components are unions of local components that share
+    a core point.  Shared core points (present in zones 0/1 of two ranks) are all-gathered as
+    (gid, local root gid) records; a min-label merge gives each local root its global s(K)
+    (= min visit index of the component, the reference's cluster-opening order).
+  * owned global roots are all-gathered; cluster id = 1 + rank of s(K) among them.
+  * border/noise needs min over core neighbours of s(K): done after the merge on the GPU
+    (dbscan_slab_label_device), since s(K) is not monotone in the local root.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+
+OUT = 255  # point not in this rank's slab
+
+
+def reach(eps: float) -> float:
+    """Upper bound of |x'-x| over pairs the fp64 predicate accepts (grid soundness)."""
+    return max(abs(eps) * (1.0 + 2.0 ** -40), 2.0 ** -500)
+
+
+def margin1(c: float, R: float) -> float:
+    return R * (1.0 + 2.0 ** -10) + 16.0 * math.ulp(c)
+
+
+def margin2(c: float, R: float) -> float:
+    return 2.0 * margin1(c, R) + 16.0 * math.ulp(c)
+
+
+def make_cuts(x: torch.Tensor, world: int, eps: float, sample: int = 1 << 20) -> List[float]:
+    """world-1 x cuts at count quantiles of the finite x values, snapped down to the 2*eps grid
+    (the reference's partition corners, DBSCAN.scala:289,352-353).  Empty if one slab suffices
+    or eps*eps is not finite (all-pairs / no-pairs semantics do not shard)."""
+    e2 = eps * eps
+    if world <= 1 or not math.isfinite(e2):
+        return []
+    xf = x[torch.isfinite(x)]
+    if xf.numel() == 0:
+        return []
+    step = max(1, xf.numel() // sample)
+    xs, _ = torch.sort(xf[::step])
+    xs = xs.double().cpu()
+    grid = 2.0 * abs(eps)
+    cuts = []
+    for k in range(1, world):
+        q = float(xs[min(xs.numel() - 1, k * xs.numel() // world)])
+        c = math.floor(q / grid) * grid if grid > 0 and math.isfinite(q / grid) else q
+        if cuts and c < cuts[-1]:
+            c = cuts[-1]
+        cuts.append(c)
+    return cuts
+
+
+def zones(x: torch.Tensor, rank: int, cuts: List[float], eps: float):
+    """Zone of every point for `rank` (0 owned, 1 inner halo, 2 outer halo, 255 outside) and
+    the `shared` mask: points that are in zone 0/1 of at least two ranks."""
+    world = len(cuts) + 1
+    R = reach(eps)
+    lo = cuts[rank - 1] if rank > 0 else None
+    hi = cuts[rank] if rank < world - 1 else None
+    own = torch.ones_like(x, dtype=torch.bool)
+    if lo is not None:
+        own &= x >= lo
+    if hi is not None:
+        own &= x < hi
+    if rank == 0 and world > 1:
+        own |= torch.isnan(x)  # NaN x: owned by rank 0 (isolated: never anyone's neighbour)
+    in1 = torch.zeros_like(own)
+    in2 = torch.zeros_like(own)
+    shared = torch.zeros_like(own)
+    if lo is not None:
+        m1, m2 = margin1(lo, R), margin2(lo, R)
+        in1 |= (x >= lo - m1) & (x < lo)
+        in2 |= (x >= lo - m2) & (x < lo - m1)
+        shared |= own & (x <= lo + m1)  # zone 1 of rank-1 (same expression there)
+    if hi is not None:
+        m1, m2 = margin1(hi, R), margin2(hi, R)
+        in1 |= (x >= hi) & (x <= hi + m1)
+        in2 |= (x > hi + m1) & (x <= hi + m2)
+        shared |= own & (x >= hi - m1)  # zone 1 of rank+1
+    z = torch.full(x.shape, OUT, dtype=torch.uint8, device=x.device)
+    z[in2] = 2
+    z[in1] = 1
+    z[own] = 0
+    shared |= z == 1
+    return z, shared
+
+
+class Comm:
+    """Variable-length all-gather over torch.distributed (RCCL for 'nccl', host for 'gloo')."""
+
+    def __init__(self, dist=None):
+        self.dist = dist
+        if dist is not None and dist.is_initialized():
+            self.world, self.rank = dist.get_world_size(), dist.get_rank()
+            self.host = dist.get_backend() == "gloo"
+        else:
+            self.dist, self.world, self.rank, self.host = None, 1, 0, True
+
+    def allgather_varlen(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate every rank's t along its last dim, in rank order."""
+        if self.world == 1:
+            return t
+        dev = t.device
+        tt = t.cpu() if self.host else t.contiguous()
+        n = torch.tensor([tt.shape[-1]], dtype=torch.int64, device=tt.device)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n)
+        sizes = [int(v.item()) for v in ns]
+        mx = max(sizes)
+        pad = torch.zeros(tt.shape[:-1] + (mx,), dtype=tt.dtype, device=tt.device)
+        pad[..., :tt.shape[-1]] = tt
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad)
+        res = torch.cat([o[..., :k] for o, k in zip(outs, sizes)], dim=-1)
+        return res.to(dev)
+
+
+class HipSlabOps:
+    """The product slab fit: libdbscan_hip.so through device tensors."""
+
+    def __init__(self, handle: _lib.Handle):
+        self.h = handle
+
+    def fit(self, x, y, zone, eps, min_points):
+        from . import device as D
+
+        return D.slab_fit(x, y, zone, eps, min_points, self.h)
+
+    def label(self, zone, gid, gs_of_root, label_of_root, mode):
+        from . import device as D
+
+        return D.slab_label(zone, gid, gs_of_root, label_of_root, mode, self.h)
+
+
+def merge_min_labels(a: torch.Tensor, b: torch.Tensor):
+    """Connected components of the graph with edges (a_i, b_i) over int64 node ids; returns
+    (nodes sorted, min node id of each node's component).  Min-label propagation with pointer
+    jumping (each round: scatter-min over edges, then label = label[label])."""
+    nodes = torch.unique(torch.cat([a, b]))
+    ia = torch.searchsorted(nodes, a)
+    ib = torch.searchsorted(nodes, b)
+    lab = nodes.clone()
+    for _ in range(64):
+        m = torch.minimum(lab[ia], lab[ib])
+        new = lab.scatter_reduce(0, ia, m, reduce="amin").scatter_reduce(0, ib, m,
+                                                                          reduce="amin")
+        new = new[torch.searchsorted(nodes, new)]  # pointer jump
+        if torch.equal(new, lab):
+            break
+        lab = new
+    return nodes, lab
+
+
+class NodeJob:
+    """One rank's share of a whole-node fit.  run() is one step (timed by bench.py)."""
+
+    def __init__(self, x, y, zone, gid, shared, eps, min_points, mode, comm: Comm, ops):
+        self.x, self.y, self.zone, self.gid, self.shared = x, y, zone, gid, shared
+        self.eps, self.min_points, self.mode = float(eps), int(min_points), int(mode)
+        self.comm, self.ops = comm, ops
+        self.cluster = self.flag = None
+        self.n_clusters = 0
+
+    @classmethod
+    def from_global(cls, x_all, y_all, eps, min_points, mode, comm: Comm, ops,
+                    cuts: Optional[List[float]] = None) -> "NodeJob":
+        """Select this rank's slab (zones 0/1/2, global visit order kept) from the global
+        arrays.  Setup, not part of a step."""
+        if cuts is None:
+            cuts = make_cuts(x_all, comm.world, eps)
+        assert len(cuts) == comm.world - 1 or (not cuts), "one slab per rank"
+        if not cuts and comm.world > 1:  # unshardable eps: everything on rank 0
+            own = torch.full(x_all.shape, OUT, dtype=torch.uint8, device=x_all.device)
+            if comm.rank == 0:
+                own[:] = 0
+            z, sh = own, torch.zeros_like(own, dtype=torch.bool)
+        else:
+            z, sh = zones(x_all, comm.rank, cuts, eps)
+        idx = torch.nonzero(z != OUT).flatten()  # ascending: global visit order preserved
+        job = cls(x_all[idx].contiguous(), y_all[idx].contiguous(), z[idx].contiguous(),
+                  idx.to(torch.int64).contiguous(), sh[idx].contiguous(), eps, min_points, mode,
+                  comm, ops)
+        job.cuts = cuts
+        return job
+
+    @classmethod
+    def synthetic(cls, n_total, noise, dense, seed, eps, min_points, handle, dist,
+                  mode: int = 0) -> "NodeJob":
+        """bench.py setup: every rank generates the same G(n_total) on its GPU (device
+        generator), then keeps its slab."""
+        from . import device as D
+
+        x_all, y_all = D.generate_blobs(n_total, noise, dense, seed, handle)
+        comm = Comm(dist)
+        job = cls.from_global(x_all, y_all, eps, min_points, mode, comm, HipSlabOps(handle))
+        del x_all, y_all
+        torch.cuda.empty_cache()
+        return job
+
+    def run(self) -> int:
+        n = self.x.numel()
+        dev = self.x.device
+        core, root = self.ops.fit(self.x, self.y, self.zone, self.eps, self.min_points)
+        corb = core.bool()
+        rootl = root.long()
+        # records: shared core points -> their local root, as global visit indices
+        sel = self.shared & corb
+        rec = torch.stack([self.gid[sel], self.gid[rootl[sel]]])
+        allrec = self.comm.allgather_varlen(rec)
+        ar = torch.arange(n, device=dev)
+        lmask = corb & (rootl == ar)  # local roots (zones 0/1)
+        lroots = torch.nonzero(lmask).flatten()
+        gs_of_root = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        gs_of_root[lroots] = self.gid[lroots]
+        if allrec.shape[-1] > 0:
+            nodes, lab = merge_min_labels(allrec[0], allrec[1])
+            g = self.gid[lroots]
+            pos = torch.searchsorted(nodes, g).clamp(max=nodes.numel() - 1)
+            hit = nodes[pos] == g
+            gs_of_root[lroots[hit]] = lab[pos[hit]]
+        # global roots owned here: s(K) is a zone-0 core that is its own local root
+        own = lmask & (self.zone == 0) & (gs_of_root == self.gid)
+        all_roots, _ = torch.sort(self.comm.allgather_varlen(self.gid[own]))
+        label_of_root = torch.zeros(n, dtype=torch.int32, device=dev)
+        label_of_root[lroots] = (torch.searchsorted(all_roots, gs_of_root[lroots]) + 1).to(
+            torch.int32)
+        self.cluster, self.flag = self.ops.label(self.zone, self.gid, gs_of_root,
+                                                 label_of_root, self.mode)
+        self.n_clusters = int(all_roots.numel())
+        return self.n_clusters
+
+    def owned(self):
+        """(global visit index, cluster, flag) of this rank's owned points."""
+        m = self.zone == 0
+        return self.gid[m], self.cluster[m], self.flag[m]

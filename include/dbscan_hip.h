@@ -105,22 +105,29 @@ int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, do
                             int64_t* launches, int32_t max);
 
 /* ---------------------------------------------------------------------------------------
- * Slab fit for the multi-GPU node path.  The caller passes the points of one
- * spatial slab grown by 2*eps halos, in increasing global visit order, with a zone per point:
- *   0 = owned (inside this rank's main slab), 1 = inner halo (within eps of the slab),
- *   2 = outer halo (only used as neighbour-count candidates).
- * Counts are exact for zones 0 and 1.  The slab fit then unions core-core edges among zone
- * 0/1 points and returns, per point, in slab order:
- *   d_core[i]   1 if core (zones 0/1), else 0
- *   d_root[i]   cores: slab index of the minimum-index core of the point's local component;
- *               non-cores: -1
- *   d_bmin[i]   zone-0 non-cores: slab index of the smallest root among adjacent cores'
- *               components (or -1); others -1
- * Global merge and relabel happen above this call (dbscan_amd/node.py, RCCL all-gather). */
-int32_t dbscan_fit_slab_device(dbscan_handle* h, const double* d_x, const double* d_y,
+ * Slab fits for the multi-GPU node path (dbscan_amd/node.py).  The caller
+ * passes the points of one spatial slab grown by halos, in increasing global visit order, with
+ * a zone per point:
+ *   0 = owned (inside this rank's slab), 1 = inner halo (within eps of the slab: exact counts,
+ *   joins the local union-find), 2 = outer halo (within 2*eps: neighbour-count candidate only).
+ * Phase 1, dbscan_slab_fit_device: exact core flags for zones 0/1 and, per core, the slab
+ *   index of the minimum-index core of its local component (d_root; -1 for non-cores).
+ *   This mirrors the per-partition LocalDBSCANNaive.fit of DBSCAN.scala:150-155 with the
+ *   partition's eps-grown rectangle (DBSCAN.scala:116-137).
+ * The caller merges local components across slabs (RCCL all-gather of shared core points,
+ * global min-label union; replaces DBSCAN.scala:158-222) and numbers global clusters.
+ * Phase 2, dbscan_slab_label_device (same handle, no fit in between): labels of the zone-0
+ *   points in slab order.  d_gid[i] = global visit index of slab point i; for every local root
+ *   r: d_gs_of_root[r] = global s(K) of its component, d_label_of_root[r] = global cluster id.
+ *   Cores get label_of_root[root]; a non-core takes the neighbour root with the smallest
+ *   gs_of_root (Naive: only if that is < its own gid).  Zone 1/2 entries are left untouched.
+ *   This replaces the relabel of DBSCAN.scala:232-270.                                      */
+int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
-                               int32_t min_points, uint8_t* d_core, int32_t* d_root,
-                               int32_t* d_bmin);
+                               int32_t min_points, uint8_t* d_core, int32_t* d_root);
+int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                                 const int64_t* d_gs_of_root, const int32_t* d_label_of_root,
+                                 int32_t mode, int32_t* d_cluster, uint8_t* d_flag);
 
 /* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
  * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the

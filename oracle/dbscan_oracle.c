@@ -405,9 +405,8 @@ static void radix_sort_pairs(int64_t* key, int64_t* val, int64_t n, int bits) {
     free(v2);
 }
 
-int32_t oracle_fit_grid(const double* x, const double* y, int64_t n, double eps,
-                        int32_t min_points, int32_t mode, int32_t nthreads, int32_t* cluster,
-                        uint8_t* flag, int64_t* counts_out) {
+static void grid_build(grid_ctx* gp, const double* x, const double* y, int64_t n, double eps,
+                       int32_t min_points) {
     grid_ctx g;
     memset(&g, 0, sizeof(g));
     g.x = x;
@@ -488,20 +487,96 @@ int32_t oracle_fit_grid(const double* x, const double* y, int64_t n, double eps,
             g.ncells = nc;
         }
     }
+    *gp = g;
+}
+
+static void grid_free(grid_ctx* g) {
+    free(g->core);
+    free(g->counts);
+    free(g->parent);
+    free(g->bmin);
+    free(g->cell_of);
+    free(g->order);
+    free(g->okey);
+    free(g->ckey);
+    free(g->cstart);
+}
+
+int32_t oracle_fit_grid(const double* x, const double* y, int64_t n, double eps,
+                        int32_t min_points, int32_t mode, int32_t nthreads, int32_t* cluster,
+                        uint8_t* flag, int64_t* counts_out) {
+    grid_ctx g;
+    grid_build(&g, x, y, n, eps, min_points);
     run_phase(&g, 0, nthreads);
     run_phase(&g, 1, nthreads);
     run_phase(&g, 2, nthreads);
     if (counts_out)
         for (int64_t i = 0; i < n; ++i) counts_out[i] = g.counts[i];
     int32_t k = finish_labels(n, g.core, g.parent, g.bmin, mode, cluster, flag);
-    free(g.core);
-    free(g.counts);
-    free(g.parent);
-    free(g.bmin);
-    free(g.cell_of);
-    free(g.order);
-    free(g.okey);
-    free(g.ckey);
-    free(g.cstart);
+    grid_free(&g);
     return k;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * 4. Slab semantics of the node path (dbscan_slab_fit_device / dbscan_slab_label_device),
+ *    restated on the CPU so the multi-rank merge (dbscan_amd/node.py) can be tested with the
+ *    gloo backend on machines without a GPU.  Zones: 0 owned, 1 inner halo, 2 outer halo.
+ * ------------------------------------------------------------------------------------------ */
+int32_t oracle_slab_fit(const double* x, const double* y, const uint8_t* zone, int64_t n,
+                        double eps, int32_t min_points, int32_t nthreads, uint8_t* core_out,
+                        int32_t* root_out) {
+    grid_ctx g;
+    grid_build(&g, x, y, n, eps, min_points);
+    run_phase(&g, 0, nthreads);
+    for (int64_t i = 0; i < n; ++i)
+        if (zone[i] == 2) g.core[i] = 0; /* halo-only candidates are never core */
+    run_phase(&g, 1, nthreads);
+    for (int64_t i = 0; i < n; ++i) {
+        core_out[i] = g.core[i];
+        root_out[i] = g.core[i] ? (int32_t)uf_find(g.parent, i) : -1;
+    }
+    grid_free(&g);
+    return 0;
+}
+
+int32_t oracle_slab_label(const double* x, const double* y, const uint8_t* zone, int64_t n,
+                          double eps, const uint8_t* core, const int32_t* root,
+                          const int64_t* gid, const int64_t* gs_of_root,
+                          const int32_t* label_of_root, int32_t mode, int32_t* cluster_out,
+                          uint8_t* flag_out) {
+    grid_ctx g;
+    grid_build(&g, x, y, n, eps, 1);
+    for (int64_t i = 0; i < n; ++i) {
+        if (zone[i] != 0) continue;
+        if (core[i]) {
+            cluster_out[i] = label_of_root[root[i]];
+            flag_out[i] = FLAG_CORE;
+            continue;
+        }
+        int64_t m = INT64_MAX;
+        int32_t mr = -1;
+        int64_t b[3] = {0, 0, 0}, e[3] = {0, 0, 0};
+        int nr = 0;
+        if (g.all_pairs) {
+            e[0] = n;
+            nr = 1;
+        } else if (!g.no_pairs && g.cell_of[i] >= 0) {
+            nr = stencil_ranges(&g, g.cell_of[i], b, e);
+        }
+        for (int r = 0; r < nr; ++r)
+            for (int64_t t = b[r]; t < e[r]; ++t) {
+                int64_t j = g.all_pairs ? t : g.order[t];
+                if (!core[j] || !within(x[i], y[i], x[j], y[j], g.eps2)) continue;
+                int64_t v = gs_of_root[root[j]];
+                if (v < m) {
+                    m = v;
+                    mr = root[j];
+                }
+            }
+        int ok = mr >= 0 && (mode != MODE_NAIVE || m < gid[i]);
+        cluster_out[i] = ok ? label_of_root[mr] : 0;
+        flag_out[i] = ok ? FLAG_BORDER : FLAG_NOISE;
+    }
+    grid_free(&g);
+    return 0;
 }

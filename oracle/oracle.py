@@ -66,6 +66,11 @@ def lib() -> ctypes.CDLL:
         L.ref_train.argtypes = [dp, dp, i64, ctypes.c_double, i32, i64, i32, vp, vp, vp, vp,
                                 vp, i64]
         L.ref_train.restype = i64
+        L.oracle_slab_fit.argtypes = [dp, dp, vp, i64, ctypes.c_double, i32, i32, vp, vp]
+        L.oracle_slab_fit.restype = i32
+        L.oracle_slab_label.argtypes = [dp, dp, vp, i64, ctypes.c_double, vp, vp, vp, vp, vp,
+                                        i32, vp, vp]
+        L.oracle_slab_label.restype = i32
         _lib = L
     return _lib
 
@@ -183,6 +188,35 @@ def ref_train(x, y, eps, min_points, max_points_per_partition, nthreads=None):
     npt = int(npart[0])
     return dict(cluster=cl, flag=fl, records=oc, n_clusters=int(k),
                 rects=rects[:min(npt, mp)].copy())
+
+
+def slab_fit(x, y, zone, eps, min_points, nthreads=None):
+    """CPU restatement of dbscan_slab_fit_device (node path test double)."""
+    x, y = _xy(x, y)
+    zone = np.ascontiguousarray(zone, np.uint8)
+    n = x.size
+    core = np.zeros(n, np.uint8)
+    root = np.zeros(n, np.int32)
+    nt = nthreads or min(8, os.cpu_count() or 1)
+    lib().oracle_slab_fit(_ptr(x), _ptr(y), _ptr(zone), n, float(eps), int(min_points), nt,
+                          _ptr(core), _ptr(root))
+    return core, root
+
+
+def slab_label(x, y, zone, eps, core, root, gid, gs_of_root, label_of_root, mode):
+    """CPU restatement of dbscan_slab_label_device (zone-0 entries written)."""
+    x, y = _xy(x, y)
+    n = x.size
+    args = [np.ascontiguousarray(a, t) for a, t in ((zone, np.uint8), (core, np.uint8),
+                                                     (root, np.int32), (gid, np.int64),
+                                                     (gs_of_root, np.int64),
+                                                     (label_of_root, np.int32))]
+    cl = np.zeros(n, np.int32)
+    fl = np.full(n, NOT_FLAGGED, np.uint8)
+    lib().oracle_slab_label(_ptr(x), _ptr(y), _ptr(args[0]), n, float(eps), _ptr(args[1]),
+                            _ptr(args[2]), _ptr(args[3]), _ptr(args[4]), _ptr(args[5]),
+                            int(mode), _ptr(cl), _ptr(fl))
+    return cl, fl
 
 
 # --------------------------------------------------------------------------------------------

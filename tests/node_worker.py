@@ -1,0 +1,71 @@
+"""Worker processes for the multi-rank node-path tests (spawned by test_node*.py).
+
+Every rank builds its slab of the same global data set, runs one NodeJob step, and writes its
+owned (global index, cluster, flag) triples to `out_dir/rank<r>.npz`."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "dbscan-on-spark_amd"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+class OracleSlabOps:
+    """CPU test double of HipSlabOps: the oracle's restatement of the slab semantics, so the
+    merge logic (collectives, global union, numbering) runs under gloo without a GPU."""
+
+    def fit(self, x, y, zone, eps, min_points):
+        import oracle as O
+
+        xs, ys, zs = x.numpy(), y.numpy(), zone.numpy()
+        core, root = O.slab_fit(xs, ys, zs, eps, min_points, nthreads=2)
+        self.state = (xs, ys, zs, eps, core, root)
+        return torch.from_numpy(core), torch.from_numpy(root)
+
+    def label(self, zone, gid, gs_of_root, label_of_root, mode):
+        import oracle as O
+
+        xs, ys, zs, eps, core, root = self.state
+        cl, fl = O.slab_label(xs, ys, zs, eps, core, root, gid.numpy(), gs_of_root.numpy(),
+                              label_of_root.numpy(), mode)
+        return torch.from_numpy(cl), torch.from_numpy(fl)
+
+
+def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dbscan_amd import node
+
+    d = np.load(data_path)
+    x, y = torch.from_numpy(d["x"]), torch.from_numpy(d["y"])
+    if use_gpu:
+        import dbscan_amd
+
+        torch.cuda.set_device(0)
+        h = dbscan_amd.Handle(0)
+        ops = node.HipSlabOps(h)
+        x, y = x.cuda(), y.cuda()
+    else:
+        ops = OracleSlabOps()
+    job = node.NodeJob.from_global(x, y, eps, min_points, mode, node.Comm(dist), ops)
+    k = job.run()
+    k2 = job.run()  # a second step on the same handle must give the same answer
+    g, c, f = (t.cpu().numpy() for t in job.owned())
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), gid=g, cluster=c, flag=f,
+             k=np.array([k, k2]), n_slab=np.array([job.x.numel()]),
+             cuts=np.array(job.cuts, dtype=np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    args = sys.argv[1:]
+    run(int(args[0]), int(args[1]), int(args[2]), args[3], args[4], float(args[5]),
+        int(args[6]), int(args[7]), args[8] == "1")
