@@ -360,39 +360,31 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict
 // Loads/stores are agent-scope relaxed atomics (L1-bypassing), hooks are CAS on roots only;
 // stale reads only ever show an older ancestor, which is still an ancestor.
 // ---------------------------------------------------------------------------------------
-// UF variant (template parameter V): 0 = agent-scope atomic loads (L1-bypassing) + path-halving
-// stores; 1 = plain loads, no stores (stale L1 copies are older ancestors: still correct);
-// 2 = atomic loads, no stores.
-__device__ unsigned long long g_uf_stats[8];  // debug variant 3: finds, hops, cas, cas_fail, pairs
-
+// UF load policy (template parameter V): 0 = agent-scope atomic loads (L1-bypassing) with
+// path-halving stores (per-point fallback union); 1 = plain L1-cacheable loads, no stores
+// (quarter union; measured 2.4 vs 5.0 ms, tools/uf_variants.sh).  Stale copies are older
+// ancestors, which are still ancestors, so both are correct; only CAS hooks write roots.
 template <int V>
 __device__ __forceinline__ int ld_par(int* par, int i) {
-    if constexpr (V == 3) atomicAdd(&g_uf_stats[1], 1ull);
-    if constexpr (V == 1 || V == 4) {
-        return par[i];  // plain (L1-cacheable) load
+    if constexpr (V == 1) {
+        return par[i];
     } else {
         return __hip_atomic_load(par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-template <int V>
 __device__ __forceinline__ void st_par(int* par, int i, int v) {
-    if constexpr (V == 4) {
-        par[i] = v;  // plain store: a hint only (any ancestor is a valid parent)
-    } else {
-        __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    __hip_atomic_store(par + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int V = 0>
 __device__ int uf_find(int* par, int x) {
-    if constexpr (V == 3) atomicAdd(&g_uf_stats[0], 1ull);
     int cur = ld_par<V>(par, x);
     if (cur == x) return x;
     int prev = x;
     for (;;) {
         const int next = ld_par<V>(par, cur);
         if (next == cur) return cur;
-        if constexpr (V == 0 || V == 3 || V == 4) st_par<V>(par, prev, next);  // path halving
+        if constexpr (V == 0) st_par(par, prev, next);  // path halving (prev is a non-root)
         prev = cur;
         cur = next;
     }
@@ -409,7 +401,7 @@ __device__ int uf_find_until(int* par, int x, int target) {
     for (;;) {
         const int next = ld_par<V>(par, cur);
         if (next == cur || next == target) return next;
-        if constexpr (V == 0 || V == 3 || V == 4) st_par<V>(par, prev, next);
+        if constexpr (V == 0) st_par(par, prev, next);
         prev = cur;
         cur = next;
     }
@@ -423,11 +415,9 @@ __device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra
         const int hi = swap ? rb : ra;  // larger visit index: hooked
         const int lo = swap ? ra : rb;
         int expected = hi;
-        if constexpr (V == 3) atomicAdd(&g_uf_stats[2], 1ull);
         if (__hip_atomic_compare_exchange_strong(par + hi, &expected, lo, __ATOMIC_RELAXED,
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             return lo;
-        if constexpr (V == 3) atomicAdd(&g_uf_stats[3], 1ull);
         ra = uf_find<V>(par, expected);  // hi was hooked meanwhile: continue from its new parent
         rb = uf_find<V>(par, lo);
     }
@@ -470,80 +460,138 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 // by the later quarter in sorted order, and one union per connected pair.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void quarter_init_kernel(const int32_t* __restrict__ qstart,
+                                                              const uint32_t* __restrict__ qkey,
                                                               const int32_t* __restrict__ nq_p,
                                                               const int32_t* __restrict__ perm,
                                                               const uint8_t* __restrict__ core,
-                                                              int32_t* __restrict__ qrep,
+                                                              int4* __restrict__ qinfo,
+                                                              uint32_t* __restrict__ qmask,
                                                               int32_t* __restrict__ parent) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
     const int b = qstart[q], e = qstart[q + 1];
     int rep = -1, best = 0x7FFFFFFF;
+    uint32_t mask = 0;  // cores among the first 32 slots (quarters rarely hold more)
     for (int j = b; j < e; ++j)
-        if (core[j] && perm[j] < best) {
-            best = perm[j];
-            rep = j;
+        if (core[j]) {
+            if (j - b < 32) mask |= 1u << (j - b);
+            if (perm[j] < best) {
+                best = perm[j];
+                rep = j;
+            }
         }
-    qrep[q] = rep;
+    qinfo[q] = make_int4(b, e, rep, (int)qkey[q]);  // one 16-B record per quarter cell
+    qmask[q] = mask;
     if (rep < 0) return;
     for (int j = b; j < e; ++j)
         if (core[j]) parent[j] = rep;
 }
 
-__device__ __forceinline__ void quarter_xy(uint32_t key, uint32_t nx, int& gx, int& gy) {
-    const uint32_t ck = key >> 2;
-    const uint32_t cy = ck / nx, cx = ck - cy * nx;
-    gx = (int)(2 * cx + (key & 1u));
-    gy = (int)(2 * cy + ((key >> 1) & 1u));
-}
+// ABL: timing ablations for attribution only (1 no union, 2 no pair test, 3 metadata only).
+constexpr int kQReg = 8;  // own-quarter core points kept in registers for the pair tests
 
-template <int V>
+// ABL: timing ablations for attribution only (1 no union, 2 no pair test, 3 metadata only).
+template <int ABL = 0>
 __global__ __launch_bounds__(kBlock) void quarter_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ qidx,
-    const uint32_t* __restrict__ qkey, const int32_t* __restrict__ qstart,
-    const int32_t* __restrict__ qrep, const int32_t* __restrict__ nq_p, GridParams g,
-    double eps2, const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    const int4* __restrict__ qinfo, const uint32_t* __restrict__ qmask,
+    const int32_t* __restrict__ nq_p, GridParams g, double eps2,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
     int32_t* __restrict__ parent) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
-    const int rq = qrep[q];
-    if (rq < 0) return;
-    int gx, gy;
-    quarter_xy(qkey[q], g.nx, gx, gy);
-    const int qs = qstart[q], qe = qstart[q + 1];
-    const Seg s = load_seg(seg, cell[qs]);
-    int rp = uf_find<V>(parent, rq);
-    const int rb[2] = {s.b0, s.b1}, re[2] = {s.e0, s.e1};
+    const int4 me = qinfo[q];
+    if (me.z < 0) return;
+    const uint32_t key = (uint32_t)me.w, ck = key >> 2;
+    const uint32_t cy = ck / g.nx, cx = ck - cy * g.nx;
+    const int gx = (int)(2 * cx + (key & 1u)), gy = (int)(2 * cy + ((key >> 1) & 1u));
+    const Seg s = load_seg(seg, cell[me.x]);
+    // own cores in registers (the same set is tested against every neighbour quarter)
+    double px[kQReg], py[kQReg];
+    int nmine = 0;
+    const bool small = me.y - me.x <= 32;
+    {
+        uint32_t m = qmask[q];
+        const uint32_t m0 = small ? m : 0u;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {  // rows cy-1 and cy: every quarter there with a smaller key
-        if (rb[r] >= re[r]) continue;
-        const int q_lo = qidx[rb[r]], q_hi = qidx[re[r] - 1];
-        for (int q2 = q_lo; q2 <= q_hi && q2 < q; ++q2) {
-            const int r2 = qrep[q2];
-            if (r2 < 0) continue;
-            int gx2, gy2;
-            quarter_xy(qkey[q2], g.nx, gx2, gy2);
-            if (abs(gx2 - gx) > 2 || abs(gy2 - gy) > 2) continue;
-            int rr = uf_find_until<V>(parent, r2, rp);
-            if (rr == rp) continue;  // already one set: skip the pair test
-            if constexpr (V == 3) atomicAdd(&g_uf_stats[4], 1ull);
-            const int b2 = qstart[q2], e2 = qstart[q2 + 1];
-            bool found = false;
-            for (int a = qs; a < qe && !found; ++a) {
-                if (!core[a]) continue;
-                const double2 pa = xy[a];
-                for (int b = b2; b < e2; ++b) {
-                    if (!core[b]) continue;
-                    const double2 pb = xy[b];
-                    if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) {
-                        found = true;
-                        break;
+        for (int k = 0; k < kQReg; ++k) {
+            px[k] = 0.0;
+            py[k] = 0.0;
+        }
+        uint32_t mm = m0;
+#pragma unroll
+        for (int k = 0; k < kQReg; ++k) {
+            if (mm) {
+                const int j = me.x + (__ffs(mm) - 1);
+                mm &= mm - 1;
+                const double2 v = xy[j];
+                px[k] = v.x;
+                py[k] = v.y;
+                nmine = k + 1;
+            }
+        }
+        if (mm) nmine = -1;  // more than kQReg cores: generic loop below
+    }
+    const bool inreg = small && nmine >= 0;
+    int rp = uf_find<1>(parent, me.z);
+    // two sweeps: adjacent quarters (Chebyshev distance 1) first so most merges happen early
+    // and the far (distance-2) candidates are usually skipped by the find-first check
+#pragma unroll
+    for (int sweep = 0; sweep < 2; ++sweep) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {  // rows cy-1 and cy: every quarter there with a smaller key
+            const int rb = r == 0 ? s.b0 : s.b1, re = r == 0 ? s.e0 : s.e1;
+            if (rb >= re) continue;
+            const int ry = (int)cy + r - 1;
+            const int64_t rowbase = (int64_t)ry * g.nx;
+            const int q_lo = qidx[rb], q_hi = qidx[re - 1];
+            for (int q2 = q_lo; q2 <= q_hi && q2 < q; ++q2) {
+                const int4 o = qinfo[q2];
+                if (o.z < 0) continue;
+                const uint32_t k2 = (uint32_t)o.w;
+                const int gx2 = (int)(2 * ((int64_t)(k2 >> 2) - rowbase)) + (int)(k2 & 1u);
+                const int gy2 = 2 * ry + (int)((k2 >> 1) & 1u);
+                const int d = max(abs(gx2 - gx), abs(gy2 - gy));
+                if (d > 2 || (sweep == 0) != (d <= 1)) continue;
+                if constexpr (ABL == 3) {
+                    asm volatile("" ::"v"(gx2));
+                    continue;
+                }
+                const int rr = uf_find_until<1>(parent, o.z, rp);
+                if (rr == rp) continue;  // already one set: skip the pair test
+                bool found = ABL == 2;
+                if (!found && inreg && o.y - o.x <= 32) {
+                    uint32_t om = qmask[q2];
+                    while (om && !found) {
+                        const int b2 = o.x + (__ffs(om) - 1);
+                        om &= om - 1;
+                        const double2 pb = xy[b2];
+#pragma unroll
+                        for (int k = 0; k < kQReg; ++k)
+                            found |= (k < nmine) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
+                    }
+                } else if (!found) {
+                    for (int a = me.x; a < me.y && !found; ++a) {
+                        if (!core[a]) continue;
+                        const double2 pa = xy[a];
+                        for (int b2 = o.x; b2 < o.y; ++b2) {
+                            if (!core[b2]) continue;
+                            const double2 pb = xy[b2];
+                            if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) {
+                                found = true;
+                                break;
+                            }
+                        }
                     }
                 }
+                if (!found) continue;
+                if constexpr (ABL == 1) {
+                    asm volatile("" ::"v"(rr));
+                    continue;
+                }
+                rp = uf_unite_roots<1>(parent, perm, rp, rr);
             }
-            if (!found) continue;
-            rp = uf_unite_roots<V>(parent, perm, rp, rr);
         }
     }
 }
@@ -787,12 +835,14 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     int32_t* qidx = nullptr;
     uint32_t* qkey = nullptr;
     int32_t* qstart = nullptr;
-    int32_t* qrep = nullptr;
+    int4* qinfo = nullptr;
+    uint32_t* qmask = nullptr;
     if (clique) {
         qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
         qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
         qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
-        qrep = static_cast<int32_t*>(ws.qrep.ensure(nfa * sizeof(int32_t)));
+        qinfo = static_cast<int4*>(ws.qrep.ensure(nfa * sizeof(int4)));
+        qmask = static_cast<uint32_t*>(ws.qmask.ensure(nfa * sizeof(uint32_t)));
     }
 
     if (nf > 0) {
@@ -837,37 +887,21 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         {
             StageTimer t(prof, s, "quarter_init");
             hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qstart,
-                               &misc_i[3], perm, core, qrep, parent);
+                               qkey, &misc_i[3], perm, core, qinfo, qmask, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union");
-        static const int variant = [] {
-            const char* e = getenv("DBSCAN_UF_VARIANT");
-            return e ? atoi(e) : 1;
+        static const int ablate = [] {
+            const char* e = getenv("DBSCAN_UF_ABLATE");
+            return e ? atoi(e) : 0;
         }();
-        auto* kq = variant == 0   ? quarter_union_kernel<0>
-                   : variant == 2 ? quarter_union_kernel<2>
-                   : variant == 3 ? quarter_union_kernel<3>
-                   : variant == 4 ? quarter_union_kernel<4>
-                                  : quarter_union_kernel<1>;
-        if (variant == 3) {
-            unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            DBSCAN_HIP_CHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_uf_stats), z, sizeof(z), 0,
-                                                    hipMemcpyHostToDevice, s));
-        }
-        hipLaunchKernelGGL(kq, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, qidx, qkey,
-                           qstart, qrep, &misc_i[3], g, eps2, perm, core, parent);
+        auto* kq = ablate == 1   ? quarter_union_kernel<1>
+                   : ablate == 2 ? quarter_union_kernel<2>
+                   : ablate == 3 ? quarter_union_kernel<3>
+                                 : quarter_union_kernel<0>;
+        hipLaunchKernelGGL(kq, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, qidx, qinfo,
+                           qmask, &misc_i[3], g, eps2, perm, core, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
-        if (variant == 3) {
-            unsigned long long z[8];
-            int32_t nq = 0;
-            DBSCAN_HIP_CHECK(hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_uf_stats), sizeof(z), 0,
-                                                      hipMemcpyDeviceToHost, s));
-            DBSCAN_HIP_CHECK(hipMemcpyAsync(&nq, &misc_i[3], 4, hipMemcpyDeviceToHost, s));
-            DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-            fprintf(stderr, "uf stats: quarters=%d finds=%llu hops=%llu cas=%llu cas_fail=%llu "
-                    "pair_tests=%llu\n", nq, z[0], z[1], z[2], z[3], z[4]);
-        }
     } else if (nf > 0) {
         StageTimer t(prof, s, "union");
         hipLaunchKernelGGL(union_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, nf,

@@ -86,12 +86,12 @@ struct StageTimer {
 
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
-        is_root, rank, misc, qidx, qkey, qstart, qrep, blockcnt;
+        is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
-                          &qstart, &qrep, &blockcnt})
+                          &qstart, &qrep, &qmask, &blockcnt})
             b->release();
     }
 };
