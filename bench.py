@@ -29,13 +29,16 @@ sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
 METRIC = "points clustered/sec (whole node) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # SURVEY.md §8d algorithmic bytes per point, by pipeline stage (each array crosses HBM once).
+# The §8d "union" (21 B) is split over the kernels that carry it: quarter_init
+# (core 1 + perm 4 + parent 4), union_tile (xy 16 + rep parent writes ~0), union_edge and
+# union_root (tile-edge strips and quarter reps only: ~0 per point).
 ALG_BYTES = {
     "bbox": 16, "bin": 20, "sort_upsweep": 4, "sort_scan": 0, "sort_downsweep": 16,
-    "gather": 36, "cells": 8, "segs": 0, "count": 17, "union": 21, "final": 13, "rank": 5,
+    "gather": 36, "cells": 8, "tables": 0, "segs": 0, "count": 17, "quarter_init": 9,
+    "union_tile": 16, "union_edge": 0, "union_root": 0, "union": 21, "final": 13, "rank": 5,
     "output": 30,
 }
 PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
-
 
 def parse():
     ap = argparse.ArgumentParser()

@@ -1,5 +1,5 @@
-// fit.hip -- the local DBSCAN fit on gfx950: eps grid, neighbour counts, lock-free
-// union-find, border/noise labelling and cluster numbering.
+// fit.hip -- the local DBSCAN fit on gfx950: eps grid in 8x8-cell tiles, neighbour counts,
+// lock-free union-find, border/noise labelling and cluster numbering.
 //
 // Reference semantics restated here (src/main/scala/org/apache/spark/mllib/clustering/dbscan/):
 //   DBSCANPoint.scala:26-30           the fp64 predicate dx*dx + dy*dy <= eps*eps, no FMA
@@ -11,21 +11,34 @@
 //       Archery: Border of the cluster with s = m if A != {}, else Noise
 //                                                    (LocalDBSCANArchery.scala:103-106 re-claim)
 //
-// Kernels, in pipeline order (one HIP stream per handle; see DESIGN.md for the rooflines):
-//   bin        key = cy*nx + cx (u32) per point, perm = input index
-//   [radix sort (primitives.hip)]
-//   gather     sorted double2 coordinates (AoS) -- one global_load_dwordx4 per candidate test
-//   cells      occupied cells from the key head flags (scan) -> ckey, cstart, cell-of-slot
-//   segs       per cell: slot ranges of the 3 stencil rows (row-major keys make the 3 cells of a
-//              stencil row one contiguous slot range)
-//   count      thread per slot: candidate loop with early exit at minPoints -> core flag
-//   union      thread per core slot: candidates with smaller slot only (rows cy-1 and the
-//              head of row cy); lock-free union-find hooking the root with the larger visit
-//              index under the smaller (CAS, agent scope), so every root is s(K) directly
-//   final      root of every core -> lab = visit index of its root; roots flagged in input order
+// Layout.  Cells of side >= eps are grouped in 8x8-cell tiles; the sort key is
+//   tile (row-major over tiles) | cell in tile (row-major) | quadrant (2x2 quarter cells)
+// so every tile is one contiguous slot range and every cell and quarter cell is a contiguous
+// sub-range.  A dense per-tile table tslot[tile][0..64] gives the slot start of every local
+// cell, so any cell's points are found in O(1).
+//
+// Kernels, in pipeline order (one HIP stream per handle; DESIGN.md has the rooflines):
+//   bin          key per point, perm = input index            [radix sort: primitives.hip]
+//   gather       sorted double2 coordinates (AoS)
+//   groups       occupied cells / quarter cells / tiles from key head flags (3 scans)
+//   tables       tmap (tile id -> occupied tile) and tslot (per-tile cell starts)
+//   segs         per cell: up to 6 slot pieces of the 3x3 stencil (global-memory fallback)
+//   count_tile   ONE WORKGROUP PER TILE: the tile and its 1-cell halo (<= 100 cells) are staged
+//                in LDS; each point scans its 3 contiguous LDS stencil ranges, own cell first,
+//                with early exit at minPoints -> core flag
+//   quarter_init quarter cells (side ~eps/2, diagonal ~0.71 eps: cliques of the predicate):
+//                every core points at the quarter's minimum-visit-index core
+//   tile_union   ONE WORKGROUP PER TILE: union-find in LDS over the tile's quarter cells (one
+//                core-core edge per quarter pair within reach), then each tile component's
+//                quarter reps point at its minimum-visit-index core
+//   edge_union   tile-crossing quarter pairs, one wave per pair of adjacent tiles: LDS union-find
+//                over the facing strips, then one global union per joined pair of tile
+//                components (lock-free, hooking the root with the larger visit index under the
+//                smaller, so a root IS s(K)); quarter reps then point at their roots
+//   final        root of every core -> lab = s(K); roots flagged in input order
 //   [scan of root flags in input order -> rank = cluster id - 1]
-//   output     cores: rank[lab]+1; non-cores: min lab over core neighbours + Naive/Archery rule;
-//              written in input order
+//   output       cores rank[lab]+1; non-cores min lab over core neighbours + Naive/Archery
+//                rule; written in input order
 #include "internal.h"
 
 #include <cmath>
@@ -37,13 +50,12 @@ namespace dbscan {
 
 enum GridMode { kGridEps = 0, kGridAllPairs = 1, kGridNoPairs = 2 };
 
-struct GridParams {
-    double xmin2, ymin2, invx, invy;  // cell = floor((v*0.5 - vmin*0.5) * inv)
-    uint32_t nx, ny;
-    int clique;  // cell side <= eps*(1+2^-14): quarter cells are cliques of the predicate
-};
-
 namespace {
+
+constexpr int kTslot = 65;        // per-tile cell-start table stride (64 cells + end)
+constexpr int kStageCap = 3072;   // points staged per tile (48 KB of double2)
+constexpr int kQReg = 8;          // own-quarter core points kept in registers for pair tests
+constexpr int64_t kTileGrid = 8192;  // workgroups of the per-tile kernels (grid stride)
 
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
 // two rounded multiplies, one rounded add, <=.  The whole library is built with
@@ -58,29 +70,40 @@ __device__ __forceinline__ bool within_eps(double px, double py, double ox, doub
     return (a + b) <= eps2;
 }
 
-struct Seg {  // 32 B: rows dy = -1, 0, +1 as [b, e) slot ranges, then the cell's own range
-    int b0, e0, b1, e1, b2, e2, cs, ce;
+__device__ __forceinline__ void cell_xy(uint32_t ck, uint32_t ntx, uint32_t& cx, uint32_t& cy) {
+    const uint32_t t = ck >> 6, l = ck & 63u;
+    const uint32_t ty = t / ntx, tx = t - ty * ntx;
+    cx = (tx << 3) | (l & 7u);
+    cy = (ty << 3) | (l >> 3);
+}
+
+__device__ __forceinline__ int tile_occ(const int32_t* __restrict__ tmap, const GridParams& g,
+                                        int tx, int ty) {
+    if (tx < 0 || ty < 0 || tx >= (int)g.ntx || ty >= (int)g.nty) return -1;
+    return tmap[(int64_t)ty * g.ntx + tx];
+}
+
+struct Seg {  // 64 B: stencil pieces (rows cy, cy-1, cy+1; <= 2 tiles each), own cell range
+    int b[6], e[6], cs, ce, pad0, pad1;
 };
 
 __device__ __forceinline__ Seg load_seg(const Seg* seg, int c) {
     const int4* p = reinterpret_cast<const int4*>(seg + c);
-    const int4 u = p[0];
-    const int4 v = p[1];
+    const int4 u0 = p[0], u1 = p[1], u2 = p[2], u3 = p[3];
     Seg s;
-    s.b0 = u.x; s.e0 = u.y; s.b1 = u.z; s.e1 = u.w; s.b2 = v.x; s.e2 = v.y;
-    s.cs = v.z; s.ce = v.w;
+    s.b[0] = u0.x; s.b[1] = u0.y; s.b[2] = u0.z; s.b[3] = u0.w;
+    s.b[4] = u1.x; s.b[5] = u1.y; s.e[0] = u1.z; s.e[1] = u1.w;
+    s.e[2] = u2.x; s.e[3] = u2.y; s.e[4] = u2.z; s.e[5] = u2.w;
+    s.cs = u3.x; s.ce = u3.y; s.pad0 = 0; s.pad1 = 0;
     return s;
 }
 
-// Candidate iteration over up to three slot ranges [b0,e0) [b1,e1) [b2,e2) (the stencil rows).
-// f(j) returns false to stop early.
+// f(j) for every candidate slot j of the 3x3 stencil; f returns false to stop early.
 template <class F>
 __device__ __forceinline__ void for_candidates(const Seg& s, F f) {
-    const int b[3] = {s.b0, s.b1, s.b2};
-    const int e[3] = {s.e0, s.e1, s.e2};
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
-        for (int j = b[r]; j < e[r]; ++j)
+    for (int r = 0; r < 6; ++r)
+        for (int j = s.b[r]; j < s.e[r]; ++j)
             if (!f(j)) return;
 }
 
@@ -100,8 +123,10 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
         fx = fx < 0 ? 0 : (fx > mx ? mx : fx);
         fy = fy < 0 ? 0 : (fy > my ? my : fy);
         const uint32_t qx = (uint32_t)fx, qy = (uint32_t)fy;
-        const uint64_t cellk = (uint64_t)(qy >> 1) * g.nx + (qx >> 1);
-        k = (uint32_t)((cellk << 2) | ((qy & 1u) << 1) | (qx & 1u));
+        const uint32_t cx = qx >> 1, cy = qy >> 1;
+        const uint32_t tile = (cy >> 3) * g.ntx + (cx >> 3);
+        const uint32_t local = ((cy & 7u) << 3) | (cx & 7u);
+        k = (tile << 8) | (local << 2) | ((qy & 1u) << 1) | (qx & 1u);
     }
     key[i] = k;
     perm[i] = (int32_t)i;
@@ -126,244 +151,340 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
     xy[p] = make_double2(x[o], y[o]);
 }
 
-// cell[p] holds the exclusive scan of head flags on entry; converted to the group index.
-// shift = 2: eps cells (key >> 2); shift = 0: quarter cells (full key).
-__global__ __launch_bounds__(kBlock) void cells_kernel(const uint32_t* __restrict__ key,
+// gidx[p] holds the exclusive scan of head flags on entry; converted to the group index.
+// shift = 0: quarter cells (full key); 2: eps cells; 8: tiles.
+__global__ __launch_bounds__(kBlock) void group_kernel(const uint32_t* __restrict__ key,
                                                        int shift, int64_t nf,
-                                                       int32_t* __restrict__ cell,
-                                                       uint32_t* __restrict__ ckey,
-                                                       int32_t* __restrict__ cstart,
-                                                       const int32_t* __restrict__ ncells) {
+                                                       int32_t* __restrict__ gidx,
+                                                       uint32_t* __restrict__ gkey,
+                                                       int32_t* __restrict__ gstart,
+                                                       const int32_t* __restrict__ ngroups) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= nf) {
-        if (p == nf) cstart[*ncells] = (int32_t)nf;
+        if (p == nf) gstart[*ngroups] = (int32_t)nf;
         return;
     }
-    const int32_t ex = cell[p];
+    const int32_t ex = gidx[p];
     const bool head = (p == 0) || (key[p] >> shift) != (key[p - 1] >> shift);
     if (head) {
-        ckey[ex] = key[p] >> shift;
-        cstart[ex] = (int32_t)p;
+        gkey[ex] = key[p] >> shift;
+        gstart[ex] = (int32_t)p;
     }
-    cell[p] = ex + (head ? 1 : 0) - 1;
+    gidx[p] = ex + (head ? 1 : 0) - 1;
 }
 
-__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t k) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = lo + ((hi - lo) >> 1);
-        if (a[mid] < k) lo = mid + 1; else hi = mid;
-    }
-    return lo;
+__global__ __launch_bounds__(kBlock) void tmap_kernel(const uint32_t* __restrict__ tkey,
+                                                      const int32_t* __restrict__ ntiles_p,
+                                                      int32_t* __restrict__ tmap) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t < *ntiles_p) tmap[tkey[t]] = t;
 }
 
+// tslot[t][l] = first slot of the first occupied cell of tile t with local index >= l
+// (tile end if none): the slots of local cells [l0, l1] are [tslot[l0], tslot[l1 + 1]).
+__global__ __launch_bounds__(kBlock) void tslot_kernel(
+    const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
+    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ cell,
+    const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
+    const int32_t* __restrict__ ncells_p, int32_t* __restrict__ tslot) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= *ntiles_p) return;
+    const int C = *ncells_p;
+    const uint32_t tk = tkey[t];
+    int32_t* ts = tslot + (int64_t)t * kTslot;
+    int pos = 0;
+    for (int c = cell[tstart[t]]; c < C && (ckey[c] >> 6) == tk; ++c) {
+        const int l = (int)(ckey[c] & 63u);
+        const int st = cstart[c];
+        while (pos <= l) ts[pos++] = st;
+    }
+    const int end = tstart[t + 1];
+    while (pos < kTslot) ts[pos++] = end;
+}
+
+// Per cell: the stencil's slot pieces (rows cy, cy-1, cy+1; a row of 3 cells splits in two
+// where it crosses a tile edge) and the cell's own range.  Used by the global-memory paths.
 __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict__ ckey,
                                                       const int32_t* __restrict__ cstart,
                                                       const int32_t* __restrict__ ncells_p,
+                                                      const int32_t* __restrict__ tmap,
+                                                      const int32_t* __restrict__ tslot,
                                                       GridParams g, Seg* __restrict__ seg) {
     const int c = blockIdx.x * kBlock + threadIdx.x;
-    const int C = *ncells_p;
-    if (c >= C) return;
-    const uint32_t key = ckey[c];
-    const uint32_t cy = key / g.nx, cx = key - cy * g.nx;
-    const uint32_t lox = cx > 0 ? cx - 1 : cx;
-    const uint32_t hix = cx + 1 < g.nx ? cx + 1 : cx;
-    int rb[3], re[3];
+    if (c >= *ncells_p) return;
+    uint32_t cx, cy;
+    cell_xy(ckey[c], g.ntx, cx, cy);
+    const uint32_t lox = cx > 0 ? cx - 1 : cx, hix = cx + 1 < g.nx ? cx + 1 : cx;
+    Seg s;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        s.b[k] = 0;
+        s.e[k] = 0;
+    }
+    const int rows[3] = {(int)cy, (int)cy - 1, (int)cy + 1};
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        rb[r] = 0;
-        re[r] = 0;
-        const int64_t ry = (int64_t)cy + r - 1;
-        if (ry < 0 || ry >= (int64_t)g.ny) continue;
-        const uint32_t klo = (uint32_t)ry * g.nx + lox, khi = (uint32_t)ry * g.nx + hix;
-        int a, z;
-        if (r == 1) {  // own row: neighbours are adjacent entries of ckey
-            a = (c > 0 && ckey[c - 1] == klo && lox != cx) ? c - 1 : c;
-            z = (c + 1 < C && ckey[c + 1] == khi && hix != cx) ? c + 2 : c + 1;
-        } else {
-            a = lower_bound_u32(ckey, C, klo);
-            z = a;
-            while (z < C && ckey[z] <= khi) ++z;
+        const int ry = rows[r];
+        if (ry < 0 || ry >= (int)g.ny) continue;
+        const int ty = ry >> 3, ly = ry & 7;
+        const int txa = (int)(lox >> 3), txb = (int)(hix >> 3);
+        int occ = tile_occ(tmap, g, txa, ty);
+        if (occ >= 0) {
+            const int l0 = ly * 8 + (int)(lox & 7u);
+            const int l1 = ly * 8 + (txa == txb ? (int)(hix & 7u) : 7);
+            s.b[2 * r] = tslot[(int64_t)occ * kTslot + l0];
+            s.e[2 * r] = tslot[(int64_t)occ * kTslot + l1 + 1];
         }
-        rb[r] = cstart[a];
-        re[r] = cstart[z];
+        if (txb != txa) {
+            occ = tile_occ(tmap, g, txb, ty);
+            if (occ >= 0) {
+                s.b[2 * r + 1] = tslot[(int64_t)occ * kTslot + ly * 8];
+                s.e[2 * r + 1] = tslot[(int64_t)occ * kTslot + ly * 8 + (int)(hix & 7u) + 1];
+            }
+        }
     }
-    Seg s;
-    s.b0 = rb[0]; s.e0 = re[0]; s.b1 = rb[1]; s.e1 = re[1]; s.b2 = rb[2]; s.e2 = re[2];
-    s.cs = cstart[c]; s.ce = cstart[c + 1];
+    s.cs = cstart[c];
+    s.ce = cstart[c + 1];
+    s.pad0 = 0;
+    s.pad1 = 0;
     seg[c] = s;
 }
 
 // ---------------------------------------------------------------------------------------
-// Block staging of stencil candidates in LDS.  Slots are in row-major cell-key order, so the
-// 256 slots of a block usually cover a run of cells [c0, c1] of ONE cell row; the candidates
-// of all of them are then the three contiguous slot ranges of rows cy-1, cy, cy+1 spanning
-// cells cx0-1 .. cx1+1.  Those are loaded once (coalesced 16-B loads) into LDS and every
-// thread's candidate loop reads LDS instead of issuing dependent global gathers.  Blocks that
-// straddle two cell rows, or whose candidates exceed the LDS budget, read global memory.
+// Tile staging: a tile and its 1-cell halo as a 10x10 "extended" cell grid in LDS.  Extended
+// cell k = (ey+1)*10 + (ex+1), ex, ey in -1..8; cells are stored in k order, so extended row ey
+// is contiguous and a point at local cell (lx, ly) finds each of its 3 stencil rows as ONE LDS
+// range [off[(ey+1)*10 + lx], off[(ey+1)*10 + lx + 3]).  Tiles whose tile+halo exceeds
+// kStageCap points (dense data) fall back to the global-memory path.
+// The per-tile kernels loop over occupied tiles with a grid stride (the tile count is only
+// known on the device); every loop trip ends in a barrier before the stage is overwritten.
 // ---------------------------------------------------------------------------------------
-constexpr int kStageCap = 3072;  // points (48 KB of double2)
-
-struct StageInfo {
-    int ok;          // 1: the block's candidates are in LDS
-    int B[3], E[3];  // global slot range of each stencil row
-    int off[3];      // LDS offset of each row's first point
+struct TileStage {
+    int ok, total, ts, te, t;
+    int cb[100];   // global slot begin of each extended cell
+    int off[101];  // LDS offset of each extended cell
+    int cn[100];
 };
 
-__device__ __forceinline__ int row_of(uint32_t ck, uint32_t nx) { return (int)(ck / nx); }
-
-// Fills `st` (LDS) and stages candidates into `buf` (LDS).  All threads must call it.
-__device__ void stage_block(const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-                            const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
-                            int C, int64_t p0, int64_t p1, GridParams g, StageInfo& st,
-                            double2* buf) {
-    if (threadIdx.x < 3) {
-        const int r = threadIdx.x;
-        const int c0 = cell[p0], c1 = cell[p1 - 1];
-        const uint32_t k0 = ckey[c0], k1 = ckey[c1];
-        const int cy = row_of(k0, g.nx);
-        int ok = row_of(k1, g.nx) == cy;
-        int B = 0, E = 0;
-        const int64_t ry = (int64_t)cy + r - 1;
-        if (ok && ry >= 0 && ry < (int64_t)g.ny) {
-            const uint32_t cx0 = k0 - (uint32_t)cy * g.nx, cx1 = k1 - (uint32_t)cy * g.nx;
-            const uint32_t lo = (uint32_t)ry * g.nx + (cx0 > 0 ? cx0 - 1 : 0);
-            const uint32_t hi = (uint32_t)ry * g.nx + (cx1 + 1 < g.nx ? cx1 + 1 : cx1);
-            int a = lower_bound_u32(ckey, C, lo);
-            int z = lower_bound_u32(ckey, C, hi + 1);
-            B = cstart[a];
-            E = cstart[z];
+__device__ bool stage_tile(int t, const double2* __restrict__ xy,
+                           const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
+                           const int32_t* __restrict__ tmap, const int32_t* __restrict__ tslot,
+                           const GridParams& g, TileStage& st, double2* buf) {
+    const int tid = threadIdx.x;
+    if (tid < 100) {
+        const uint32_t tk = tkey[t];
+        const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
+        const int ey = tid / 10 - 1, ex = tid % 10 - 1;
+        const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
+        const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
+        const int occ = tile_occ(tmap, g, tx, ty);
+        int b = 0, cnt = 0;
+        if (occ >= 0) {
+            const int l = (ey & 7) * 8 + (ex & 7);
+            b = tslot[(int64_t)occ * kTslot + l];
+            cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
         }
-        st.B[r] = B;
-        st.E[r] = E;
-        if (r == 0) st.ok = ok;
+        st.cb[tid] = b;
+        st.cn[tid] = cnt;
+    }
+    if (tid == 0) {
+        st.ts = tstart[t];
+        st.te = tstart[t + 1];
+        st.t = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int n0 = st.E[0] - st.B[0], n1 = st.E[1] - st.B[1], n2 = st.E[2] - st.B[2];
-        st.off[0] = 0;
-        st.off[1] = n0;
-        st.off[2] = n0 + n1;
-        if (n0 + n1 + n2 > kStageCap) st.ok = 0;
+    if (tid < 64) {  // exclusive scan of the 100 counts by wave 0 (2 chunks)
+        int carry = 0;
+        for (int base = 0; base < 100; base += 64) {
+            const int i = base + tid;
+            const int v = i < 100 ? st.cn[i] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += u;
+            }
+            if (i < 100) st.off[i] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (tid == 0) {
+            st.off[100] = carry;
+            st.total = carry;
+            st.ok = carry <= kStageCap;
+        }
     }
     __syncthreads();
     if (st.ok) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int B = st.B[r], n = st.E[r] - B, o = st.off[r];
-            for (int t = threadIdx.x; t < n; t += kBlock) buf[o + t] = xy[B + t];
+        const int total = st.total;
+        for (int i = tid; i < total; i += kBlock) {
+            int lo = 0, hi = 99;  // largest k with off[k] <= i
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (st.off[mid] <= i) lo = mid; else hi = mid - 1;
+            }
+            buf[i] = xy[st.cb[lo] + (i - st.off[lo])];
         }
     }
     __syncthreads();
+    return st.ok;
+}
+
+struct LdsRanges {  // a point's stencil in LDS: rows ly, ly-1, ly+1 and its own cell
+    int b[3], e[3], cs, ce;
+};
+
+__device__ __forceinline__ LdsRanges lds_ranges(const TileStage& st, int l) {
+    const int lx = l & 7, ly = l >> 3;
+    LdsRanges r;
+    const int rows[3] = {ly, ly - 1, ly + 1};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int base = (rows[k] + 1) * 10 + lx;
+        r.b[k] = st.off[base];
+        r.e[k] = st.off[base + 3];
+    }
+    const int own = (ly + 1) * 10 + lx + 1;
+    r.cs = st.off[own];
+    r.ce = st.off[own + 1];
+    return r;
 }
 
 // ---------------------------------------------------------------------------------------
-// Neighbour counts -> core flags (LocalDBSCANNaive.scala:52-54, :99-101), with early exit
-// once minPoints neighbours are seen (the count itself is never an output).
-// zone (optional, slab fits): zone-2 points are halo-only candidates -> never core.
+// Neighbour counts -> core flags (LocalDBSCANNaive.scala:52-54, :99-101), with early exit once
+// minPoints neighbours are seen (the count itself is never an output).  Own cell first, then
+// the rest of its row, then the rows below and above; 8 candidates per batch.
 // ---------------------------------------------------------------------------------------
-template <bool STAGED>
-__device__ __forceinline__ bool count_ranges(const double2* __restrict__ src, const Seg& s,
-                                             const StageInfo& st, double2 me, double eps2,
-                                             int min_points, int& cnt) {
-    // own cell first (most likely neighbours -> earliest exit), then the rest of its row,
-    // then the rows below and above; 8 candidates per batch
-    auto map = [&](int j, int r) -> int { return STAGED ? j - st.B[r] + st.off[r] : j; };
-    auto scan = [&](int b, int e, int r) -> bool {
-        int j = b;
-        for (; j + 8 <= e; j += 8) {
-            const int m0 = map(j, r);
-            double2 qq[8];
+template <class Src>
+__device__ __forceinline__ bool scan_count(const Src* __restrict__ src, int b, int e,
+                                           double2 me, double eps2, int min_points, int& cnt) {
+    int j = b;
+    for (; j + 8 <= e; j += 8) {
+        double2 qq[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) qq[u] = src[m0 + u];
+        for (int u = 0; u < 8; ++u) qq[u] = src[j + u];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                cnt += within_eps(me.x, me.y, qq[u].x, qq[u].y, eps2) ? 1 : 0;
-            if (cnt >= min_points) return true;
-        }
-        for (; j < e; ++j) {
-            const double2 q = src[map(j, r)];
-            cnt += within_eps(me.x, me.y, q.x, q.y, eps2) ? 1 : 0;
-        }
-        return cnt >= min_points;
-    };
-    return scan(s.cs, s.ce, 1) || scan(s.b1, s.cs, 1) || scan(s.ce, s.e1, 1) ||
-           scan(s.b0, s.e0, 0) || scan(s.b2, s.e2, 2);
+        for (int u = 0; u < 8; ++u) cnt += within_eps(me.x, me.y, qq[u].x, qq[u].y, eps2) ? 1 : 0;
+        if (cnt >= min_points) return true;
+    }
+    for (; j < e; ++j) {
+        const double2 q = src[j];
+        cnt += within_eps(me.x, me.y, q.x, q.y, eps2) ? 1 : 0;
+    }
+    return cnt >= min_points;
 }
 
-__global__ __launch_bounds__(kBlock) void count_kernel(const double2* __restrict__ xy,
-                                                       const int32_t* __restrict__ cell,
-                                                       const Seg* __restrict__ seg,
-                                                       const uint32_t* __restrict__ ckey,
-                                                       const int32_t* __restrict__ cstart,
-                                                       const int32_t* __restrict__ ncells_p,
-                                                       GridParams g, int64_t n, int64_t nf,
-                                                       double eps2, int32_t min_points,
-                                                       const int32_t* __restrict__ perm,
-                                                       const uint8_t* __restrict__ zone,
-                                                       const int32_t* __restrict__ qidx,
-                                                       const int32_t* __restrict__ qstart,
-                                                       uint8_t* __restrict__ core,
-                                                       int32_t* __restrict__ parent,
-                                                       int32_t* __restrict__ block_cores) {
-    __shared__ StageInfo st;
-    __shared__ int wcores[kBlock / 64];
+// one count over ranges (b[k], e[k]) with the own cell [cs, ce) first and excluded after
+template <int K>
+__device__ __forceinline__ void count_pieces(const double2* __restrict__ src, const int* b,
+                                             const int* e, int cs, int ce, double2 me,
+                                             double eps2, int min_points, int& cnt) {
+    if (scan_count(src, cs, ce, me, eps2, min_points, cnt)) return;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int lo = b[k], hi = e[k];
+        if (lo <= cs && ce <= hi) {  // the piece holding the own cell: around it
+            if (scan_count(src, lo, cs, me, eps2, min_points, cnt)) return;
+            if (scan_count(src, ce, hi, me, eps2, min_points, cnt)) return;
+        } else if (scan_count(src, lo, hi, me, eps2, min_points, cnt)) {
+            return;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void count_tile_kernel(
+    const double2* __restrict__ xy, const uint32_t* __restrict__ key,
+    const int32_t* __restrict__ cell, const Seg* __restrict__ seg,
+    const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
+    const int32_t* __restrict__ tmap, const int32_t* __restrict__ tslot,
+    const int32_t* __restrict__ ntiles_p, GridParams g, double eps2, int32_t min_points,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
+    const int32_t* __restrict__ qidx, const int32_t* __restrict__ qstart,
+    uint8_t* __restrict__ core, int32_t* __restrict__ parent, int32_t* __restrict__ block_cores) {
+    __shared__ TileStage st;
     __shared__ double2 buf[kStageCap];
-    const int64_t p0 = (int64_t)blockIdx.x * kBlock;
-    const int64_t p = p0 + threadIdx.x;
-    // stage only blocks entirely inside the grid (block-uniform condition)
-    const bool stage = min_points > 0 && p0 + kBlock <= nf;
-    if (stage) stage_block(xy, cell, ckey, cstart, *ncells_p, p0, p0 + kBlock, g, st, buf);
-    bool is_core = false;
-    if (p >= n) {
-        // no neighbours to count
-    } else if (zone && zone[perm[p]] == 2) {
-        is_core = false;
-    } else if (min_points <= 0) {
-        is_core = true;
-    } else if (p >= nf) {
-        is_core = false;  // outside the grid: no neighbours, not even itself
-    } else {
-        const int32_t c = cell[p];
-        const double2 me = xy[p];
-        const int32_t q = qidx ? qidx[p] : 0;
-        const Seg s = load_seg(seg, c);
-        // a clique quarter holding >= minPoints points (a dense box): core without a test
-        const bool dense = qidx && (qstart[q + 1] - qstart[q] >= min_points);
-        int cnt = dense ? min_points : 0;
-        if (!dense) {
-            if (stage && st.ok)
-                count_ranges<true>(buf, s, st, me, eps2, min_points, cnt);
-            else
-                count_ranges<false>(xy, s, st, me, eps2, min_points, cnt);
+    __shared__ int wcores[kBlock / 64];
+    const int ntiles = *ntiles_p;
+    int mine = 0;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const bool staged = stage_tile(t, xy, tstart, tkey, tmap, tslot, g, st, buf);
+        for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
+            bool is_core;
+            if (zone && zone[perm[p]] == 2) {
+                is_core = false;  // outer halo of a slab fit: a count candidate only
+            } else if (min_points <= 0) {
+                is_core = true;
+            } else {
+                const double2 me = xy[p];
+                // a clique quarter holding >= minPoints points (a dense box): core, no test
+                int cnt = 0;
+                if (qidx) {
+                    const int q = qidx[p];
+                    if (qstart[q + 1] - qstart[q] >= min_points) cnt = min_points;
+                }
+                if (cnt < min_points) {
+                    if (staged) {
+                        const LdsRanges r = lds_ranges(st, (int)((key[p] >> 2) & 63u));
+                        count_pieces<3>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points, cnt);
+                    } else {
+                        const Seg s = load_seg(seg, cell[p]);
+                        count_pieces<6>(xy, s.b, s.e, s.cs, s.ce, me, eps2, min_points, cnt);
+                    }
+                }
+                is_core = cnt >= min_points;
+            }
+            parent[p] = p;
+            core[p] = is_core ? 1 : 0;
+            mine += is_core ? 1 : 0;
         }
-        is_core = cnt >= min_points;
+        __syncthreads();
     }
-    if (p < n) {
-        parent[p] = (int32_t)p;
-        core[p] = is_core ? 1 : 0;
-    }
-    // per-block core count (no same-address atomics: 156K of them cost ~1.7 ms at 10^7 points)
-    const uint64_t cm = __ballot(is_core);
-    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = (int)__popcll(cm);
+    // per-block core count (same-address atomics from every wave cost ~1.7 ms at 10^7 points)
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int t = 0;
-        for (int w = 0; w < kBlock / 64; ++w) t += wcores[w];
-        block_cores[blockIdx.x] = t;
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        block_cores[blockIdx.x] = tot;
+    }
+}
+
+// Slots outside the grid (non-finite coordinates, or every slot when eps*eps is NaN): no
+// neighbours, not even themselves.
+__global__ __launch_bounds__(kBlock) void count_rest_kernel(int64_t nf, int64_t n,
+                                                            int32_t min_points,
+                                                            const int32_t* __restrict__ perm,
+                                                            const uint8_t* __restrict__ zone,
+                                                            uint8_t* __restrict__ core,
+                                                            int32_t* __restrict__ parent,
+                                                            int32_t* __restrict__ block_cores) {
+    __shared__ int wcores[kBlock / 64];
+    const int64_t p = nf + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int mine = 0;
+    if (p < n) {
+        const bool is_core = min_points <= 0 && !(zone && zone[perm[p]] == 2);
+        parent[p] = (int32_t)p;
+        core[p] = is_core ? 1 : 0;
+        mine = is_core ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        block_cores[blockIdx.x] = tot;
     }
 }
 
 // ---------------------------------------------------------------------------------------
 // Lock-free union-find over slots.  parent pointers always lead to a strictly smaller visit
 // index (perm), so there are no cycles and a root is the minimum-index core of its set.
-// Loads/stores are agent-scope relaxed atomics (L1-bypassing), hooks are CAS on roots only;
-// stale reads only ever show an older ancestor, which is still an ancestor.
+// Only CAS hooks write roots; stale reads only ever show an older ancestor (still an
+// ancestor), so plain loads are safe.
+// V = 0: agent-scope atomic loads (L1-bypassing) with path-halving stores (per-point fallback);
+// V = 1: plain L1-cacheable loads, no stores (quarter unions; measured faster, r01 notes).
 // ---------------------------------------------------------------------------------------
-// UF load policy (template parameter V): 0 = agent-scope atomic loads (L1-bypassing) with
-// path-halving stores (per-point fallback union); 1 = plain L1-cacheable loads, no stores
-// (quarter union; measured 2.4 vs 5.0 ms, tools/uf_variants.sh).  Stale copies are older
-// ancestors, which are still ancestors, so both are correct; only CAS hooks write roots.
 template <int V>
 __device__ __forceinline__ int ld_par(int* par, int i) {
     if constexpr (V == 1) {
@@ -424,6 +545,8 @@ __device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra
     return ra;
 }
 
+// Per-point union (used when quarter cells are not cliques: grown grid, all-pairs mode).
+// Each core-core edge once: from the endpoint with the larger slot.
 __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict__ xy,
                                                        const int32_t* __restrict__ cell,
                                                        const Seg* __restrict__ seg, int64_t nf,
@@ -434,13 +557,10 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= nf || !core[p]) return;
     const double2 me = xy[p];
-    Seg s = load_seg(seg, cell[p]);
-    // only slots < p: row cy-1 entirely, row cy up to p, row cy+1 never
-    s.e1 = (int)p;
-    s.b2 = 0;
-    s.e2 = 0;
+    const Seg s = load_seg(seg, cell[p]);
     int rp = uf_find(parent, (int)p);
     for_candidates(s, [&](int j) {
+        if (j >= (int)p) return true;
         const double2 q = xy[j];
         if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
             const int rj = uf_find(parent, j);
@@ -453,20 +573,15 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 // ---------------------------------------------------------------------------------------
 // Clique-quarter union (cell side <= eps*(1+2^-14)).  A quarter cell has side ~eps/2 and
 // diagonal ~0.71*eps, so any two of its points satisfy the fp64 predicate: its cores are one
-// connected set without a single distance test.  quarter_init points every core of a quarter at
-// the quarter's minimum-visit-index core (a valid union-find state: pointers go to a smaller
-// visit index); quarter_union then needs ONE core-core edge per pair of quarter cells within
-// reach (offsets <= 2 on the quarter grid, i.e. inside the 3x3 eps-cell stencil), examined once
-// by the later quarter in sorted order, and one union per connected pair.
+// connected set without a single distance test.  Two quarter cells can hold an eps pair only
+// if their quarter-grid offsets are <= 2 (inside the 3x3 eps-cell stencil); ONE core-core
+// edge per such pair suffices.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void quarter_init_kernel(const int32_t* __restrict__ qstart,
-                                                              const uint32_t* __restrict__ qkey,
-                                                              const int32_t* __restrict__ nq_p,
-                                                              const int32_t* __restrict__ perm,
-                                                              const uint8_t* __restrict__ core,
-                                                              int4* __restrict__ qinfo,
-                                                              uint32_t* __restrict__ qmask,
-                                                              int32_t* __restrict__ parent) {
+__global__ __launch_bounds__(kBlock) void quarter_init_kernel(
+    const int32_t* __restrict__ qstart, const uint32_t* __restrict__ qkey,
+    const int32_t* __restrict__ nq_p, GridParams g, const int32_t* __restrict__ perm,
+    const uint8_t* __restrict__ core, int4* __restrict__ qinfo, int2* __restrict__ qg,
+    int32_t* __restrict__ parent) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
     const int b = qstart[q], e = qstart[q + 1];
@@ -480,120 +595,312 @@ __global__ __launch_bounds__(kBlock) void quarter_init_kernel(const int32_t* __r
                 rep = j;
             }
         }
-    qinfo[q] = make_int4(b, e, rep, (int)qkey[q]);  // one 16-B record per quarter cell
-    qmask[q] = mask;
+    const uint32_t k = qkey[q];
+    uint32_t cx, cy;
+    cell_xy(k >> 2, g.ntx, cx, cy);
+    qinfo[q] = make_int4(b, e, rep, (int)mask);
+    qg[q] = make_int2((int)(2 * cx + (k & 1u)), (int)(2 * cy + ((k >> 1) & 1u)));
     if (rep < 0) return;
     for (int j = b; j < e; ++j)
         if (core[j]) parent[j] = rep;
 }
 
-// ABL: timing ablations for attribution only (1 no union, 2 no pair test, 3 metadata only).
-constexpr int kQReg = 8;  // own-quarter core points kept in registers for the pair tests
+// Does any core of quarter A (points in registers: px/py, n) lie within eps of a core of B?
+template <class Src>
+__device__ __forceinline__ bool pair_found(const double* px, const double* py, int na,
+                                           const Src* __restrict__ src, int b0, int b1,
+                                           uint32_t bmask, const uint8_t* __restrict__ core,
+                                           int boff, double eps2) {
+    if (b1 - b0 <= 32) {
+        uint32_t m = bmask;
+        while (m) {
+            const int j = __ffs(m) - 1;
+            m &= m - 1;
+            const double2 pb = src[b0 - boff + j];
+            bool f = false;
+#pragma unroll
+            for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
+            if (f) return true;
+        }
+        return false;
+    }
+    for (int j = b0; j < b1; ++j) {
+        if (!core[j]) continue;
+        const double2 pb = src[j - boff];
+        bool f = false;
+#pragma unroll
+        for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
+        if (f) return true;
+    }
+    return false;
+}
 
-// ABL: timing ablations for attribution only (1 no union, 2 no pair test, 3 metadata only).
-template <int ABL = 0>
-__global__ __launch_bounds__(kBlock) void quarter_union_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, const int32_t* __restrict__ qidx,
-    const int4* __restrict__ qinfo, const uint32_t* __restrict__ qmask,
-    const int32_t* __restrict__ nq_p, GridParams g, double eps2,
+// own quarter's cores into registers; returns the count, or -1 if > kQReg (generic path)
+template <class Src>
+__device__ __forceinline__ int load_own(const Src* __restrict__ src, int4 me, int off,
+                                        double* px, double* py) {
+#pragma unroll
+    for (int k = 0; k < kQReg; ++k) {
+        px[k] = 0.0;
+        py[k] = 0.0;
+    }
+    if (me.y - me.x > 32) return -1;
+    uint32_t m = (uint32_t)me.w;
+    int na = 0;
+#pragma unroll
+    for (int k = 0; k < kQReg; ++k) {
+        if (m) {
+            const int j = __ffs(m) - 1;
+            m &= m - 1;
+            const double2 v = src[me.x - off + j];
+            px[k] = v.x;
+            py[k] = v.y;
+            na = k + 1;
+        }
+    }
+    return m ? -1 : na;
+}
+
+// generic pair test when a quarter holds more than kQReg cores (dense data)
+template <class Src>
+__device__ bool pair_found_generic(const Src* __restrict__ src, int off, int4 a, int4 b,
+                                   const uint8_t* __restrict__ core, double eps2) {
+    for (int i = a.x; i < a.y; ++i) {
+        if (!core[i]) continue;
+        const double2 pa = src[i - off];
+        for (int j = b.x; j < b.y; ++j) {
+            if (!core[j]) continue;
+            const double2 pb = src[j - off];
+            if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) return true;
+        }
+    }
+    return false;
+}
+
+// LDS union-find over the tile's quarter cells (local indices; hook larger under smaller).
+__device__ __forceinline__ int lfind(int* lp, int x) {
+    while (true) {
+        const int p = lp[x];
+        if (p == x) return x;
+        const int gp = lp[p];
+        if (gp != p) lp[x] = gp;
+        x = gp;
+    }
+}
+__device__ __forceinline__ void lunite(int* lp, int a, int b) {
+    for (;;) {
+        a = lfind(lp, a);
+        b = lfind(lp, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(&lp[a], a, b) == a) return;
+    }
+}
+
+constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
+
+__global__ __launch_bounds__(kBlock) void tile_union_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
+    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ qidx,
+    const int4* __restrict__ qinfo, const int2* __restrict__ qg, double eps2,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
     int32_t* __restrict__ parent) {
+    __shared__ int lp[kMaxTileQ];
+    __shared__ int4 lqi[kMaxTileQ];
+    __shared__ int qmap[kMaxTileQ];  // 16x16 local quarter grid -> local quarter index
+    __shared__ int cmin[kMaxTileQ];
+    __shared__ int crep[kMaxTileQ];
+    __shared__ double2 buf[kStageCap];
+    const int ntiles = *ntiles_p;
+    const int i = threadIdx.x;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int ts = tstart[t], te = tstart[t + 1];
+        const int q0 = qidx[ts], nq = qidx[te - 1] + 1 - q0;
+        const bool staged = te - ts <= kStageCap;
+        qmap[i] = -1;
+        cmin[i] = 0x7FFFFFFF;
+        if (staged)
+            for (int k = i; k < te - ts; k += kBlock) buf[k] = xy[ts + k];
+        __syncthreads();
+        int lqx = 0, lqy = 0, prio = 0x7FFFFFFF;
+        int4 me = make_int4(0, 0, -1, 0);
+        if (i < nq) {
+            me = qinfo[q0 + i];
+            const int2 gq = qg[q0 + i];
+            lqx = gq.x & 15;
+            lqy = gq.y & 15;
+            lqi[i] = me;
+            lp[i] = i;
+            qmap[lqy * 16 + lqx] = i;
+            if (me.z >= 0) prio = perm[me.z];
+        }
+        __syncthreads();
+        if (i < nq && me.z >= 0) {
+            const double2* src = staged ? buf : xy;
+            const int off = staged ? ts : 0;
+            double px[kQReg], py[kQReg];
+            const int na = load_own(src, me, off, px, py);
+            // adjacent quarters first (merges happen early), then the distance-2 ring
+#pragma unroll
+            for (int sweep = 1; sweep <= 2; ++sweep)
+                for (int dy = -2; dy <= 2; ++dy)
+                    for (int dx = -2; dx <= 2; ++dx) {
+                        if (max(abs(dx), abs(dy)) != sweep) continue;
+                        const int ux = lqx + dx, uy = lqy + dy;
+                        if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+                        const int j = qmap[uy * 16 + ux];
+                        if (j < 0 || j >= i) continue;  // each pair once, from the larger index
+                        const int4 o = lqi[j];
+                        if (o.z < 0) continue;
+                        if (lfind(lp, i) == lfind(lp, j)) continue;
+                        const bool f = na >= 0 ? pair_found(px, py, na, src, o.x, o.y,
+                                                            (uint32_t)o.w, core, off, eps2)
+                                               : pair_found_generic(src, off, me, o, core, eps2);
+                        if (f) lunite(lp, i, j);
+                    }
+        }
+        __syncthreads();
+        int r = -1;
+        if (i < nq && me.z >= 0) {
+            r = lfind(lp, i);
+            atomicMin(&cmin[r], prio);
+        }
+        __syncthreads();
+        if (r >= 0 && prio == cmin[r]) crep[r] = me.z;
+        __syncthreads();
+        // quarter reps (roots after quarter_init) now point at their tile component's rep
+        if (r >= 0 && crep[r] != me.z) parent[me.z] = crep[r];
+        __syncthreads();
+    }
+}
+
+// Quarter pairs that cross a tile edge.  One wave per (tile, relation): E (tx+1, ty),
+// S (tx, ty+1), SE (tx+1, ty+1), SW (tx-1, ty+1) -- with the mirrored relations of the other
+// tiles, every pair of adjacent tiles exactly once.  The wave loads the quarter cells of the
+// two facing cell strips (<= 8 cells = 32 quarters per side) into LDS, tags each with its tile
+// component (parent of its rep after tile_union), pre-joins equal tags in an LDS union-find,
+// then pair-tests facing quarters within quarter distance 2 (adjacent first) only while the
+// two are not yet joined in LDS.  A found edge is one global union of the two tile components,
+// so the global union-find sees about one operation per component pair per tile edge.
+constexpr int kEdgeNodes = 64;
+
+__global__ __launch_bounds__(kBlock) void edge_union_kernel(
+    const double2* __restrict__ xy, const uint32_t* __restrict__ tkey,
+    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ tmap,
+    const int32_t* __restrict__ tslot, const int32_t* __restrict__ qidx,
+    const int4* __restrict__ qinfo, const int2* __restrict__ qg, GridParams g, double eps2,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    int32_t* __restrict__ parent) {
+    __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
+    __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
+    __shared__ int ncomp[kBlock / 64][kEdgeNodes];
+    __shared__ int nlp[kBlock / 64][kEdgeNodes];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int dtx = (w == 0 || w == 2) ? 1 : (w == 3 ? -1 : 0);
+    const int dty = w == 0 ? 0 : 1;
+    const int ntiles = *ntiles_p;
+    int* lp = nlp[w];
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t tk = tkey[t];
+        const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
+        const int occB = tile_occ(tmap, g, tx + dtx, ty + dty);  // wave-uniform
+        int nA = 0, ntot = 0;
+        if (occB >= 0) {
+            const int side = lane >> 3, k = lane & 7;
+            const int ncell = w < 2 ? 8 : 1;
+            int cnt = 0, q0 = 0;
+            if (lane < 16 && k < ncell) {
+                int lxA, lyA, lxB, lyB;
+                if (w == 0) { lxA = 7; lyA = k; lxB = 0; lyB = k; }
+                else if (w == 1) { lxA = k; lyA = 7; lxB = k; lyB = 0; }
+                else if (w == 2) { lxA = 7; lyA = 7; lxB = 0; lyB = 0; }
+                else { lxA = 0; lyA = 7; lxB = 7; lyB = 0; }
+                const int occ = side ? occB : t;
+                const int l = side ? lyB * 8 + lxB : lyA * 8 + lxA;
+                const int b = tslot[(int64_t)occ * kTslot + l];
+                const int e = tslot[(int64_t)occ * kTslot + l + 1];
+                if (b < e) {
+                    q0 = qidx[b];
+                    cnt = qidx[e - 1] + 1 - q0;
+                }
+            }
+            int incl = cnt;  // lanes 0-7: side A cells, 8-15: side B cells -> A nodes first
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const int u = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += u;
+            }
+            nA = __shfl(incl, 7, 64);
+            ntot = __shfl(incl, 15, 64);
+            for (int j = 0; j < cnt; ++j) {
+                const int idx = incl - cnt + j;
+                nqi[w][idx] = qinfo[q0 + j];
+                ngq[w][idx] = qg[q0 + j];
+            }
+        }
+        __syncthreads();
+        int4 me = make_int4(0, 0, -1, 0);
+        int2 mg = make_int2(0, 0);
+        int comp = -1;
+        if (lane < ntot) {
+            me = nqi[w][lane];
+            mg = ngq[w][lane];
+            comp = me.z >= 0 ? parent[me.z] : -1;  // tile component (a member of the set)
+            ncomp[w][lane] = comp;
+        }
+        __syncthreads();
+        if (lane < ntot) {  // pre-join quarters of one side that share a tile component
+            int r = lane;
+            if (comp >= 0)
+                for (int j = lane < nA ? 0 : nA; j < lane; ++j)
+                    if (ncomp[w][j] == comp) {
+                        r = j;
+                        break;
+                    }
+            lp[lane] = r;
+        }
+        __syncthreads();
+        if (lane < nA && me.z >= 0) {
+            double px[kQReg], py[kQReg];
+            const int na = load_own(xy, me, 0, px, py);
+#pragma unroll
+            for (int sweep = 1; sweep <= 2; ++sweep)
+                for (int b = nA; b < ntot; ++b) {
+                    const int2 og = ngq[w][b];
+                    if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
+                    const int4 o = nqi[w][b];
+                    if (o.z < 0) continue;
+                    if (lfind(lp, lane) == lfind(lp, b)) continue;
+                    const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y, (uint32_t)o.w,
+                                                        core, 0, eps2)
+                                           : pair_found_generic(xy, 0, me, o, core, eps2);
+                    if (!f) continue;
+                    lunite(lp, lane, b);
+                    const int ra = uf_find(parent, comp);
+                    const int rb = uf_find(parent, ncomp[w][b]);
+                    if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
+                }
+        }
+        __syncthreads();
+    }
+}
+
+// After all unions: every quarter rep points straight at its root, so the per-point walk in
+// final_kernel is core -> rep -> root.
+__global__ __launch_bounds__(kBlock) void quarter_root_kernel(const int4* __restrict__ qinfo,
+                                                              const int32_t* __restrict__ nq_p,
+                                                              int32_t* __restrict__ parent) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
-    const int4 me = qinfo[q];
-    if (me.z < 0) return;
-    const uint32_t key = (uint32_t)me.w, ck = key >> 2;
-    const uint32_t cy = ck / g.nx, cx = ck - cy * g.nx;
-    const int gx = (int)(2 * cx + (key & 1u)), gy = (int)(2 * cy + ((key >> 1) & 1u));
-    const Seg s = load_seg(seg, cell[me.x]);
-    // own cores in registers (the same set is tested against every neighbour quarter)
-    double px[kQReg], py[kQReg];
-    int nmine = 0;
-    const bool small = me.y - me.x <= 32;
-    {
-        uint32_t m = qmask[q];
-        const uint32_t m0 = small ? m : 0u;
-#pragma unroll
-        for (int k = 0; k < kQReg; ++k) {
-            px[k] = 0.0;
-            py[k] = 0.0;
-        }
-        uint32_t mm = m0;
-#pragma unroll
-        for (int k = 0; k < kQReg; ++k) {
-            if (mm) {
-                const int j = me.x + (__ffs(mm) - 1);
-                mm &= mm - 1;
-                const double2 v = xy[j];
-                px[k] = v.x;
-                py[k] = v.y;
-                nmine = k + 1;
-            }
-        }
-        if (mm) nmine = -1;  // more than kQReg cores: generic loop below
-    }
-    const bool inreg = small && nmine >= 0;
-    int rp = uf_find<1>(parent, me.z);
-    // two sweeps: adjacent quarters (Chebyshev distance 1) first so most merges happen early
-    // and the far (distance-2) candidates are usually skipped by the find-first check
-#pragma unroll
-    for (int sweep = 0; sweep < 2; ++sweep) {
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {  // rows cy-1 and cy: every quarter there with a smaller key
-            const int rb = r == 0 ? s.b0 : s.b1, re = r == 0 ? s.e0 : s.e1;
-            if (rb >= re) continue;
-            const int ry = (int)cy + r - 1;
-            const int64_t rowbase = (int64_t)ry * g.nx;
-            const int q_lo = qidx[rb], q_hi = qidx[re - 1];
-            for (int q2 = q_lo; q2 <= q_hi && q2 < q; ++q2) {
-                const int4 o = qinfo[q2];
-                if (o.z < 0) continue;
-                const uint32_t k2 = (uint32_t)o.w;
-                const int gx2 = (int)(2 * ((int64_t)(k2 >> 2) - rowbase)) + (int)(k2 & 1u);
-                const int gy2 = 2 * ry + (int)((k2 >> 1) & 1u);
-                const int d = max(abs(gx2 - gx), abs(gy2 - gy));
-                if (d > 2 || (sweep == 0) != (d <= 1)) continue;
-                if constexpr (ABL == 3) {
-                    asm volatile("" ::"v"(gx2));
-                    continue;
-                }
-                const int rr = uf_find_until<1>(parent, o.z, rp);
-                if (rr == rp) continue;  // already one set: skip the pair test
-                bool found = ABL == 2;
-                if (!found && inreg && o.y - o.x <= 32) {
-                    uint32_t om = qmask[q2];
-                    while (om && !found) {
-                        const int b2 = o.x + (__ffs(om) - 1);
-                        om &= om - 1;
-                        const double2 pb = xy[b2];
-#pragma unroll
-                        for (int k = 0; k < kQReg; ++k)
-                            found |= (k < nmine) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
-                    }
-                } else if (!found) {
-                    for (int a = me.x; a < me.y && !found; ++a) {
-                        if (!core[a]) continue;
-                        const double2 pa = xy[a];
-                        for (int b2 = o.x; b2 < o.y; ++b2) {
-                            if (!core[b2]) continue;
-                            const double2 pb = xy[b2];
-                            if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) {
-                                found = true;
-                                break;
-                            }
-                        }
-                    }
-                }
-                if (!found) continue;
-                if constexpr (ABL == 1) {
-                    asm volatile("" ::"v"(rr));
-                    continue;
-                }
-                rp = uf_unite_roots<1>(parent, perm, rp, rr);
-            }
-        }
-    }
+    const int rep = qinfo[q].z;
+    if (rep < 0) return;
+    int r = rep;
+    for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
+    parent[rep] = r;
 }
 
 __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
@@ -614,35 +921,61 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
     if (r == (int)p && is_root) is_root[perm[p]] = 1;
 }
 
-// Border / noise rule + cluster numbering, written in input order.
+// Border minimum over core neighbours: min lab (full fits) or argmin gs_of_root (slab fits).
+template <bool SLAB, class Src>
+__device__ __forceinline__ void border_scan(const Src* __restrict__ src, int b, int e, int off,
+                                            double2 me, double eps2,
+                                            const uint8_t* __restrict__ core,
+                                            const int32_t* __restrict__ lab,
+                                            const int64_t* __restrict__ gs_of_root, int64_t& m,
+                                            int32_t& mr) {
+    for (int j = b; j < e; ++j) {
+        const double2 q = src[j];
+        const int sj = j + off;  // global slot
+        if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[sj]) {
+            const int32_t lj = lab[sj];
+            const int64_t v = SLAB ? gs_of_root[lj] : (int64_t)lj;
+            if (v < m) {
+                m = v;
+                mr = lj;
+            }
+        }
+    }
+}
+
+// Labels, one thread per sorted slot (only non-cores scan their stencil, ~10% of the points
+// at the bench workload, so staging whole tiles does not pay here).  Full fits write
+// cluster/flag in input order; slab fits (SLAB) label zone-0 points from the merged global
+// component ids.  Slots >= nf are outside the grid: never anyone's neighbour.
+template <bool SLAB>
 __global__ __launch_bounds__(kBlock) void output_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2, int32_t mode,
+    const Seg* __restrict__ seg, int64_t nf, int64_t n, double eps2, int32_t mode,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
     const int32_t* __restrict__ lab, const int32_t* __restrict__ rank,
+    const uint8_t* __restrict__ zone, const int64_t* __restrict__ gid,
+    const int64_t* __restrict__ gs_of_root, const int32_t* __restrict__ label_of_root,
     int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const int32_t o = perm[p];
+    if (SLAB && zone[o] != 0) return;
     int32_t cl = 0;
     uint8_t fl = 2;  // Noise
     if (core[p]) {
-        cl = rank[lab[p]] + 1;
+        cl = SLAB ? label_of_root[lab[p]] : rank[lab[p]] + 1;
         fl = 1;  // Core
     } else if (p < nf) {
         const double2 me = xy[p];
+        int64_t m = 0x7FFFFFFFFFFFFFFFll;
+        int32_t mr = -1;
         const Seg s = load_seg(seg, cell[p]);
-        int32_t m = 0x7FFFFFFF;
-        for_candidates(s, [&](int j) {
-            const double2 q = xy[j];
-            if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
-                const int32_t lj = lab[j];
-                m = lj < m ? lj : m;
-            }
-            return true;
-        });
-        if (m != 0x7FFFFFFF && (mode != 0 || m < o)) {
-            cl = rank[m] + 1;
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            border_scan<SLAB>(xy, s.b[k], s.e[k], 0, me, eps2, core, lab, gs_of_root, m, mr);
+        const int64_t self = SLAB ? gid[o] : (int64_t)o;
+        if (mr >= 0 && (mode != 0 || m < self)) {
+            cl = SLAB ? label_of_root[mr] : rank[mr] + 1;
             fl = 0;  // Border
         }
     }
@@ -665,54 +998,6 @@ __global__ __launch_bounds__(kBlock) void slab_roots_kernel(int64_t n,
     root_out[o] = core[p] ? lab[p] : -1;
 }
 
-// Slab fit, phase 2 (after the global merge): labels of the owned (zone 0) points.
-//   gs_of_root[r]    global s(K) (a global visit index) of local root r (slab index)
-//   label_of_root[r] global cluster id of that component
-// Border rule on global visit indices: m = min over core neighbours of gs_of_root[root];
-// Naive: Border iff m < gid(b); Archery: Border iff a core neighbour exists.
-__global__ __launch_bounds__(kBlock) void slab_label_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, int64_t n, int64_t nf, double eps2, int32_t mode,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
-    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
-    const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
-    const int32_t* __restrict__ label_of_root, int32_t* __restrict__ cluster_out,
-    uint8_t* __restrict__ flag_out) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= n) return;
-    const int32_t o = perm[p];
-    if (zone[o] != 0) return;
-    int32_t cl = 0;
-    uint8_t fl = 2;
-    if (core[p]) {
-        cl = label_of_root[lab[p]];
-        fl = 1;
-    } else if (p < nf) {
-        const double2 me = xy[p];
-        const Seg s = load_seg(seg, cell[p]);
-        int64_t m = 0x7FFFFFFFFFFFFFFFll;
-        int32_t mr = -1;
-        for_candidates(s, [&](int j) {
-            const double2 q = xy[j];
-            if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
-                const int32_t r = lab[j];
-                const int64_t v = gs_of_root[r];
-                if (v < m) {
-                    m = v;
-                    mr = r;
-                }
-            }
-            return true;
-        });
-        if (mr >= 0 && (mode != 0 || m < gid[o])) {
-            cl = label_of_root[mr];
-            fl = 0;
-        }
-    }
-    cluster_out[o] = cl;
-    flag_out[o] = fl;
-}
-
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -723,28 +1008,31 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 
 // Grid sizing on the host (see DESIGN.md "grid soundness"): cell side >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500) bounds |x'-x| for every pair the fp64 predicate accepts;
-// nx*ny <= 2^29 (u32 keys = cell*4 + quadrant, below the sentinel), growing the side (never
-// shrinking it) when the extent would need more cells.  Quarter cells are cliques only while
-// the side was not grown: clique = side <= |eps|*(1+2^-14).
+// at most 2^23 tiles of 8x8 cells (u32 keys = tile*256 + cell*4 + quadrant, below the
+// sentinel), growing the side (never shrinking it) when the extent would need more.  Quarter
+// cells are cliques only while the side was not grown: clique = side <= |eps|*(1+2^-14).
 static bool make_grid(const double bb[5], double eps, GridParams* g) {
     const double xmin = bb[0], xmax = bb[1], ymin = bb[2], ymax = bb[3];
     double R = std::fabs(eps) * (1.0 + 0x1p-40);
     if (R < 0x1p-500) R = 0x1p-500;
     double hx = R * (1.0 + 0x1p-16), hy = hx;
-    const double limit = 536870912.0;  // 2^29 cells
+    const double limit = 8388608.0;  // 2^23 tiles
     auto cells = [](double vmax, double vmin, double h) {
         const double t = (vmax * 0.5 - vmin * 0.5) * (2.0 / h);
         return std::floor(t) + 1.0;  // may be +inf for absurd extents
     };
     for (int it = 0; it < 4096; ++it) {
         const double cx = cells(xmax, xmin, hx), cy = cells(ymax, ymin, hy);
-        if (cx <= limit && cy <= limit && cx * cy <= limit) {
+        const double tx = std::ceil(cx / 8.0), ty = std::ceil(cy / 8.0);
+        if (tx <= limit && ty <= limit && tx * ty <= limit) {
             g->invx = 2.0 / hx;
             g->invy = 2.0 / hy;
             g->xmin2 = xmin * 0.5;
             g->ymin2 = ymin * 0.5;
             g->nx = (uint32_t)cx;
             g->ny = (uint32_t)cy;
+            g->ntx = (uint32_t)tx;
+            g->nty = (uint32_t)ty;
             const double cl = std::fabs(eps) * (1.0 + 0x1p-14);
             g->clique = (hx <= cl && hy <= cl) ? 1 : 0;
             return true;
@@ -777,10 +1065,11 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     int32_t* perm = static_cast<int32_t*>(ws.perm.ensure(n * sizeof(int32_t)));
     int32_t* perm2 = static_cast<int32_t*>(ws.perm2.ensure(n * sizeof(int32_t)));
     double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
-    int32_t* misc_i = reinterpret_cast<int32_t*>(misc + 16);  // [0] ncells, [1] nclusters
+    // misc_i: [0] ncells [1] nclusters [2] ncore [3] nquarters [4] ntiles
+    int32_t* misc_i = reinterpret_cast<int32_t*>(misc + 16);
 
-    DBSCAN_HIP_CHECK(hipMemsetAsync(misc_i, 0, 4 * sizeof(int32_t), s));
-    GridParams g{0, 0, 0, 0, 1, 1, 0};
+    DBSCAN_HIP_CHECK(hipMemsetAsync(misc_i, 0, 8 * sizeof(int32_t), s));
+    GridParams g{0, 0, 0, 0, 1, 1, 1, 1, 0};
     int64_t nf = 0;
     int bits = 0;
     if (mode == kGridEps) {
@@ -809,9 +1098,9 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        const uint64_t qcells = 4ull * g.nx * g.ny;  // valid keys < qcells <= 2^31
+        const uint64_t nkeys = 256ull * g.ntx * g.nty;  // valid keys < nkeys <= 2^31
         bits = 1;
-        while (bits < 32 && (1ull << bits) <= qcells) ++bits;  // keys < 2^bits - 1 (sentinel)
+        while (bits < 32 && (1ull << bits) <= nkeys) ++bits;  // keys < 2^bits - 1 (sentinel)
         radix_sort_pairs(s, key, perm, key2, perm2, n, bits, ws.hist, ws.scan_tmp, prof);
     } else {
         StageTimer t(prof, s, "bin");
@@ -821,13 +1110,22 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     }
     stats.bits = bits;
     ws.perm_sorted = perm;
+    ws.key_sorted = key;
 
     const int64_t nfa = nf > 0 ? nf : 1;
+    const int64_t ntile_bound = std::min<int64_t>(nfa, (int64_t)g.ntx * g.nty);
     double2* xy = static_cast<double2*>(ws.xy.ensure(nfa * sizeof(double2)));
     int32_t* cell = static_cast<int32_t*>(ws.cell.ensure(nfa * sizeof(int32_t)));
     uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(nfa * sizeof(uint32_t)));
     int32_t* cstart = static_cast<int32_t*>(ws.cstart.ensure((nfa + 1) * sizeof(int32_t)));
     Seg* seg = static_cast<Seg*>(ws.seg.ensure(nfa * sizeof(Seg)));
+    int32_t* tidx = static_cast<int32_t*>(ws.tidx.ensure(nfa * sizeof(int32_t)));
+    uint32_t* tkey = static_cast<uint32_t*>(ws.tkey.ensure(nfa * sizeof(uint32_t)));
+    int32_t* tstart = static_cast<int32_t*>(ws.tstart.ensure((nfa + 1) * sizeof(int32_t)));
+    int32_t* tmap =
+        static_cast<int32_t*>(ws.tmap.ensure((size_t)g.ntx * g.nty * sizeof(int32_t)));
+    int32_t* tslot =
+        static_cast<int32_t*>(ws.tslot.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
     uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
     int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
     int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
@@ -836,13 +1134,13 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     uint32_t* qkey = nullptr;
     int32_t* qstart = nullptr;
     int4* qinfo = nullptr;
-    uint32_t* qmask = nullptr;
+    int2* qg = nullptr;
     if (clique) {
         qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
         qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
         qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
         qinfo = static_cast<int4*>(ws.qrep.ensure(nfa * sizeof(int4)));
-        qmask = static_cast<uint32_t*>(ws.qmask.ensure(nfa * sizeof(uint32_t)));
+        qg = static_cast<int2*>(ws.qmask.ensure(nfa * sizeof(int2)));
     }
 
     if (nf > 0) {
@@ -855,52 +1153,81 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         {
             StageTimer t(prof, s, "cells");
             exclusive_scan(s, 3, key, cell, nf, &misc_i[0], ws.scan_tmp);
-            hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 2, nf,
+            hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 2, nf,
                                cell, ckey, cstart, &misc_i[0]);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+            exclusive_scan(s, 4, key, tidx, nf, &misc_i[4], ws.scan_tmp);
+            hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 8, nf,
+                               tidx, tkey, tstart, &misc_i[4]);
             DBSCAN_HIP_CHECK(hipGetLastError());
             if (clique) {
                 exclusive_scan(s, 2, key, qidx, nf, &misc_i[3], ws.scan_tmp);
-                hipLaunchKernelGGL(cells_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 0,
+                hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 0,
                                    nf, qidx, qkey, qstart, &misc_i[3]);
                 DBSCAN_HIP_CHECK(hipGetLastError());
             }
         }
         {
+            StageTimer t(prof, s, "tables");
+            DBSCAN_HIP_CHECK(
+                hipMemsetAsync(tmap, 0xFF, (size_t)g.ntx * g.nty * sizeof(int32_t), s));
+            hipLaunchKernelGGL(tmap_kernel, dim3(nblk(ntile_bound)), dim3(kBlock), 0, s, tkey,
+                               &misc_i[4], tmap);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(tslot_kernel, dim3(nblk(ntile_bound)), dim3(kBlock), 0, s, tstart,
+                               tkey, &misc_i[4], cell, ckey, cstart, &misc_i[0], tslot);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
             StageTimer t(prof, s, "segs");
             hipLaunchKernelGGL(segs_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, ckey, cstart,
-                               &misc_i[0], g, seg);
+                               &misc_i[0], tmap, tslot, g, seg);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     }
-    int32_t* block_cores =
-        static_cast<int32_t*>(ws.blockcnt.ensure(2 * (nblk(n) + 1) * sizeof(int32_t)));
+    // per-tile kernels: grid stride over occupied tiles (their count stays on the device)
+    const unsigned tile_grid = nf > 0 ? (unsigned)std::min<int64_t>(ntile_bound, kTileGrid) : 0u;
+    const unsigned rest_grid = nblk(n - nf);
+    int32_t* block_cores = static_cast<int32_t*>(
+        ws.blockcnt.ensure(2 * ((size_t)tile_grid + rest_grid + 1) * sizeof(int32_t)));
     {
         StageTimer t(prof, s, "count");
-        hipLaunchKernelGGL(count_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, ckey,
-                           cstart, &misc_i[0], g, n, nf, eps2, a.min_points, perm, a.zone, qidx,
-                           qstart, core, parent, block_cores);
+        if (tile_grid)
+            hipLaunchKernelGGL(count_tile_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, key,
+                               cell, seg, tstart, tkey, tmap, tslot, &misc_i[4], g, eps2,
+                               a.min_points, perm, a.zone, qidx, qstart, core, parent,
+                               block_cores);
+        if (rest_grid)
+            hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf, n,
+                               a.min_points, perm, a.zone, core, parent,
+                               block_cores + tile_grid);
         DBSCAN_HIP_CHECK(hipGetLastError());
-        exclusive_scan(s, 0, block_cores, block_cores + nblk(n) + 1, nblk(n), &misc_i[2],
-                       ws.scan_tmp);
+        const int64_t nb = (int64_t)tile_grid + rest_grid;
+        exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &misc_i[2], ws.scan_tmp);
     }
     if (clique) {
         {
             StageTimer t(prof, s, "quarter_init");
             hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qstart,
-                               qkey, &misc_i[3], perm, core, qinfo, qmask, parent);
+                               qkey, &misc_i[3], g, perm, core, qinfo, qg, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        StageTimer t(prof, s, "union");
-        static const int ablate = [] {
-            const char* e = getenv("DBSCAN_UF_ABLATE");
-            return e ? atoi(e) : 0;
-        }();
-        auto* kq = ablate == 1   ? quarter_union_kernel<1>
-                   : ablate == 2 ? quarter_union_kernel<2>
-                   : ablate == 3 ? quarter_union_kernel<3>
-                                 : quarter_union_kernel<0>;
-        hipLaunchKernelGGL(kq, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, qidx, qinfo,
-                           qmask, &misc_i[3], g, eps2, perm, core, parent);
+        {
+            StageTimer t(prof, s, "union_tile");
+            hipLaunchKernelGGL(tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart,
+                               &misc_i[4], qidx, qinfo, qg, eps2, perm, core, parent);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        {
+            StageTimer t(prof, s, "union_edge");
+            hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tkey,
+                               &misc_i[4], tmap, tslot, qidx, qinfo, qg, g, eps2, perm, core,
+                               parent);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        StageTimer t(prof, s, "union_root");
+        hipLaunchKernelGGL(quarter_root_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qinfo,
+                           &misc_i[3], parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
     } else if (nf > 0) {
         StageTimer t(prof, s, "union");
@@ -925,11 +1252,14 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "output");
-            hipLaunchKernelGGL(output_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, n,
-                               nf, eps2, a.mode, perm, core, lab, rank, a.cluster, a.flag);
+            hipLaunchKernelGGL(output_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell,
+                               seg, nf, n, eps2, a.mode, perm, core, lab, rank,
+                               (const uint8_t*)nullptr, (const int64_t*)nullptr,
+                               (const int64_t*)nullptr, (const int32_t*)nullptr, a.cluster,
+                               a.flag);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        int32_t hv[3];
+        int32_t hv[5];
         DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
         DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
         k = hv[1];
@@ -948,7 +1278,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
                                core, lab, a.core_out, a.root_out);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        int32_t hv[3];
+        int32_t hv[5];
         DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
         DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
         stats.ncells = nf > 0 ? hv[0] : 0;
@@ -961,6 +1291,8 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         slab->n = n;
         slab->nf = nf;
         slab->eps2 = eps2;
+        slab->g = g;
+        slab->tile_grid = tile_grid;
     }
     return k;
 }
@@ -972,13 +1304,13 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     if (!st.valid) throw ArgError{"dbscan_slab_label_device: no slab fit on this handle"};
     if (st.n == 0) return;
     StageTimer t(prof, s, "slab_label");
-    hipLaunchKernelGGL(slab_label_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(output_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
-                       static_cast<const Seg*>(ws.seg.p), st.n, st.nf, st.eps2, mode,
+                       static_cast<const Seg*>(ws.seg.p), st.nf, st.n, st.eps2, mode,
                        static_cast<const int32_t*>(ws.perm_sorted),
-                       zone, static_cast<const uint8_t*>(ws.core.p),
-                       static_cast<const int32_t*>(ws.lab.p), gid, gs_of_root, label_of_root,
-                       cluster, flag);
+                       static_cast<const uint8_t*>(ws.core.p),
+                       static_cast<const int32_t*>(ws.lab.p), (const int32_t*)nullptr, zone, gid,
+                       gs_of_root, label_of_root, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
     DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
 }

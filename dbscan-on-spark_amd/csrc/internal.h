@@ -1,15 +1,20 @@
 // internal.h -- shared declarations of libdbscan_hip.so (gfx950 only).
 //
 // Device data layout (one fit, n points, nf finite points in the eps grid):
-//   key[n]   u32 cell key cy*nx+cx (0xFFFFFFFF for points outside the grid)   -> radix sorted
+//   key[n]   u32 tile<<8 | cell-in-tile<<2 | quadrant, tiles of 8x8 eps cells row-major over
+//            the grid (0xFFFFFFFF for points outside the grid)                -> radix sorted
 //   perm[n]  i32 input index of each sorted slot (the reference's visit index)
 //   xy[nf]   double2 sorted coordinates, SoA->AoS so one 16-B load feeds a candidate test
 //   cell[nf] i32 occupied-cell index of each sorted slot
-//   ckey[C], cstart[C+1]  occupied cells (sorted keys) and their first slot
-//   seg[C]   int8 (b0,e0,b1,e1,b2,e2,-,-): slot ranges of the 3 rows of the 3x3 stencil
-//   qidx[nf], qkey[Q], qstart[Q+1], qrep[Q]  quarter cells (2x2 per eps cell; key low 2 bits =
-//            quadrant): side ~eps/2, so each is a clique under the exact predicate; qrep =
-//            its minimum-visit-index core (or -1)
+//   ckey[C], cstart[C+1]  occupied cells (key >> 2) and their first slot
+//   tidx[nf], tkey[T], tstart[T+1]  occupied tiles (key >> 8) and their first slot
+//   tmap[ntx*nty]  occupied-tile index of every tile of the grid (-1: empty)
+//   tslot[T][65]   first slot of the first occupied cell with local index >= l
+//   seg[C]   64 B: <= 6 slot pieces of the 3x3 stencil + the own cell range
+//   qidx[nf], qkey[Q], qstart[Q+1]  quarter cells (2x2 per eps cell; key low 2 bits =
+//            quadrant): side ~eps/2, so each is a clique under the exact predicate
+//   qrep[Q]  int4 (begin, end, minimum-visit-index core or -1, core mask); qmask[Q] int2
+//            quarter-grid coordinates
 //   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
 //   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
 #pragma once
@@ -86,14 +91,23 @@ struct StageTimer {
 
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
-        is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt;
+        is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, tidx, tkey, tstart, tmap,
+        tslot;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
+    uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
-                          &qstart, &qrep, &qmask, &blockcnt})
+                          &qstart, &qrep, &qmask, &blockcnt, &tidx, &tkey, &tstart, &tmap, &tslot})
             b->release();
     }
+};
+
+struct GridParams {
+    double xmin2, ymin2, invx, invy;  // cell = floor((v*0.5 - vmin*0.5) * inv)
+    uint32_t nx, ny;                  // eps cells per axis
+    uint32_t ntx, nty;                // 8x8-cell tiles per axis
+    int clique;  // cell side <= eps*(1+2^-14): quarter cells are cliques of the predicate
 };
 
 struct FitStats {
@@ -123,6 +137,8 @@ struct SlabState {
     bool valid = false;
     int64_t n = 0, nf = 0;
     double eps2 = 0;
+    GridParams g{};
+    unsigned tile_grid = 0;  // workgroups of the per-tile kernels (0: no finite points)
 };
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
