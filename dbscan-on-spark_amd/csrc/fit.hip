@@ -53,9 +53,9 @@ enum GridMode { kGridEps = 0, kGridAllPairs = 1, kGridNoPairs = 2 };
 namespace {
 
 constexpr int kTslot = 65;        // per-tile cell-start table stride (64 cells + end)
-constexpr int kStageCap = 3072;   // points staged per tile (48 KB of double2)
 constexpr int kQReg = 8;          // own-quarter core points kept in registers for pair tests
 constexpr int64_t kTileGrid = 8192;  // workgroups of the per-tile kernels (grid stride)
+constexpr int kMaxNbr = 11;  // neighbour lists of non-cores kept while minPoints - 1 <= this
 
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
 // two rounded multiplies, one rounded add, <=.  The whole library is built with
@@ -254,8 +254,8 @@ __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict
 // Tile staging: a tile and its 1-cell halo as a 10x10 "extended" cell grid in LDS.  Extended
 // cell k = (ey+1)*10 + (ex+1), ex, ey in -1..8; cells are stored in k order, so extended row ey
 // is contiguous and a point at local cell (lx, ly) finds each of its 3 stencil rows as ONE LDS
-// range [off[(ey+1)*10 + lx], off[(ey+1)*10 + lx + 3]).  Tiles whose tile+halo exceeds
-// kStageCap points (dense data) fall back to the global-memory path.
+// range [off[(ey+1)*10 + lx], off[(ey+1)*10 + lx + 3]).  Tiles whose tile+halo exceeds the
+// kernel's staging capacity (dense data) fall back to the global-memory path.
 // The per-tile kernels loop over occupied tiles with a grid stride (the tile count is only
 // known on the device); every loop trip ends in a barrier before the stage is overwritten.
 // ---------------------------------------------------------------------------------------
@@ -269,7 +269,7 @@ struct TileStage {
 __device__ bool stage_tile(int t, const double2* __restrict__ xy,
                            const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
                            const int32_t* __restrict__ tmap, const int32_t* __restrict__ tslot,
-                           const GridParams& g, TileStage& st, double2* buf) {
+                           const GridParams& g, TileStage& st, double2* buf, int cap) {
     const int tid = threadIdx.x;
     if (tid < 100) {
         const uint32_t tk = tkey[t];
@@ -310,7 +310,7 @@ __device__ bool stage_tile(int t, const double2* __restrict__ xy,
         if (tid == 0) {
             st.off[100] = carry;
             st.total = carry;
-            st.ok = carry <= kStageCap;
+            st.ok = carry <= cap;
         }
     }
     __syncthreads();
@@ -354,43 +354,55 @@ __device__ __forceinline__ LdsRanges lds_ranges(const TileStage& st, int l) {
 // minPoints neighbours are seen (the count itself is never an output).  Own cell first, then
 // the rest of its row, then the rows below and above; 8 candidates per batch.
 // ---------------------------------------------------------------------------------------
-template <class Src>
+// REC: the first nbr_k hits (self included) are also noted as LDS indices in the thread's
+// column of `lst` (stride kBlock), so a point that ends below minPoints has its complete
+// neighbour list without a second scan.
+template <bool REC, class Src>
 __device__ __forceinline__ bool scan_count(const Src* __restrict__ src, int b, int e,
-                                           double2 me, double eps2, int min_points, int& cnt) {
+                                           double2 me, double eps2, int min_points, int& cnt,
+                                           uint16_t* lst, int nbr_k) {
     int j = b;
     for (; j + 8 <= e; j += 8) {
         double2 qq[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) qq[u] = src[j + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cnt += within_eps(me.x, me.y, qq[u].x, qq[u].y, eps2) ? 1 : 0;
+        for (int u = 0; u < 8; ++u) {
+            const bool hit = within_eps(me.x, me.y, qq[u].x, qq[u].y, eps2);
+            if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)(j + u);
+            cnt += hit ? 1 : 0;
+        }
         if (cnt >= min_points) return true;
     }
     for (; j < e; ++j) {
         const double2 q = src[j];
-        cnt += within_eps(me.x, me.y, q.x, q.y, eps2) ? 1 : 0;
+        const bool hit = within_eps(me.x, me.y, q.x, q.y, eps2);
+        if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)j;
+        cnt += hit ? 1 : 0;
     }
     return cnt >= min_points;
 }
 
 // one count over ranges (b[k], e[k]) with the own cell [cs, ce) first and excluded after
-template <int K>
+template <int K, bool REC = false>
 __device__ __forceinline__ void count_pieces(const double2* __restrict__ src, const int* b,
                                              const int* e, int cs, int ce, double2 me,
-                                             double eps2, int min_points, int& cnt) {
-    if (scan_count(src, cs, ce, me, eps2, min_points, cnt)) return;
+                                             double eps2, int min_points, int& cnt,
+                                             uint16_t* lst = nullptr, int nbr_k = 0) {
+    if (scan_count<REC>(src, cs, ce, me, eps2, min_points, cnt, lst, nbr_k)) return;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int lo = b[k], hi = e[k];
         if (lo <= cs && ce <= hi) {  // the piece holding the own cell: around it
-            if (scan_count(src, lo, cs, me, eps2, min_points, cnt)) return;
-            if (scan_count(src, ce, hi, me, eps2, min_points, cnt)) return;
-        } else if (scan_count(src, lo, hi, me, eps2, min_points, cnt)) {
+            if (scan_count<REC>(src, lo, cs, me, eps2, min_points, cnt, lst, nbr_k)) return;
+            if (scan_count<REC>(src, ce, hi, me, eps2, min_points, cnt, lst, nbr_k)) return;
+        } else if (scan_count<REC>(src, lo, hi, me, eps2, min_points, cnt, lst, nbr_k)) {
             return;
         }
     }
 }
 
+template <int CAP>
 __global__ __launch_bounds__(kBlock) void count_tile_kernel(
     const double2* __restrict__ xy, const uint32_t* __restrict__ key,
     const int32_t* __restrict__ cell, const Seg* __restrict__ seg,
@@ -399,14 +411,17 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
     const int32_t* __restrict__ ntiles_p, GridParams g, double eps2, int32_t min_points,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
     const int32_t* __restrict__ qidx, const int32_t* __restrict__ qstart,
-    uint8_t* __restrict__ core, int32_t* __restrict__ parent, int32_t* __restrict__ block_cores) {
+    uint8_t* __restrict__ core, int32_t* __restrict__ parent, int32_t* __restrict__ block_cores,
+    int32_t* __restrict__ nbr, int nbr_k) {
     __shared__ TileStage st;
-    __shared__ double2 buf[kStageCap];
+    __shared__ double2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
+    __shared__ uint16_t lsts[kMaxNbr * kBlock];
+    uint16_t* lst = lsts + threadIdx.x;
     const int ntiles = *ntiles_p;
     int mine = 0;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const bool staged = stage_tile(t, xy, tstart, tkey, tmap, tslot, g, st, buf);
+        const bool staged = stage_tile(t, xy, tstart, tkey, tmap, tslot, g, st, buf, CAP);
         for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
             bool is_core;
             if (zone && zone[perm[p]] == 2) {
@@ -422,7 +437,11 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
                     if (qstart[q + 1] - qstart[q] >= min_points) cnt = min_points;
                 }
                 if (cnt < min_points) {
-                    if (staged) {
+                    if (staged && nbr) {
+                        const LdsRanges r = lds_ranges(st, (int)((key[p] >> 2) & 63u));
+                        count_pieces<3, true>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points,
+                                              cnt, lst, nbr_k);
+                    } else if (staged) {
                         const LdsRanges r = lds_ranges(st, (int)((key[p] >> 2) & 63u));
                         count_pieces<3>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points, cnt);
                     } else {
@@ -431,6 +450,33 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
                     }
                 }
                 is_core = cnt >= min_points;
+                // A non-core has fewer than minPoints neighbours: keep their slots (self
+                // excluded, -1 terminated) so the label pass needs no second stencil scan.
+                if (!is_core && nbr) {
+                    int32_t* out = nbr + (int64_t)p * nbr_k;
+                    int w = 0;
+                    if (staged) {  // the count noted every hit (cnt <= nbr_k): LDS index -> slot
+                        for (int k = 0; k < cnt; ++k) {
+                            const int j = lst[k * kBlock];
+                            int lo = 0, hi = 99;  // extended cell holding LDS index j
+                            while (lo < hi) {
+                                const int mid = (lo + hi + 1) >> 1;
+                                if (st.off[mid] <= j) lo = mid; else hi = mid - 1;
+                            }
+                            const int sj = st.cb[lo] + (j - st.off[lo]);
+                            if (sj != p) out[w++] = sj;
+                        }
+                    } else {
+                        const Seg s = load_seg(seg, cell[p]);
+                        for (int k = 0; k < 6; ++k)
+                            for (int j = s.b[k]; j < s.e[k]; ++j) {
+                                const double2 q = xy[j];
+                                if (j != p && within_eps(me.x, me.y, q.x, q.y, eps2) && w < nbr_k)
+                                    out[w++] = j;
+                            }
+                    }
+                    if (w < nbr_k) out[w] = -1;
+                }
             }
             parent[p] = p;
             core[p] = is_core ? 1 : 0;
@@ -703,24 +749,25 @@ __device__ __forceinline__ void lunite(int* lp, int a, int b) {
 
 constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
 
+template <int CAP>
 __global__ __launch_bounds__(kBlock) void tile_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
     const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ qidx,
     const int4* __restrict__ qinfo, const int2* __restrict__ qg, double eps2,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
-    int32_t* __restrict__ parent) {
+    int32_t* __restrict__ parent, int32_t* __restrict__ qcomp) {
     __shared__ int lp[kMaxTileQ];
     __shared__ int4 lqi[kMaxTileQ];
     __shared__ int qmap[kMaxTileQ];  // 16x16 local quarter grid -> local quarter index
     __shared__ int cmin[kMaxTileQ];
     __shared__ int crep[kMaxTileQ];
-    __shared__ double2 buf[kStageCap];
+    __shared__ double2 buf[CAP > 0 ? CAP : 1];
     const int ntiles = *ntiles_p;
     const int i = threadIdx.x;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int ts = tstart[t], te = tstart[t + 1];
         const int q0 = qidx[ts], nq = qidx[te - 1] + 1 - q0;
-        const bool staged = te - ts <= kStageCap;
+        const bool staged = te - ts <= CAP;
         qmap[i] = -1;
         cmin[i] = 0x7FFFFFFF;
         if (staged)
@@ -774,6 +821,7 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
         __syncthreads();
         // quarter reps (roots after quarter_init) now point at their tile component's rep
         if (r >= 0 && crep[r] != me.z) parent[me.z] = crep[r];
+        if (i < nq) qcomp[q0 + i] = r >= 0 ? crep[r] : -1;
         __syncthreads();
     }
 }
@@ -792,7 +840,8 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
     const double2* __restrict__ xy, const uint32_t* __restrict__ tkey,
     const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ tmap,
     const int32_t* __restrict__ tslot, const int32_t* __restrict__ qidx,
-    const int4* __restrict__ qinfo, const int2* __restrict__ qg, GridParams g, double eps2,
+    const int4* __restrict__ qinfo, const int2* __restrict__ qg,
+    const int32_t* __restrict__ qcomp, GridParams g, double eps2,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
     int32_t* __restrict__ parent) {
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
@@ -840,46 +889,47 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
                 const int idx = incl - cnt + j;
                 nqi[w][idx] = qinfo[q0 + j];
                 ngq[w][idx] = qg[q0 + j];
+                ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
             }
         }
         __syncthreads();
+        const int a = lane & 31, half = lane >> 5;  // two lanes per side-A quarter
         int4 me = make_int4(0, 0, -1, 0);
         int2 mg = make_int2(0, 0);
         int comp = -1;
-        if (lane < ntot) {
-            me = nqi[w][lane];
-            mg = ngq[w][lane];
-            comp = me.z >= 0 ? parent[me.z] : -1;  // tile component (a member of the set)
-            ncomp[w][lane] = comp;
+        if (a < ntot) {
+            me = nqi[w][a];
+            mg = ngq[w][a];
+            comp = ncomp[w][a];
         }
-        __syncthreads();
-        if (lane < ntot) {  // pre-join quarters of one side that share a tile component
+        if (lane < ntot) {  // pre-join quarters of one side sharing a tile component
+            const int c = ncomp[w][lane];
             int r = lane;
-            if (comp >= 0)
+            if (c >= 0)
                 for (int j = lane < nA ? 0 : nA; j < lane; ++j)
-                    if (ncomp[w][j] == comp) {
+                    if (ncomp[w][j] == c) {
                         r = j;
                         break;
                     }
             lp[lane] = r;
         }
         __syncthreads();
-        if (lane < nA && me.z >= 0) {
+        if (a < nA && me.z >= 0) {
             double px[kQReg], py[kQReg];
             const int na = load_own(xy, me, 0, px, py);
 #pragma unroll
             for (int sweep = 1; sweep <= 2; ++sweep)
-                for (int b = nA; b < ntot; ++b) {
+                for (int b = nA + half; b < ntot; b += 2) {
                     const int2 og = ngq[w][b];
                     if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
                     const int4 o = nqi[w][b];
                     if (o.z < 0) continue;
-                    if (lfind(lp, lane) == lfind(lp, b)) continue;
+                    if (lfind(lp, a) == lfind(lp, b)) continue;
                     const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y, (uint32_t)o.w,
                                                         core, 0, eps2)
                                            : pair_found_generic(xy, 0, me, o, core, eps2);
                     if (!f) continue;
-                    lunite(lp, lane, b);
+                    lunite(lp, a, b);
                     const int ra = uf_find(parent, comp);
                     const int rb = uf_find(parent, ncomp[w][b]);
                     if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
@@ -921,41 +971,21 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
     if (r == (int)p && is_root) is_root[perm[p]] = 1;
 }
 
-// Border minimum over core neighbours: min lab (full fits) or argmin gs_of_root (slab fits).
-template <bool SLAB, class Src>
-__device__ __forceinline__ void border_scan(const Src* __restrict__ src, int b, int e, int off,
-                                            double2 me, double eps2,
-                                            const uint8_t* __restrict__ core,
-                                            const int32_t* __restrict__ lab,
-                                            const int64_t* __restrict__ gs_of_root, int64_t& m,
-                                            int32_t& mr) {
-    for (int j = b; j < e; ++j) {
-        const double2 q = src[j];
-        const int sj = j + off;  // global slot
-        if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[sj]) {
-            const int32_t lj = lab[sj];
-            const int64_t v = SLAB ? gs_of_root[lj] : (int64_t)lj;
-            if (v < m) {
-                m = v;
-                mr = lj;
-            }
-        }
-    }
-}
-
-// Labels, one thread per sorted slot (only non-cores scan their stencil, ~10% of the points
-// at the bench workload, so staging whole tiles does not pay here).  Full fits write
-// cluster/flag in input order; slab fits (SLAB) label zone-0 points from the merged global
-// component ids.  Slots >= nf are outside the grid: never anyone's neighbour.
+// Labels, one thread per sorted slot: cores rank[lab]+1 (or the merged label for slab fits);
+// non-cores the minimum lab over their core neighbours, read from the neighbour lists the
+// count pass kept (nbr != nullptr: minPoints <= kMaxNbr + 1), else by a stencil scan.  Full
+// fits write cluster/flag in input order; slab fits (SLAB) label zone-0 points from the merged
+// global component ids.  Slots >= nf are outside the grid: never anyone's neighbour.
 template <bool SLAB>
 __global__ __launch_bounds__(kBlock) void output_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, int64_t nf, int64_t n, double eps2, int32_t mode,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
-    const int32_t* __restrict__ lab, const int32_t* __restrict__ rank,
-    const uint8_t* __restrict__ zone, const int64_t* __restrict__ gid,
-    const int64_t* __restrict__ gs_of_root, const int32_t* __restrict__ label_of_root,
-    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nbr, int nbr_k, int64_t nf,
+    int64_t n, double eps2, int32_t mode, const int32_t* __restrict__ perm,
+    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
+    const int32_t* __restrict__ rank, const uint8_t* __restrict__ zone,
+    const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
+    const int32_t* __restrict__ label_of_root, int32_t* __restrict__ cluster_out,
+    uint8_t* __restrict__ flag_out) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const int32_t o = perm[p];
@@ -966,13 +996,33 @@ __global__ __launch_bounds__(kBlock) void output_kernel(
         cl = SLAB ? label_of_root[lab[p]] : rank[lab[p]] + 1;
         fl = 1;  // Core
     } else if (p < nf) {
-        const double2 me = xy[p];
         int64_t m = 0x7FFFFFFFFFFFFFFFll;
         int32_t mr = -1;
-        const Seg s = load_seg(seg, cell[p]);
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            border_scan<SLAB>(xy, s.b[k], s.e[k], 0, me, eps2, core, lab, gs_of_root, m, mr);
+        auto visit = [&](int j) {
+            if (!core[j]) return;
+            const int32_t lj = lab[j];
+            const int64_t v = SLAB ? gs_of_root[lj] : (int64_t)lj;
+            if (v < m) {
+                m = v;
+                mr = lj;
+            }
+        };
+        if (nbr) {
+            const int32_t* l = nbr + p * nbr_k;
+            for (int k = 0; k < nbr_k; ++k) {
+                const int j = l[k];
+                if (j < 0) break;
+                visit(j);
+            }
+        } else {
+            const double2 me = xy[p];
+            const Seg s = load_seg(seg, cell[p]);
+            for (int k = 0; k < 6; ++k)
+                for (int j = s.b[k]; j < s.e[k]; ++j) {
+                    const double2 q = xy[j];
+                    if (within_eps(me.x, me.y, q.x, q.y, eps2)) visit(j);
+                }
+        }
         const int64_t self = SLAB ? gid[o] : (int64_t)o;
         if (mr >= 0 && (mode != 0 || m < self)) {
             cl = SLAB ? label_of_root[mr] : rank[mr] + 1;
@@ -1040,6 +1090,22 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
         if (cx >= cy) hx *= 2.0; else hy *= 2.0;
     }
     return false;
+}
+
+// LDS staging capacities of the per-tile kernels (points).  DBSCAN_TILE_CAPS="count,union"
+// overrides them for measurements (count: 3072/2048/1024, union: 3072/1536/0); results are
+// identical for every choice (tiles over capacity take the global-memory path).
+struct TileVariant {  // defaults: the fastest of the r02 sweep (tools/tile_variants.sh)
+    int count_cap = 2048, union_cap = 0;
+};
+static const TileVariant& tile_variant() {
+    static const TileVariant v = [] {
+        TileVariant t;
+        if (const char* e = std::getenv("DBSCAN_TILE_CAPS"))
+            std::sscanf(e, "%d,%d", &t.count_cap, &t.union_cap);
+        return t;
+    }();
+    return v;
 }
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
@@ -1135,7 +1201,9 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     int32_t* qstart = nullptr;
     int4* qinfo = nullptr;
     int2* qg = nullptr;
+    int32_t* qcomp = nullptr;
     if (clique) {
+        qcomp = static_cast<int32_t*>(ws.qcomp.ensure(nfa * sizeof(int32_t)));
         qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
         qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
         qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
@@ -1190,13 +1258,23 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     const unsigned rest_grid = nblk(n - nf);
     int32_t* block_cores = static_cast<int32_t*>(
         ws.blockcnt.ensure(2 * ((size_t)tile_grid + rest_grid + 1) * sizeof(int32_t)));
+    const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
+    int32_t* nbr = (nf > 0 && nbr_k > 0)
+                       ? static_cast<int32_t*>(ws.nbr.ensure((size_t)nf * nbr_k * sizeof(int32_t)))
+                       : nullptr;
     {
         StageTimer t(prof, s, "count");
-        if (tile_grid)
-            hipLaunchKernelGGL(count_tile_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, key,
-                               cell, seg, tstart, tkey, tmap, tslot, &misc_i[4], g, eps2,
-                               a.min_points, perm, a.zone, qidx, qstart, core, parent,
-                               block_cores);
+        if (tile_grid) {
+            auto kern = count_tile_kernel<2048>;
+            switch (tile_variant().count_cap) {
+                case 3072: kern = count_tile_kernel<3072>; break;
+                case 1024: kern = count_tile_kernel<1024>; break;
+                default: break;
+            }
+            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, key, cell, seg,
+                               tstart, tkey, tmap, tslot, &misc_i[4], g, eps2, a.min_points, perm,
+                               a.zone, qidx, qstart, core, parent, block_cores, nbr, nbr_k);
+        }
         if (rest_grid)
             hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf, n,
                                a.min_points, perm, a.zone, core, parent,
@@ -1214,15 +1292,21 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "union_tile");
-            hipLaunchKernelGGL(tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart,
-                               &misc_i[4], qidx, qinfo, qg, eps2, perm, core, parent);
+            auto kern = tile_union_kernel<0>;
+            switch (tile_variant().union_cap) {
+                case 1536: kern = tile_union_kernel<1536>; break;
+                case 3072: kern = tile_union_kernel<3072>; break;
+                default: break;
+            }
+            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, &misc_i[4],
+                               qidx, qinfo, qg, eps2, perm, core, parent, qcomp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_edge");
             hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tkey,
-                               &misc_i[4], tmap, tslot, qidx, qinfo, qg, g, eps2, perm, core,
-                               parent);
+                               &misc_i[4], tmap, tslot, qidx, qinfo, qg, qcomp, g, eps2, perm,
+                               core, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
@@ -1253,7 +1337,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         {
             StageTimer t(prof, s, "output");
             hipLaunchKernelGGL(output_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell,
-                               seg, nf, n, eps2, a.mode, perm, core, lab, rank,
+                               seg, nbr, nbr_k, nf, n, eps2, a.mode, perm, core, lab, rank,
                                (const uint8_t*)nullptr, (const int64_t*)nullptr,
                                (const int64_t*)nullptr, (const int32_t*)nullptr, a.cluster,
                                a.flag);
@@ -1292,7 +1376,8 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         slab->nf = nf;
         slab->eps2 = eps2;
         slab->g = g;
-        slab->tile_grid = tile_grid;
+        slab->nbr = nbr;
+        slab->nbr_k = nbr_k;
     }
     return k;
 }
@@ -1306,7 +1391,8 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     StageTimer t(prof, s, "slab_label");
     hipLaunchKernelGGL(output_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
-                       static_cast<const Seg*>(ws.seg.p), st.nf, st.n, st.eps2, mode,
+                       static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k, st.nf, st.n, st.eps2,
+                       mode,
                        static_cast<const int32_t*>(ws.perm_sorted),
                        static_cast<const uint8_t*>(ws.core.p),
                        static_cast<const int32_t*>(ws.lab.p), (const int32_t*)nullptr, zone, gid,

@@ -15,6 +15,7 @@
 //            quadrant): side ~eps/2, so each is a clique under the exact predicate
 //   qrep[Q]  int4 (begin, end, minimum-visit-index core or -1, core mask); qmask[Q] int2
 //            quarter-grid coordinates
+//   nbr[nf][minPoints-1]  slots of each non-core's neighbours (-1 terminated), minPoints <= 12
 //   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
 //   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
 #pragma once
@@ -92,13 +93,14 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, tidx, tkey, tstart, tmap,
-        tslot;
+        tslot, qcomp, nbr;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
-                          &qstart, &qrep, &qmask, &blockcnt, &tidx, &tkey, &tstart, &tmap, &tslot})
+                          &qstart, &qrep, &qmask, &blockcnt, &tidx, &tkey, &tstart, &tmap, &tslot,
+                          &qcomp, &nbr})
             b->release();
     }
 };
@@ -138,7 +140,8 @@ struct SlabState {
     int64_t n = 0, nf = 0;
     double eps2 = 0;
     GridParams g{};
-    unsigned tile_grid = 0;  // workgroups of the per-tile kernels (0: no finite points)
+    const int32_t* nbr = nullptr;  // non-core neighbour lists (nullptr: label by stencil scan)
+    int nbr_k = 0;
 };
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
@@ -153,6 +156,7 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
 //   1: in = const uint8_t* flags (0/1)
 //   2: head flags of a sorted u32 key array: v[i] = (i == 0 || key[i] != key[i-1])
 //   3: head flags of key >> 2 (the eps cell of a quarter-cell key)
+//   4: head flags of key >> 8 (the tile of a quarter-cell key)
 // Writes out[0..n) and, if total_dev != nullptr, the total at *total_dev.
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
                     int32_t* total_dev, DevBuf& tmp);

@@ -19,11 +19,12 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE_OF = {  # kernel base name -> bench.py stage name
-    "quarter_union_kernel": "union", "union_kernel": "union", "count_kernel": "count",
+    "tile_union_kernel": "union_tile", "edge_union_kernel": "union_edge",
+    "quarter_root_kernel": "union_root", "union_kernel": "union", "count_tile_kernel": "count",
     "output_kernel": "output", "gather_kernel": "gather", "radix_downsweep_kernel":
     "sort_downsweep", "radix_upsweep_kernel": "sort_upsweep", "final_kernel": "final",
-    "quarter_init_kernel": "quarter_init", "segs_kernel": "segs", "cells_kernel": "cells",
-    "bin_kernel": "bin", "bbox_partial_kernel": "bbox",
+    "quarter_init_kernel": "quarter_init", "segs_kernel": "segs", "group_kernel": "cells",
+    "tslot_kernel": "tables", "bin_kernel": "bin", "bbox_partial_kernel": "bbox",
 }
 
 
