@@ -151,26 +151,122 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
     xy[p] = make_double2(x[o], y[o]);
 }
 
-// gidx[p] holds the exclusive scan of head flags on entry; converted to the group index.
-// shift = 0: quarter cells (full key); 2: eps cells; 8: tiles.
-__global__ __launch_bounds__(kBlock) void group_kernel(const uint32_t* __restrict__ key,
-                                                       int shift, int64_t nf,
-                                                       int32_t* __restrict__ gidx,
-                                                       uint32_t* __restrict__ gkey,
-                                                       int32_t* __restrict__ gstart,
-                                                       const int32_t* __restrict__ ngroups) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= nf) {
-        if (p == nf) gstart[*ngroups] = (int32_t)nf;
-        return;
+// Occupied tiles, eps cells and quarter cells in one pass over the sorted keys (they are
+// nested prefixes of the key: tile = key >> 8, cell = key >> 2, quarter = key).  A head flag
+// marks the first slot of each group; groups are numbered by an exclusive scan of the flags:
+// heads_reduce counts the flags per 4096-slot tile, the three rows of counts are scanned, and
+// heads_down ranks each slot within its tile with wave ballots and writes the group tables.
+constexpr int kHeadTile = 4096;
+
+struct Heads {
+    bool c, q, t;
+};
+
+__device__ __forceinline__ Heads heads_at(const uint32_t* __restrict__ key, int64_t p,
+                                          int64_t nf, uint32_t& k) {
+    if (p >= nf) return {false, false, false};
+    k = key[p];
+    if (p == 0) return {true, true, true};
+    const uint32_t km = key[p - 1];
+    return {(k >> 2) != (km >> 2), k != km, (k >> 8) != (km >> 8)};
+}
+
+__global__ __launch_bounds__(kBlock) void heads_reduce_kernel(const uint32_t* __restrict__ key,
+                                                              int64_t nf, int nb,
+                                                              int32_t* __restrict__ partial) {
+    __shared__ int wsum[3][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kHeadTile;
+    int c = 0, q = 0, t = 0;
+    for (int r = 0; r < kHeadTile / kBlock; ++r) {
+        uint32_t k;
+        const Heads h = heads_at(key, base + r * kBlock + threadIdx.x, nf, k);
+        c += h.c;
+        q += h.q;
+        t += h.t;
     }
-    const int32_t ex = gidx[p];
-    const bool head = (p == 0) || (key[p] >> shift) != (key[p - 1] >> shift);
-    if (head) {
-        gkey[ex] = key[p] >> shift;
-        gstart[ex] = (int32_t)p;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, 64);
+        q += __shfl_xor(q, o, 64);
+        t += __shfl_xor(t, o, 64);
     }
-    gidx[p] = ex + (head ? 1 : 0) - 1;
+    const int w = threadIdx.x >> 6;
+    if (__lane_id() == 0) {
+        wsum[0][w] = c;
+        wsum[1][w] = q;
+        wsum[2][w] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        int s = 0;
+        for (int k = 0; k < kBlock / 64; ++k) s += wsum[threadIdx.x][k];
+        partial[threadIdx.x * nb + blockIdx.x] = s;
+    }
+}
+
+// offs: the exclusive scans of the three rows of partial counts.  qidx == nullptr: no quarter
+// tables (quarter cells are not cliques of the predicate).
+__global__ __launch_bounds__(kBlock) void heads_down_kernel(
+    const uint32_t* __restrict__ key, int64_t nf, int nb, const int32_t* __restrict__ offs,
+    int32_t* __restrict__ cell, uint32_t* __restrict__ ckey, int32_t* __restrict__ cstart,
+    int32_t* __restrict__ qidx, uint32_t* __restrict__ qkey, int32_t* __restrict__ qstart,
+    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart) {
+    __shared__ int wcnt[2][3][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kHeadTile;
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int oc = offs[blockIdx.x], oq = offs[nb + blockIdx.x], ot = offs[2 * nb + blockIdx.x];
+    for (int r = 0; r < kHeadTile / kBlock; ++r) {
+        const int64_t p = base + r * kBlock + threadIdx.x;
+        uint32_t k = 0;
+        const Heads h = heads_at(key, p, nf, k);
+        const uint64_t bc = __ballot(h.c), bq = __ballot(h.q), bt = __ballot(h.t);
+        if (lane == 0) {
+            wcnt[r & 1][0][w] = __popcll(bc);
+            wcnt[r & 1][1][w] = __popcll(bq);
+            wcnt[r & 1][2][w] = __popcll(bt);
+        }
+        __syncthreads();
+        int wc = 0, wq = 0, wt = 0, tc = 0, tq = 0, tt = 0;
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+            const int c = wcnt[r & 1][0][v], q = wcnt[r & 1][1][v], t = wcnt[r & 1][2][v];
+            wc += v < w ? c : 0;
+            wq += v < w ? q : 0;
+            wt += v < w ? t : 0;
+            tc += c;
+            tq += q;
+            tt += t;
+        }
+        if (p < nf) {
+            const int ic = oc + wc + __popcll(bc & lt);  // heads before p
+            const int iq = oq + wq + __popcll(bq & lt);
+            const int it = ot + wt + __popcll(bt & lt);
+            cell[p] = ic + h.c - 1;
+            if (h.c) {
+                ckey[ic] = k >> 2;
+                cstart[ic] = (int32_t)p;
+            }
+            if (qidx) {
+                qidx[p] = iq + h.q - 1;
+                if (h.q) {
+                    qkey[iq] = k;
+                    qstart[iq] = (int32_t)p;
+                }
+            }
+            if (h.t) {
+                tkey[it] = k >> 8;
+                tstart[it] = (int32_t)p;
+            }
+            if (p == nf - 1) {  // end sentinels
+                cstart[ic + h.c] = (int32_t)nf;
+                if (qidx) qstart[iq + h.q] = (int32_t)nf;
+                tstart[it + h.t] = (int32_t)nf;
+            }
+        }
+        oc += tc;
+        oq += tq;
+        ot += tt;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void tmap_kernel(const uint32_t* __restrict__ tkey,
@@ -182,24 +278,47 @@ __global__ __launch_bounds__(kBlock) void tmap_kernel(const uint32_t* __restrict
 
 // tslot[t][l] = first slot of the first occupied cell of tile t with local index >= l
 // (tile end if none): the slots of local cells [l0, l1] are [tslot[l0], tslot[l1 + 1]).
+// With quarter cells (qidx != nullptr) also tq[t][l], the same table over quarter indices, and
+// tnb[t] = occupied index of the E, S, SE, SW neighbour tiles (-1: empty), for edge_union.
 __global__ __launch_bounds__(kBlock) void tslot_kernel(
     const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
     const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ cell,
     const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
-    const int32_t* __restrict__ ncells_p, int32_t* __restrict__ tslot) {
-    const int t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= *ntiles_p) return;
-    const int C = *ncells_p;
+    const int32_t* __restrict__ ncells_p, const int32_t* __restrict__ qidx,
+    const int32_t* __restrict__ tmap, GridParams g, int32_t* __restrict__ tslot,
+    int32_t* __restrict__ tq, int4* __restrict__ tnb) {
+    // one wave per tile, one lane per local cell
+    const int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (t >= *ntiles_p) return;  // wave-uniform; no block barriers below
     const uint32_t tk = tkey[t];
-    int32_t* ts = tslot + (int64_t)t * kTslot;
-    int pos = 0;
-    for (int c = cell[tstart[t]]; c < C && (ckey[c] >> 6) == tk; ++c) {
-        const int l = (int)(ckey[c] & 63u);
-        const int st = cstart[c];
-        while (pos <= l) ts[pos++] = st;
+    const int ts0 = tstart[t], end = tstart[t + 1];
+    const int c0 = cell[ts0];
+    const int c = c0 + lane;
+    const bool mine = c < *ncells_p && (ckey[c] >> 6) == tk;
+    uint64_t occ = mine ? 1ull << (ckey[c] & 63u) : 0ull;  // occupied local cells
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) occ |= __shfl_xor(occ, o, 64);
+    const uint64_t rest = occ >> lane;
+    int st = end;
+    if (rest) {
+        const int nl = lane + __builtin_ctzll(rest);  // first occupied local >= lane
+        const int rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
+        st = cstart[c0 + rank];
     }
-    const int end = tstart[t + 1];
-    while (pos < kTslot) ts[pos++] = end;
+    int32_t* ts = tslot + (int64_t)t * kTslot;
+    ts[lane] = st;
+    if (lane == 0) ts[64] = end;
+    if (qidx) {
+        int32_t* tqq = tq + (int64_t)t * kTslot;
+        tqq[lane] = st < end ? qidx[st] : qidx[end - 1] + 1;
+        if (lane == 0) {
+            tqq[64] = qidx[end - 1] + 1;
+            const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
+            tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
+                               tile_occ(tmap, g, tx + 1, ty + 1), tile_occ(tmap, g, tx - 1, ty + 1));
+        }
+    }
 }
 
 // Per cell: the stencil's slot pieces (rows cy, cy-1, cy+1; a row of 3 cells splits in two
@@ -826,65 +945,63 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
     }
 }
 
-// Quarter pairs that cross a tile edge.  One wave per (tile, relation): E (tx+1, ty),
-// S (tx, ty+1), SE (tx+1, ty+1), SW (tx-1, ty+1) -- with the mirrored relations of the other
-// tiles, every pair of adjacent tiles exactly once.  The wave loads the quarter cells of the
-// two facing cell strips (<= 8 cells = 32 quarters per side) into LDS, tags each with its tile
-// component (parent of its rep after tile_union), pre-joins equal tags in an LDS union-find,
-// then pair-tests facing quarters within quarter distance 2 (adjacent first) only while the
-// two are not yet joined in LDS.  A found edge is one global union of the two tile components,
-// so the global union-find sees about one operation per component pair per tile edge.
-constexpr int kEdgeNodes = 64;
+// Quarter pairs that cross a tile edge.  One wave per (tile, side): side 0 pairs the tile's
+// east cell column with the E tile's west column plus the SE tile's corner cell; side 1 its
+// south row with the S tile's north row plus the SW tile's corner cell.  With the mirrored
+// sides of the other tiles, every pair of adjacent cells in different tiles is covered once.
+// The wave loads the quarter cells of the facing strips (<= 32 + 36) into LDS, tags each with
+// its tile component (qcomp, from tile_union), pre-joins equal tags in an LDS union-find, then
+// pair-tests facing quarters within quarter distance 2 (adjacent first) only while the two are
+// not yet joined in LDS.  A found edge is one global union of the two tile components, so the
+// global union-find sees about one operation per component pair per tile side.
+constexpr int kEdgeNodes = 72;
 
 __global__ __launch_bounds__(kBlock) void edge_union_kernel(
-    const double2* __restrict__ xy, const uint32_t* __restrict__ tkey,
-    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ tmap,
-    const int32_t* __restrict__ tslot, const int32_t* __restrict__ qidx,
+    const double2* __restrict__ xy, const int32_t* __restrict__ ntiles_p,
+    const int32_t* __restrict__ tq, const int4* __restrict__ tnb,
     const int4* __restrict__ qinfo, const int2* __restrict__ qg,
-    const int32_t* __restrict__ qcomp, GridParams g, double eps2,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
-    int32_t* __restrict__ parent) {
+    const int32_t* __restrict__ qcomp, double eps2, const int32_t* __restrict__ perm,
+    const uint8_t* __restrict__ core, int32_t* __restrict__ parent) {
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
     __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
     __shared__ int ncomp[kBlock / 64][kEdgeNodes];
     __shared__ int nlp[kBlock / 64][kEdgeNodes];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int dtx = (w == 0 || w == 2) ? 1 : (w == 3 ? -1 : 0);
-    const int dty = w == 0 ? 0 : 1;
+    const int side = w & 1;
     const int ntiles = *ntiles_p;
+    const int npairs = (ntiles + 1) >> 1;
     int* lp = nlp[w];
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t tk = tkey[t];
-        const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
-        const int occB = tile_occ(tmap, g, tx + dtx, ty + dty);  // wave-uniform
+    for (int tp = blockIdx.x; tp < npairs; tp += gridDim.x) {
+        const int t = 2 * tp + (w >> 1);
         int nA = 0, ntot = 0;
-        if (occB >= 0) {
-            const int side = lane >> 3, k = lane & 7;
-            const int ncell = w < 2 ? 8 : 1;
-            int cnt = 0, q0 = 0;
-            if (lane < 16 && k < ncell) {
-                int lxA, lyA, lxB, lyB;
-                if (w == 0) { lxA = 7; lyA = k; lxB = 0; lyB = k; }
-                else if (w == 1) { lxA = k; lyA = 7; lxB = k; lyB = 0; }
-                else if (w == 2) { lxA = 7; lyA = 7; lxB = 0; lyB = 0; }
-                else { lxA = 0; lyA = 7; lxB = 7; lyB = 0; }
-                const int occ = side ? occB : t;
-                const int l = side ? lyB * 8 + lxB : lyA * 8 + lxA;
-                const int b = tslot[(int64_t)occ * kTslot + l];
-                const int e = tslot[(int64_t)occ * kTslot + l + 1];
-                if (b < e) {
-                    q0 = qidx[b];
-                    cnt = qidx[e - 1] + 1 - q0;
-                }
+        if (t < ntiles) {  // wave-uniform
+            const int4 nb = tnb[t];
+            const int occB = side ? nb.y : nb.x, occC = side ? nb.w : nb.z;
+            const int k = lane & 7;
+            int occ = -1, l = 0;
+            if (lane < 8) {  // own strip
+                occ = t;
+                l = side ? 56 + k : k * 8 + 7;
+            } else if (lane < 16) {  // facing strip
+                occ = occB;
+                l = side ? k : k * 8;
+            } else if (lane == 16) {  // corner cell
+                occ = occC;
+                l = side ? 7 : 0;
             }
-            int incl = cnt;  // lanes 0-7: side A cells, 8-15: side B cells -> A nodes first
+            int cnt = 0, q0 = 0;
+            if (occ >= 0) {
+                q0 = tq[(int64_t)occ * kTslot + l];
+                cnt = tq[(int64_t)occ * kTslot + l + 1] - q0;
+            }
+            int incl = cnt;  // own nodes first, then facing + corner
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
+            for (int o = 1; o < 32; o <<= 1) {
                 const int u = __shfl_up(incl, o, 64);
                 if (lane >= o) incl += u;
             }
             nA = __shfl(incl, 7, 64);
-            ntot = __shfl(incl, 15, 64);
+            ntot = __shfl(incl, 16, 64);
             for (int j = 0; j < cnt; ++j) {
                 const int idx = incl - cnt + j;
                 nqi[w][idx] = qinfo[q0 + j];
@@ -893,47 +1010,43 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
             }
         }
         __syncthreads();
-        const int a = lane & 31, half = lane >> 5;  // two lanes per side-A quarter
-        int4 me = make_int4(0, 0, -1, 0);
-        int2 mg = make_int2(0, 0);
-        int comp = -1;
-        if (a < ntot) {
-            me = nqi[w][a];
-            mg = ngq[w][a];
-            comp = ncomp[w][a];
-        }
-        if (lane < ntot) {  // pre-join quarters of one side sharing a tile component
-            const int c = ncomp[w][lane];
-            int r = lane;
+        for (int i = lane; i < ntot; i += 64) {  // pre-join nodes sharing a tile component
+            const int c = ncomp[w][i];
+            int r = i;
             if (c >= 0)
-                for (int j = lane < nA ? 0 : nA; j < lane; ++j)
+                for (int j = i < nA ? 0 : nA; j < i; ++j)
                     if (ncomp[w][j] == c) {
                         r = j;
                         break;
                     }
-            lp[lane] = r;
+            lp[i] = r;
         }
         __syncthreads();
-        if (a < nA && me.z >= 0) {
-            double px[kQReg], py[kQReg];
-            const int na = load_own(xy, me, 0, px, py);
+        const int a = lane & 31, half = lane >> 5;  // two lanes per own-strip quarter
+        if (a < nA) {
+            const int4 me = nqi[w][a];
+            const int2 mg = ngq[w][a];
+            if (me.z >= 0) {
+                double px[kQReg], py[kQReg];
+                const int na = load_own(xy, me, 0, px, py);
 #pragma unroll
-            for (int sweep = 1; sweep <= 2; ++sweep)
-                for (int b = nA + half; b < ntot; b += 2) {
-                    const int2 og = ngq[w][b];
-                    if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
-                    const int4 o = nqi[w][b];
-                    if (o.z < 0) continue;
-                    if (lfind(lp, a) == lfind(lp, b)) continue;
-                    const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y, (uint32_t)o.w,
-                                                        core, 0, eps2)
-                                           : pair_found_generic(xy, 0, me, o, core, eps2);
-                    if (!f) continue;
-                    lunite(lp, a, b);
-                    const int ra = uf_find(parent, comp);
-                    const int rb = uf_find(parent, ncomp[w][b]);
-                    if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
-                }
+                for (int sweep = 1; sweep <= 2; ++sweep)
+                    for (int b = nA + half; b < ntot; b += 2) {
+                        const int2 og = ngq[w][b];
+                        if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
+                        const int4 o = nqi[w][b];
+                        if (o.z < 0) continue;
+                        if (lfind(lp, a) == lfind(lp, b)) continue;
+                        const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
+                                                            (uint32_t)o.w, core, 0, eps2)
+                                               : pair_found_generic(xy, 0, me, o, core, eps2);
+                        if (!f) continue;
+                        lunite(lp, a, b);
+                        const int ra = uf_find(parent, ncomp[w][a]);
+                        const int rb = uf_find(parent, ncomp[w][b]);
+                        if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
+                    }
+            }
         }
         __syncthreads();
     }
@@ -1185,7 +1298,6 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(nfa * sizeof(uint32_t)));
     int32_t* cstart = static_cast<int32_t*>(ws.cstart.ensure((nfa + 1) * sizeof(int32_t)));
     Seg* seg = static_cast<Seg*>(ws.seg.ensure(nfa * sizeof(Seg)));
-    int32_t* tidx = static_cast<int32_t*>(ws.tidx.ensure(nfa * sizeof(int32_t)));
     uint32_t* tkey = static_cast<uint32_t*>(ws.tkey.ensure(nfa * sizeof(uint32_t)));
     int32_t* tstart = static_cast<int32_t*>(ws.tstart.ensure((nfa + 1) * sizeof(int32_t)));
     int32_t* tmap =
@@ -1202,7 +1314,11 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     int4* qinfo = nullptr;
     int2* qg = nullptr;
     int32_t* qcomp = nullptr;
+    int32_t* tq = nullptr;
+    int4* tnb = nullptr;
     if (clique) {
+        tq = static_cast<int32_t*>(ws.tq.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
+        tnb = static_cast<int4*>(ws.tnb.ensure((size_t)ntile_bound * sizeof(int4)));
         qcomp = static_cast<int32_t*>(ws.qcomp.ensure(nfa * sizeof(int32_t)));
         qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
         qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
@@ -1220,20 +1336,19 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "cells");
-            exclusive_scan(s, 3, key, cell, nf, &misc_i[0], ws.scan_tmp);
-            hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 2, nf,
-                               cell, ckey, cstart, &misc_i[0]);
+            const int nb = (int)((nf + kHeadTile - 1) / kHeadTile);
+            int32_t* part =
+                static_cast<int32_t*>(ws.heads.ensure(6 * (size_t)nb * sizeof(int32_t)));
+            int32_t* offs = part + 3 * nb;
+            hipLaunchKernelGGL(heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf, nb,
+                               part);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            exclusive_scan(s, 4, key, tidx, nf, &misc_i[4], ws.scan_tmp);
-            hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 8, nf,
-                               tidx, tkey, tstart, &misc_i[4]);
+            exclusive_scan(s, 0, part, offs, nb, &misc_i[0], ws.scan_tmp);
+            if (clique) exclusive_scan(s, 0, part + nb, offs + nb, nb, &misc_i[3], ws.scan_tmp);
+            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &misc_i[4], ws.scan_tmp);
+            hipLaunchKernelGGL(heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf, nb, offs,
+                               cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            if (clique) {
-                exclusive_scan(s, 2, key, qidx, nf, &misc_i[3], ws.scan_tmp);
-                hipLaunchKernelGGL(group_kernel, dim3(nblk(nf + 1)), dim3(kBlock), 0, s, key, 0,
-                                   nf, qidx, qkey, qstart, &misc_i[3]);
-                DBSCAN_HIP_CHECK(hipGetLastError());
-            }
         }
         {
             StageTimer t(prof, s, "tables");
@@ -1242,8 +1357,10 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
             hipLaunchKernelGGL(tmap_kernel, dim3(nblk(ntile_bound)), dim3(kBlock), 0, s, tkey,
                                &misc_i[4], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(tslot_kernel, dim3(nblk(ntile_bound)), dim3(kBlock), 0, s, tstart,
-                               tkey, &misc_i[4], cell, ckey, cstart, &misc_i[0], tslot);
+            hipLaunchKernelGGL(tslot_kernel, dim3((unsigned)((ntile_bound + 3) / 4)), dim3(kBlock),
+                               0, s, tstart,
+                               tkey, &misc_i[4], cell, ckey, cstart, &misc_i[0], qidx, tmap, g,
+                               tslot, tq, tnb);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -1304,9 +1421,8 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "union_edge");
-            hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tkey,
-                               &misc_i[4], tmap, tslot, qidx, qinfo, qg, qcomp, g, eps2, perm,
-                               core, parent);
+            hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
+                               &misc_i[4], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");

@@ -7,9 +7,10 @@
 //   xy[nf]   double2 sorted coordinates, SoA->AoS so one 16-B load feeds a candidate test
 //   cell[nf] i32 occupied-cell index of each sorted slot
 //   ckey[C], cstart[C+1]  occupied cells (key >> 2) and their first slot
-//   tidx[nf], tkey[T], tstart[T+1]  occupied tiles (key >> 8) and their first slot
+//   tkey[T], tstart[T+1]  occupied tiles (key >> 8) and their first slot
 //   tmap[ntx*nty]  occupied-tile index of every tile of the grid (-1: empty)
 //   tslot[T][65]   first slot of the first occupied cell with local index >= l
+//   tq[T][65], tnb[T]  the tslot table over quarter indices; E/S/SE/SW neighbour tiles
 //   seg[C]   64 B: <= 6 slot pieces of the 3x3 stencil + the own cell range
 //   qidx[nf], qkey[Q], qstart[Q+1]  quarter cells (2x2 per eps cell; key low 2 bits =
 //            quadrant): side ~eps/2, so each is a clique under the exact predicate
@@ -92,15 +93,15 @@ struct StageTimer {
 
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
-        is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, tidx, tkey, tstart, tmap,
-        tslot, qcomp, nbr;
+        is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
+        tslot, qcomp, nbr, tq, tnb;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
-                          &qstart, &qrep, &qmask, &blockcnt, &tidx, &tkey, &tstart, &tmap, &tslot,
-                          &qcomp, &nbr})
+                          &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
+                          &qcomp, &nbr, &tq, &tnb})
             b->release();
     }
 };
@@ -156,7 +157,6 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
 //   1: in = const uint8_t* flags (0/1)
 //   2: head flags of a sorted u32 key array: v[i] = (i == 0 || key[i] != key[i-1])
 //   3: head flags of key >> 2 (the eps cell of a quarter-cell key)
-//   4: head flags of key >> 8 (the tile of a quarter-cell key)
 // Writes out[0..n) and, if total_dev != nullptr, the total at *total_dev.
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
                     int32_t* total_dev, DevBuf& tmp);

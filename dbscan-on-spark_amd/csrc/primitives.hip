@@ -49,12 +49,9 @@ __device__ __forceinline__ int scan_value(const void* in, int64_t i, int64_t n) 
     } else if constexpr (MODE == 2) {
         const uint32_t* k = static_cast<const uint32_t*>(in);
         return (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
-    } else if constexpr (MODE == 3) {  // head flags of key >> 2 (cell of a quarter-cell key)
+    } else {  // head flags of key >> 2 (cell of a quarter-cell key)
         const uint32_t* k = static_cast<const uint32_t*>(in);
         return (i == 0 || (k[i] >> 2) != (k[i - 1] >> 2)) ? 1 : 0;
-    } else {  // head flags of key >> 8 (tile of a quarter-cell key)
-        const uint32_t* k = static_cast<const uint32_t*>(in);
-        return (i == 0 || (k[i] >> 8) != (k[i - 1] >> 8)) ? 1 : 0;
     }
 }
 
@@ -362,8 +359,7 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
         case 0: scan_impl<0>(s, in, out, n, total_dev, t, need); break;
         case 1: scan_impl<1>(s, in, out, n, total_dev, t, need); break;
         case 2: scan_impl<2>(s, in, out, n, total_dev, t, need); break;
-        case 3: scan_impl<3>(s, in, out, n, total_dev, t, need); break;
-        default: scan_impl<4>(s, in, out, n, total_dev, t, need); break;
+        default: scan_impl<3>(s, in, out, n, total_dev, t, need); break;
     }
 }
 
