@@ -373,11 +373,12 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
 
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {
     if (!h || !out) return DBSCAN_EARG;
-    const int64_t v[9] = {h->stats.n,  h->stats.nf,  h->stats.ncells,
-                          h->stats.ncore, h->stats.nclusters, h->stats.nx,
-                          h->stats.ny, h->stats.bits, h->stats.grid_mode};
+    const int64_t v[11] = {h->stats.n,     h->stats.nf,        h->stats.ncells,
+                           h->stats.ncore, h->stats.nclusters, h->stats.nx,
+                           h->stats.ny,    h->stats.bits,      h->stats.grid_mode,
+                           h->stats.ntiles, h->stats.clique};
     int k = 0;
-    for (; k < max && k < 9; ++k) out[k] = v[k];
+    for (; k < max && k < 11; ++k) out[k] = v[k];
     return k;
 }
 

@@ -385,31 +385,64 @@ struct TileStage {
     int cn[100];
 };
 
-__device__ bool stage_tile(int t, const double2* __restrict__ xy,
-                           const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
-                           const int32_t* __restrict__ tmap, const int32_t* __restrict__ tslot,
-                           const GridParams& g, TileStage& st, double2* buf, int cap) {
+// tstage[t][k] = (first slot, point count) of extended cell k of tile t: the staging table of
+// the per-tile kernels, so that staging a tile is one coalesced load per extended cell.
+__global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restrict__ tkey,
+                                                        const int32_t* __restrict__ ntiles_p,
+                                                        const int32_t* __restrict__ tmap,
+                                                        const int32_t* __restrict__ tslot,
+                                                        GridParams g, int2* __restrict__ tstage) {
+    const int t = blockIdx.x * 2 + (threadIdx.x >> 7);
+    const int k = threadIdx.x & 127;
+    if (t >= *ntiles_p || k >= 100) return;
+    const uint32_t tk = tkey[t];
+    const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
+    const int ey = k / 10 - 1, ex = k % 10 - 1;
+    const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
+    const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
+    const int occ = tile_occ(tmap, g, tx, ty);
+    int b = 0, cnt = 0;
+    if (occ >= 0) {
+        const int l = (ey & 7) * 8 + (ex & 7);
+        b = tslot[(int64_t)occ * kTslot + l];
+        cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
+    }
+    tstage[(int64_t)t * 100 + k] = make_int2(b, cnt);
+}
+
+struct StageMeta {  // one tile's staging table, held in registers (lanes < 100; lane 0: range)
+    int b = 0, cnt = 0, ts = 0, te = 0;
+};
+
+__device__ __forceinline__ StageMeta stage_meta(int t, int ntiles,
+                                                const int2* __restrict__ tstage,
+                                                const int32_t* __restrict__ tstart) {
+    StageMeta m;
+    if (t >= ntiles) return m;
     const int tid = threadIdx.x;
     if (tid < 100) {
-        const uint32_t tk = tkey[t];
-        const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
-        const int ey = tid / 10 - 1, ex = tid % 10 - 1;
-        const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
-        const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
-        const int occ = tile_occ(tmap, g, tx, ty);
-        int b = 0, cnt = 0;
-        if (occ >= 0) {
-            const int l = (ey & 7) * 8 + (ex & 7);
-            b = tslot[(int64_t)occ * kTslot + l];
-            cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
-        }
-        st.cb[tid] = b;
-        st.cn[tid] = cnt;
+        const int2 v = tstage[(int64_t)t * 100 + tid];
+        m.b = v.x;
+        m.cnt = v.y;
     }
     if (tid == 0) {
-        st.ts = tstart[t];
-        st.te = tstart[t + 1];
-        st.t = t;
+        m.ts = tstart[t];
+        m.te = tstart[t + 1];
+    }
+    return m;
+}
+
+template <int CAP>
+__device__ bool stage_build(const StageMeta& m, const double2* __restrict__ xy, TileStage& st,
+                            double2* buf) {
+    const int tid = threadIdx.x;
+    if (tid < 100) {
+        st.cb[tid] = m.b;
+        st.cn[tid] = m.cnt;
+    }
+    if (tid == 0) {
+        st.ts = m.ts;
+        st.te = m.te;
     }
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the 100 counts by wave 0 (2 chunks)
@@ -429,19 +462,24 @@ __device__ bool stage_tile(int t, const double2* __restrict__ xy,
         if (tid == 0) {
             st.off[100] = carry;
             st.total = carry;
-            st.ok = carry <= cap;
+            st.ok = carry <= CAP;
         }
     }
     __syncthreads();
     if (st.ok) {
+        // unrolled so that a thread's loads are in flight together
+        constexpr int kPer = (CAP + kBlock - 1) / kBlock;
         const int total = st.total;
-        for (int i = tid; i < total; i += kBlock) {
-            int lo = 0, hi = 99;  // largest k with off[k] <= i
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (st.off[mid] <= i) lo = mid; else hi = mid - 1;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = tid + u * kBlock;
+            if (i < total) {
+                int lo = 0;  // largest k with off[k] <= i
+#pragma unroll
+                for (int s = 64; s > 0; s >>= 1)
+                    if (lo + s < 100 && st.off[lo + s] <= i) lo += s;
+                buf[i] = xy[st.cb[lo] + (i - st.off[lo])];
             }
-            buf[i] = xy[st.cb[lo] + (i - st.off[lo])];
         }
     }
     __syncthreads();
@@ -479,7 +517,7 @@ __device__ __forceinline__ LdsRanges lds_ranges(const TileStage& st, int l) {
 template <bool REC, class Src>
 __device__ __forceinline__ bool scan_count(const Src* __restrict__ src, int b, int e,
                                            double2 me, double eps2, int min_points, int& cnt,
-                                           uint16_t* lst, int nbr_k) {
+                                           uint16_t* lst, int nbr_k, int tag = 0) {
     int j = b;
     for (; j + 8 <= e; j += 8) {
         double2 qq[8];
@@ -488,7 +526,7 @@ __device__ __forceinline__ bool scan_count(const Src* __restrict__ src, int b, i
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const bool hit = within_eps(me.x, me.y, qq[u].x, qq[u].y, eps2);
-            if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)(j + u);
+            if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)((j + u) | tag);
             cnt += hit ? 1 : 0;
         }
         if (cnt >= min_points) return true;
@@ -496,13 +534,14 @@ __device__ __forceinline__ bool scan_count(const Src* __restrict__ src, int b, i
     for (; j < e; ++j) {
         const double2 q = src[j];
         const bool hit = within_eps(me.x, me.y, q.x, q.y, eps2);
-        if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)j;
+        if (REC && hit && cnt < nbr_k) lst[cnt * kBlock] = (uint16_t)(j | tag);
         cnt += hit ? 1 : 0;
     }
     return cnt >= min_points;
 }
 
-// one count over ranges (b[k], e[k]) with the own cell [cs, ce) first and excluded after
+// one count over ranges (b[k], e[k]) with the own cell [cs, ce) first and excluded after;
+// recorded hits are tagged with their range: LDS index | k << 12
 template <int K, bool REC = false>
 __device__ __forceinline__ void count_pieces(const double2* __restrict__ src, const int* b,
                                              const int* e, int cs, int ce, double2 me,
@@ -513,93 +552,148 @@ __device__ __forceinline__ void count_pieces(const double2* __restrict__ src, co
     for (int k = 0; k < K; ++k) {
         const int lo = b[k], hi = e[k];
         if (lo <= cs && ce <= hi) {  // the piece holding the own cell: around it
-            if (scan_count<REC>(src, lo, cs, me, eps2, min_points, cnt, lst, nbr_k)) return;
-            if (scan_count<REC>(src, ce, hi, me, eps2, min_points, cnt, lst, nbr_k)) return;
-        } else if (scan_count<REC>(src, lo, hi, me, eps2, min_points, cnt, lst, nbr_k)) {
+            if (scan_count<REC>(src, lo, cs, me, eps2, min_points, cnt, lst, nbr_k, k << 12))
+                return;
+            if (scan_count<REC>(src, ce, hi, me, eps2, min_points, cnt, lst, nbr_k, k << 12))
+                return;
+        } else if (scan_count<REC>(src, lo, hi, me, eps2, min_points, cnt, lst, nbr_k, k << 12)) {
             return;
         }
     }
 }
 
+// One point's core decision + (non-core, nbr != nullptr) its neighbour list.  Staged: the
+// point sits at LDS index j of local cell l and global slot p.  Unstaged: global stencil pieces.
+template <bool STAGED>
+__device__ __forceinline__ bool count_point(const TileStage& st, const double2* __restrict__ buf,
+                                            const double2* __restrict__ xy,
+                                            const int32_t* __restrict__ cell,
+                                            const Seg* __restrict__ seg, int j, int l, int p,
+                                            double eps2, int min_points, uint16_t* lst,
+                                            int32_t* __restrict__ nbr, int nbr_k) {
+    int cnt = 0;
+    if constexpr (STAGED) {
+        const double2 me = buf[j];
+        const LdsRanges r = lds_ranges(st, l);
+        if (nbr)
+            count_pieces<3, true>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points, cnt, lst,
+                                  nbr_k);
+        else
+            count_pieces<3>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points, cnt);
+        if (cnt >= min_points) return true;
+        // A non-core has fewer than minPoints neighbours, every one of them noted by the count
+        // (self included): keep their slots, -1 terminated, for the label pass.
+        if (nbr) {
+            int32_t* out = nbr + (int64_t)p * nbr_k;
+            int w = 0;
+            const int lx = l & 7, ly = l >> 3;
+            for (int k = 0; k < cnt; ++k) {
+                const int v = lst[k * kBlock];
+                const int q = v & 4095, row = v >> 12;  // row: 0 own, 1 above, 2 below
+                const int k0 = (ly + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + lx;
+                const int c = k0 + (q >= st.off[k0 + 1] ? 1 : 0) + (q >= st.off[k0 + 2] ? 1 : 0);
+                const int sq = st.cb[c] + (q - st.off[c]);
+                if (sq != p) out[w++] = sq;
+            }
+            if (w < nbr_k) out[w] = -1;
+        }
+        return false;
+    } else {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        count_pieces<6>(xy, s.b, s.e, s.cs, s.ce, me, eps2, min_points, cnt);
+        if (cnt >= min_points) return true;
+        if (nbr) {
+            int32_t* out = nbr + (int64_t)p * nbr_k;
+            int w = 0;
+            for (int k = 0; k < 6; ++k)
+                for (int q = s.b[k]; q < s.e[k]; ++q) {
+                    const double2 v = xy[q];
+                    if (q != p && within_eps(me.x, me.y, v.x, v.y, eps2) && w < nbr_k)
+                        out[w++] = q;
+                }
+            if (w < nbr_k) out[w] = -1;
+        }
+        return false;
+    }
+}
+
+// Neighbour counts of one tile per loop trip.  Staged tiles are walked in LDS order (own rows
+// of the 10x10 extended grid), so a point's coordinates and cell come from LDS, not HBM.
 template <int CAP>
 __global__ __launch_bounds__(kBlock) void count_tile_kernel(
-    const double2* __restrict__ xy, const uint32_t* __restrict__ key,
-    const int32_t* __restrict__ cell, const Seg* __restrict__ seg,
-    const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
-    const int32_t* __restrict__ tmap, const int32_t* __restrict__ tslot,
-    const int32_t* __restrict__ ntiles_p, GridParams g, double eps2, int32_t min_points,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ zone,
-    const int32_t* __restrict__ qidx, const int32_t* __restrict__ qstart,
-    uint8_t* __restrict__ core, int32_t* __restrict__ parent, int32_t* __restrict__ block_cores,
-    int32_t* __restrict__ nbr, int nbr_k) {
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
+    const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
+    int32_t min_points, const int32_t* __restrict__ perm,
+    const uint8_t* __restrict__ zone, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate) {
     __shared__ TileStage st;
     __shared__ double2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
+    __shared__ int rowoff[9];
     __shared__ uint16_t lsts[kMaxNbr * kBlock];
     uint16_t* lst = lsts + threadIdx.x;
     const int ntiles = *ntiles_p;
     int mine = 0;
+    StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart);
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const bool staged = stage_tile(t, xy, tstart, tkey, tmap, tslot, g, st, buf, CAP);
-        for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
-            bool is_core;
-            if (zone && zone[perm[p]] == 2) {
-                is_core = false;  // outer halo of a slab fit: a count candidate only
-            } else if (min_points <= 0) {
-                is_core = true;
-            } else {
-                const double2 me = xy[p];
-                // a clique quarter holding >= minPoints points (a dense box): core, no test
-                int cnt = 0;
-                if (qidx) {
-                    const int q = qidx[p];
-                    if (qstart[q + 1] - qstart[q] >= min_points) cnt = min_points;
+        const bool staged = stage_build<CAP>(meta, xy, st, buf);
+        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart);  // in flight during the scans
+        if (staged) {
+            if (threadIdx.x == 0) {  // own points per row of the tile: prefix over rows
+                int acc = 0;
+                for (int r = 0; r < 8; ++r) {
+                    rowoff[r] = acc;
+                    acc += st.off[(r + 1) * 10 + 9] - st.off[(r + 1) * 10 + 1];
                 }
-                if (cnt < min_points) {
-                    if (staged && nbr) {
-                        const LdsRanges r = lds_ranges(st, (int)((key[p] >> 2) & 63u));
-                        count_pieces<3, true>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points,
-                                              cnt, lst, nbr_k);
-                    } else if (staged) {
-                        const LdsRanges r = lds_ranges(st, (int)((key[p] >> 2) & 63u));
-                        count_pieces<3>(buf, r.b, r.e, r.cs, r.ce, me, eps2, min_points, cnt);
-                    } else {
-                        const Seg s = load_seg(seg, cell[p]);
-                        count_pieces<6>(xy, s.b, s.e, s.cs, s.ce, me, eps2, min_points, cnt);
-                    }
-                }
-                is_core = cnt >= min_points;
-                // A non-core has fewer than minPoints neighbours: keep their slots (self
-                // excluded, -1 terminated) so the label pass needs no second stencil scan.
-                if (!is_core && nbr) {
-                    int32_t* out = nbr + (int64_t)p * nbr_k;
-                    int w = 0;
-                    if (staged) {  // the count noted every hit (cnt <= nbr_k): LDS index -> slot
-                        for (int k = 0; k < cnt; ++k) {
-                            const int j = lst[k * kBlock];
-                            int lo = 0, hi = 99;  // extended cell holding LDS index j
-                            while (lo < hi) {
-                                const int mid = (lo + hi + 1) >> 1;
-                                if (st.off[mid] <= j) lo = mid; else hi = mid - 1;
-                            }
-                            const int sj = st.cb[lo] + (j - st.off[lo]);
-                            if (sj != p) out[w++] = sj;
-                        }
-                    } else {
-                        const Seg s = load_seg(seg, cell[p]);
-                        for (int k = 0; k < 6; ++k)
-                            for (int j = s.b[k]; j < s.e[k]; ++j) {
-                                const double2 q = xy[j];
-                                if (j != p && within_eps(me.x, me.y, q.x, q.y, eps2) && w < nbr_k)
-                                    out[w++] = j;
-                            }
-                    }
-                    if (w < nbr_k) out[w] = -1;
-                }
+                rowoff[8] = acc;
             }
-            parent[p] = p;
-            core[p] = is_core ? 1 : 0;
-            mine += is_core ? 1 : 0;
+            __syncthreads();
+            const int own = rowoff[8];
+            for (int i = (int)threadIdx.x; i < own; i += kBlock) {
+                int r = 0;  // row: largest r with rowoff[r] <= i
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (r + s < 8 && rowoff[r + s] <= i) r += s;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - rowoff[r]);
+                int ex = 0;  // cell in the row: largest ex with off[base + ex] <= j
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
+                const int p = st.cb[base + ex] + (j - st.off[base + ex]);
+                bool is_core;
+                if (zone && zone[perm[p]] == 2) {
+                    is_core = false;  // outer halo of a slab fit: a count candidate only
+                } else if (min_points <= 0) {
+                    is_core = true;
+                } else if (ablate == 1) {
+                    is_core = false;
+                } else {
+                    is_core = count_point<true>(st, buf, xy, cell, seg, j, r * 8 + ex, p, eps2,
+                                                min_points, lst, ablate == 2 ? nullptr : nbr,
+                                                nbr_k);
+                }
+                parent[p] = p;
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
+            }
+        } else {
+            for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
+                bool is_core;
+                if (zone && zone[perm[p]] == 2) {
+                    is_core = false;
+                } else if (min_points <= 0) {
+                    is_core = true;
+                } else {
+                    is_core = count_point<false>(st, buf, xy, cell, seg, 0, 0, p, eps2,
+                                                 min_points, lst, nbr, nbr_k);
+                }
+                parent[p] = p;
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
+            }
         }
         __syncthreads();
     }
@@ -745,7 +839,7 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 __global__ __launch_bounds__(kBlock) void quarter_init_kernel(
     const int32_t* __restrict__ qstart, const uint32_t* __restrict__ qkey,
     const int32_t* __restrict__ nq_p, GridParams g, const int32_t* __restrict__ perm,
-    const uint8_t* __restrict__ core, int4* __restrict__ qinfo, int2* __restrict__ qg,
+    const uint8_t* __restrict__ core, int4* __restrict__ qinfo, int4* __restrict__ qg,
     int32_t* __restrict__ parent) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
@@ -764,7 +858,8 @@ __global__ __launch_bounds__(kBlock) void quarter_init_kernel(
     uint32_t cx, cy;
     cell_xy(k >> 2, g.ntx, cx, cy);
     qinfo[q] = make_int4(b, e, rep, (int)mask);
-    qg[q] = make_int2((int)(2 * cx + (k & 1u)), (int)(2 * cy + ((k >> 1) & 1u)));
+    qg[q] = make_int4((int)(2 * cx + (k & 1u)), (int)(2 * cy + ((k >> 1) & 1u)),
+                      rep >= 0 ? best : 0x7FFFFFFF, 0);
     if (rep < 0) return;
     for (int j = b; j < e; ++j)
         if (core[j]) parent[j] = rep;
@@ -868,48 +963,43 @@ __device__ __forceinline__ void lunite(int* lp, int a, int b) {
 
 constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
 
-template <int CAP>
+// One tile per loop trip: quarter records and their quarter-grid neighbours in LDS, the
+// pair tests read the (L2-resident) coordinates directly -- staging them measured slower
+// (fewer resident workgroups; tools/tile_variants.sh, r02).
 __global__ __launch_bounds__(kBlock) void tile_union_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
-    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ qidx,
-    const int4* __restrict__ qinfo, const int2* __restrict__ qg, double eps2,
-    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
-    int32_t* __restrict__ parent, int32_t* __restrict__ qcomp) {
+    const double2* __restrict__ xy, const int32_t* __restrict__ tq,
+    const int32_t* __restrict__ ntiles_p, const int4* __restrict__ qinfo,
+    const int4* __restrict__ qg, double eps2, const int32_t* __restrict__ perm,
+    const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t* __restrict__ qcomp) {
     __shared__ int lp[kMaxTileQ];
     __shared__ int4 lqi[kMaxTileQ];
     __shared__ int qmap[kMaxTileQ];  // 16x16 local quarter grid -> local quarter index
     __shared__ int cmin[kMaxTileQ];
     __shared__ int crep[kMaxTileQ];
-    __shared__ double2 buf[CAP > 0 ? CAP : 1];
     const int ntiles = *ntiles_p;
     const int i = threadIdx.x;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int ts = tstart[t], te = tstart[t + 1];
-        const int q0 = qidx[ts], nq = qidx[te - 1] + 1 - q0;
-        const bool staged = te - ts <= CAP;
+        const int q0 = tq[(int64_t)t * kTslot], nq = tq[(int64_t)t * kTslot + 64] - q0;
         qmap[i] = -1;
         cmin[i] = 0x7FFFFFFF;
-        if (staged)
-            for (int k = i; k < te - ts; k += kBlock) buf[k] = xy[ts + k];
         __syncthreads();
         int lqx = 0, lqy = 0, prio = 0x7FFFFFFF;
         int4 me = make_int4(0, 0, -1, 0);
         if (i < nq) {
             me = qinfo[q0 + i];
-            const int2 gq = qg[q0 + i];
+            const int4 gq = qg[q0 + i];
             lqx = gq.x & 15;
             lqy = gq.y & 15;
+            prio = gq.z;
             lqi[i] = me;
             lp[i] = i;
             qmap[lqy * 16 + lqx] = i;
-            if (me.z >= 0) prio = perm[me.z];
         }
         __syncthreads();
         if (i < nq && me.z >= 0) {
-            const double2* src = staged ? buf : xy;
-            const int off = staged ? ts : 0;
             double px[kQReg], py[kQReg];
-            const int na = load_own(src, me, off, px, py);
+            const int na = load_own(xy, me, 0, px, py);
             // adjacent quarters first (merges happen early), then the distance-2 ring
 #pragma unroll
             for (int sweep = 1; sweep <= 2; ++sweep)
@@ -923,9 +1013,9 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
                         const int4 o = lqi[j];
                         if (o.z < 0) continue;
                         if (lfind(lp, i) == lfind(lp, j)) continue;
-                        const bool f = na >= 0 ? pair_found(px, py, na, src, o.x, o.y,
-                                                            (uint32_t)o.w, core, off, eps2)
-                                               : pair_found_generic(src, off, me, o, core, eps2);
+                        const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
+                                                            (uint32_t)o.w, core, 0, eps2)
+                                               : pair_found_generic(xy, 0, me, o, core, eps2);
                         if (f) lunite(lp, i, j);
                     }
         }
@@ -959,7 +1049,7 @@ constexpr int kEdgeNodes = 72;
 __global__ __launch_bounds__(kBlock) void edge_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ ntiles_p,
     const int32_t* __restrict__ tq, const int4* __restrict__ tnb,
-    const int4* __restrict__ qinfo, const int2* __restrict__ qg,
+    const int4* __restrict__ qinfo, const int4* __restrict__ qg,
     const int32_t* __restrict__ qcomp, double eps2, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, int32_t* __restrict__ parent) {
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
@@ -1005,7 +1095,8 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
             for (int j = 0; j < cnt; ++j) {
                 const int idx = incl - cnt + j;
                 nqi[w][idx] = qinfo[q0 + j];
-                ngq[w][idx] = qg[q0 + j];
+                const int4 gq = qg[q0 + j];
+                ngq[w][idx] = make_int2(gq.x, gq.y);
                 ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
             }
         }
@@ -1205,18 +1296,23 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
     return false;
 }
 
-// LDS staging capacities of the per-tile kernels (points).  DBSCAN_TILE_CAPS="count,union"
-// overrides them for measurements (count: 3072/2048/1024, union: 3072/1536/0); results are
-// identical for every choice (tiles over capacity take the global-memory path).
-struct TileVariant {  // defaults: the fastest of the r02 sweep (tools/tile_variants.sh)
-    int count_cap = 2048, union_cap = 0;
-};
-static const TileVariant& tile_variant() {
-    static const TileVariant v = [] {
-        TileVariant t;
-        if (const char* e = std::getenv("DBSCAN_TILE_CAPS"))
-            std::sscanf(e, "%d,%d", &t.count_cap, &t.union_cap);
-        return t;
+// LDS staging capacity of the count pass (points of a tile + halo).  DBSCAN_COUNT_CAP
+// (3072/2048/1024) overrides it for measurements; results are identical for every choice
+// (tiles over capacity take the global-memory path).  2048 was fastest in the r02 sweep
+// (tools/tile_variants.sh): 40 KB of LDS leaves four workgroups per CU.
+// DBSCAN_COUNT_ABLATE (timing experiments only; results are wrong): 1 = staging only, no
+// neighbour scans; 2 = scans without neighbour lists.
+static int count_ablate() {
+    static const int v = [] {
+        const char* e = std::getenv("DBSCAN_COUNT_ABLATE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+static int count_cap() {
+    static const int v = [] {
+        const char* e = std::getenv("DBSCAN_COUNT_CAP");
+        return e ? std::atoi(e) : 2048;
     }();
     return v;
 }
@@ -1304,15 +1400,17 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         static_cast<int32_t*>(ws.tmap.ensure((size_t)g.ntx * g.nty * sizeof(int32_t)));
     int32_t* tslot =
         static_cast<int32_t*>(ws.tslot.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
+    int2* tstage = static_cast<int2*>(ws.tstage.ensure((size_t)ntile_bound * 100 * sizeof(int2)));
     uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
     int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
     int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
     const bool clique = mode == kGridEps && g.clique;
+    stats.clique = clique ? 1 : 0;
     int32_t* qidx = nullptr;
     uint32_t* qkey = nullptr;
     int32_t* qstart = nullptr;
     int4* qinfo = nullptr;
-    int2* qg = nullptr;
+    int4* qg = nullptr;
     int32_t* qcomp = nullptr;
     int32_t* tq = nullptr;
     int4* tnb = nullptr;
@@ -1324,7 +1422,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
         qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
         qinfo = static_cast<int4*>(ws.qrep.ensure(nfa * sizeof(int4)));
-        qg = static_cast<int2*>(ws.qmask.ensure(nfa * sizeof(int2)));
+        qg = static_cast<int4*>(ws.qmask.ensure(nfa * sizeof(int4)));
     }
 
     if (nf > 0) {
@@ -1362,6 +1460,9 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
                                tkey, &misc_i[4], cell, ckey, cstart, &misc_i[0], qidx, tmap, g,
                                tslot, tq, tnb);
             DBSCAN_HIP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(tstage_kernel, dim3((unsigned)((ntile_bound + 1) / 2)), dim3(kBlock),
+                               0, s, tkey, &misc_i[4], tmap, tslot, g, tstage);
+            DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "segs");
@@ -1383,14 +1484,14 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         StageTimer t(prof, s, "count");
         if (tile_grid) {
             auto kern = count_tile_kernel<2048>;
-            switch (tile_variant().count_cap) {
+            switch (count_cap()) {
                 case 3072: kern = count_tile_kernel<3072>; break;
                 case 1024: kern = count_tile_kernel<1024>; break;
                 default: break;
             }
-            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, key, cell, seg,
-                               tstart, tkey, tmap, tslot, &misc_i[4], g, eps2, a.min_points, perm,
-                               a.zone, qidx, qstart, core, parent, block_cores, nbr, nbr_k);
+            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
+                               tstage, &misc_i[4], eps2, a.min_points, perm, a.zone,
+                               core, parent, block_cores, nbr, nbr_k, count_ablate());
         }
         if (rest_grid)
             hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf, n,
@@ -1409,14 +1510,8 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "union_tile");
-            auto kern = tile_union_kernel<0>;
-            switch (tile_variant().union_cap) {
-                case 1536: kern = tile_union_kernel<1536>; break;
-                case 3072: kern = tile_union_kernel<3072>; break;
-                default: break;
-            }
-            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, &misc_i[4],
-                               qidx, qinfo, qg, eps2, perm, core, parent, qcomp);
+            hipLaunchKernelGGL(tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
+                               &misc_i[4], qinfo, qg, eps2, perm, core, parent, qcomp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -1465,6 +1560,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         k = hv[1];
         stats.ncells = nf > 0 ? hv[0] : 0;
         stats.ncore = hv[2];
+        stats.ntiles = nf > 0 ? hv[4] : 0;
     } else {
         {
             StageTimer t(prof, s, "final");
@@ -1483,6 +1579,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
         stats.ncells = nf > 0 ? hv[0] : 0;
         stats.ncore = hv[2];
+        stats.ntiles = nf > 0 ? hv[4] : 0;
     }
     stats.nclusters = k;
     if (st) *st = stats;

@@ -10,6 +10,7 @@
 //   tkey[T], tstart[T+1]  occupied tiles (key >> 8) and their first slot
 //   tmap[ntx*nty]  occupied-tile index of every tile of the grid (-1: empty)
 //   tslot[T][65]   first slot of the first occupied cell with local index >= l
+//   tstage[T][100]  (first slot, count) of the 10x10 cells of each tile + its 1-cell halo
 //   tq[T][65], tnb[T]  the tslot table over quarter indices; E/S/SE/SW neighbour tiles
 //   seg[C]   64 B: <= 6 slot pieces of the 3x3 stencil + the own cell range
 //   qidx[nf], qkey[Q], qstart[Q+1]  quarter cells (2x2 per eps cell; key low 2 bits =
@@ -94,14 +95,14 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb;
+        tslot, qcomp, nbr, tq, tnb, tstage;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
-                          &qcomp, &nbr, &tq, &tnb})
+                          &qcomp, &nbr, &tq, &tnb, &tstage})
             b->release();
     }
 };
@@ -115,7 +116,7 @@ struct GridParams {
 
 struct FitStats {
     int64_t n = 0, nf = 0, ncells = 0, ncore = 0, nclusters = 0, nx = 0, ny = 0, bits = 0,
-            grid_mode = 0;
+            grid_mode = 0, ntiles = 0, clique = 0;
 };
 
 // One fit.  Full fits (zone == nullptr) write cluster/flag in input order and return the

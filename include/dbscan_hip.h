@@ -93,7 +93,9 @@ void* dbscan_stream(dbscan_handle* h);
 /* Statistics of the handle's last fit:
  *   [0] n  [1] finite points in the grid  [2] occupied cells  [3] core points
  *   [4] clusters  [5] grid nx  [6] grid ny  [7] radix key bits  [8] grid mode
- *   (0 = eps grid, 1 = all pairs, 2 = no pairs)                                */
+ *   (0 = eps grid, 1 = all pairs, 2 = no pairs)  [9] occupied 8x8-cell tiles
+ *   [10] 1 if quarter cells are cliques of the predicate (tile union path)
+ * Returns the number of values written (<= max).                               */
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max);
 
 /* Per-kernel timing with HIP events on the handle's stream.  When enabled, every pipeline

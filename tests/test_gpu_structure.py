@@ -1,0 +1,116 @@
+"""GPU parity on inputs shaped to drive every branch of the tiled fit (fit.hip) -- exact vs the
+CPU grid oracle:
+  * dense clumps: tiles whose 10x10-cell stage exceeds the LDS capacity (global-memory count
+    path), quarter cells with > 32 points and > 8 cores (generic pair tests);
+  * minPoints > 12: no neighbour lists, the label pass scans the stencil itself;
+  * minPoints 1 and 2: every point core / lists of one neighbour;
+  * a grid too fine for 2^23 tiles: the cell side grows, quarter cells stop being cliques and
+    the per-point union runs;
+  * clusters laid along tile edges and corners (the tile-edge merge);
+  * a single tile (extent < 8 eps) and a one-row grid."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dbscan_amd
+
+    if dbscan_amd.load().dbscan_device_count() < 1:
+        pytest.fail("no GPU visible to libdbscan_hip.so")
+    return dbscan_amd
+
+
+@pytest.fixture(scope="module")
+def handle(dm):
+    h = dm.Handle(0)
+    yield h
+    h.close()
+
+
+def _check(dm, handle, x, y, eps, mp, modes=(0, 1)):
+    for mode in modes:
+        cl, fl, k = dm.fit_arrays(x, y, eps, mp, mode, handle=handle)
+        rc, rf, rk = O.fit_grid(x, y, eps, mp, mode)
+        assert k == rk
+        mism = np.flatnonzero((cl != rc) | (fl != rf))
+        assert mism.size == 0, f"mode {mode}: {mism.size} mismatches, first {mism[:10]}"
+
+
+def _clumps(n, seed, sigma, k=6, spread=20.0, noise=0.1):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-spread, spread, size=(k, 2))
+    m = n - int(n * noise)
+    pts = c[rng.integers(0, k, m)] + rng.normal(0, sigma, size=(m, 2))
+    pts = np.concatenate([pts, rng.uniform(-spread * 1.5, spread * 1.5, size=(n - m, 2))])
+    pts = pts[rng.permutation(n)]
+    return pts[:, 0].copy(), pts[:, 1].copy()
+
+
+@pytest.mark.parametrize("sigma", [0.05, 0.3, 1.5])
+def test_dense_clumps(dm, handle, sigma):
+    x, y = _clumps(150_000, seed=int(sigma * 100), sigma=sigma)
+    _check(dm, handle, x, y, 0.25, 10)
+    assert handle.stats()["clique"] == 1
+
+
+@pytest.mark.parametrize("mp", [13, 25, 60])
+def test_min_points_without_neighbour_lists(dm, handle, mp):
+    x, y = _clumps(120_000, seed=mp, sigma=1.0, noise=0.3)
+    _check(dm, handle, x, y, 0.3, mp)
+
+
+@pytest.mark.parametrize("mp", [1, 2, 3, 12])
+def test_small_min_points(dm, handle, mp):
+    x, y = _clumps(80_000, seed=mp, sigma=0.8, noise=0.4)
+    _check(dm, handle, x, y, 0.2, mp)
+
+
+def test_grid_too_fine_for_tiles(dm, handle):
+    """eps so small against the extent that 8x8-cell tiles would exceed 2^23: the host grows
+    the cell side and the quarter cells are no longer cliques (per-point union path)."""
+    rng = np.random.default_rng(3)
+    n = 60_000
+    x = rng.uniform(0, 1e4, n)
+    y = rng.uniform(0, 1e4, n)
+    # pairs and triples at distance < eps so that clusters exist
+    x[: n // 3] = x[n // 3: 2 * n // 3] + rng.uniform(-4e-4, 4e-4, n // 3)
+    y[: n // 3] = y[n // 3: 2 * n // 3] + rng.uniform(-4e-4, 4e-4, n // 3)
+    _check(dm, handle, x, y, 1e-3, 2, modes=(0,))
+    st = handle.stats()
+    assert st["grid_mode"] == 0 and st["clique"] == 0
+    _check(dm, handle, x, y, 1e-3, 2, modes=(1,))
+
+
+@pytest.mark.parametrize("eps", [0.5, 1.0])
+def test_clusters_on_tile_edges_and_corners(dm, handle, eps):
+    """Dense lines along multiples of 8*eps (tile edges) and blobs on tile corners."""
+    rng = np.random.default_rng(int(eps * 10))
+    parts = []
+    for k in range(-3, 4):
+        t = rng.uniform(-30 * eps, 30 * eps, 4000)
+        parts.append(np.stack([np.full_like(t, 8 * eps * k) + rng.normal(0, 0.2 * eps, t.size),
+                               t], 1))
+        parts.append(np.stack([t, np.full_like(t, 8 * eps * k) +
+                               rng.normal(0, 0.2 * eps, t.size)], 1))
+    for kx in range(-3, 4):
+        for ky in range(-3, 4):
+            parts.append(rng.normal(0, 0.6 * eps, (300, 2)) + 8 * eps * np.array([kx, ky]))
+    parts.append(rng.uniform(-32 * eps, 32 * eps, (8000, 2)))
+    pts = np.concatenate(parts)
+    pts = pts[rng.permutation(len(pts))]
+    _check(dm, handle, pts[:, 0].copy(), pts[:, 1].copy(), eps, 6)
+
+
+def test_single_tile_and_single_row(dm, handle):
+    rng = np.random.default_rng(11)
+    x = rng.normal(0, 0.5, 5000)
+    y = rng.normal(0, 0.5, 5000)
+    _check(dm, handle, x, y, 0.6, 8)  # extent ~ 6 eps: one tile
+    x = rng.uniform(0, 500, 20000)
+    y = rng.uniform(0, 0.1, 20000)
+    _check(dm, handle, x, y, 0.3, 5)  # one row of cells, many tiles along x
