@@ -141,6 +141,27 @@ __global__ __launch_bounds__(kBlock) void iota_key_kernel(int64_t n, uint32_t kv
     perm[i] = (int32_t)i;
 }
 
+// The same permutation as gather_kernel, done as scattered writes: inv[perm[p]] = p, then
+// xy[inv[i]] = (x[i], y[i]) in input order.  A random 4-B or 16-B write moves one 32-B sector;
+// a random 8-B read moves a whole 128-B line, so this moves ~4x fewer HBM bytes.
+__global__ __launch_bounds__(kBlock) void inverse_kernel(int64_t n,
+                                                         const int32_t* __restrict__ perm,
+                                                         int32_t* __restrict__ inv) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p < n) inv[perm[p]] = (int32_t)p;
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __restrict__ x,
+                                                            const double* __restrict__ y,
+                                                            int64_t n, int64_t nf,
+                                                            const int32_t* __restrict__ inv,
+                                                            double2* __restrict__ xy) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int32_t p = inv[i];
+    if (p < nf) xy[p] = make_double2(x[i], y[i]);
+}
+
 __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict__ x,
                                                         const double* __restrict__ y, int64_t nf,
                                                         const int32_t* __restrict__ perm,
@@ -1309,6 +1330,14 @@ static int count_ablate() {
     }();
     return v;
 }
+// DBSCAN_GATHER=0: sorted coordinates by random reads; 1: by random writes (default).
+static int gather_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("DBSCAN_GATHER");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
 static int count_cap() {
     static const int v = [] {
         const char* e = std::getenv("DBSCAN_COUNT_CAP");
@@ -1428,8 +1457,16 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
     if (nf > 0) {
         {
             StageTimer t(prof, s, "gather");
-            hipLaunchKernelGGL(gather_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, a.x, a.y, nf,
-                               perm, xy);
+            if (gather_mode() == 1) {
+                int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
+                hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
+                                   inv);
+                hipLaunchKernelGGL(scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y,
+                                   n, nf, inv, xy);
+            } else {
+                hipLaunchKernelGGL(gather_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, a.x, a.y,
+                                   nf, perm, xy);
+            }
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {

@@ -95,14 +95,14 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb, tstage;
+        tslot, qcomp, nbr, tq, tnb, tstage, inv;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
-                          &qcomp, &nbr, &tq, &tnb, &tstage})
+                          &qcomp, &nbr, &tq, &tnb, &tstage, &inv})
             b->release();
     }
 };
