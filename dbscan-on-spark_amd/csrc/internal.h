@@ -20,6 +20,8 @@
 //   nbr[nf][minPoints-1]  slots of each non-core's neighbours (-1 terminated), minPoints <= 12
 //   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
 //   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
+//   inv[n]   i32 sorted slot of each input index (inverse of perm)
+//   packed[n] u32 per sorted slot: (cluster << 1) | core, moved to input order through inv
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -95,14 +97,14 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb, tstage, inv;
+        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
-                          &qcomp, &nbr, &tq, &tnb, &tstage, &inv})
+                          &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed})
             b->release();
     }
 };
