@@ -7,7 +7,8 @@
 Workload (BASELINE.json configs[1]): G(n = 10^7 x N, 32 Gaussian blobs, no noise,
 seed 1), eps = 2.55 (k_bar ~ 49), minPoints = 10, LocalDBSCANNaive semantics, visit order =
 generation order (i.i.d. draws).  A step = one full local fit of the resident points (HBM in ->
-labels in HBM).  N = 1: one dbscan_fit_device per step.  N > 1: the slab-sharded node path
+labels in HBM).  N = 1: one dbscan_fit_device_async per step (the fit never synchronizes with
+the host; the K steps are enqueued back to back and the timed region ends with one sync).  N > 1: the slab-sharded node path
 (dbscan_amd/node.py): per-GPU slab fits with 2*eps halos + RCCL all-gathers of the boundary
 records + global union-find + relabel; per-GPU work is fixed (weak scaling).
 
@@ -125,8 +126,12 @@ def main():
         cl = torch.empty(n_total, dtype=torch.int32, device="cuda")
         fl = torch.empty(n_total, dtype=torch.uint8, device="cuda")
 
-        def step():
-            return D.fit_tensors(x, y, args.eps, args.min_points, 0, h, cl, fl)[2]
+        nk = torch.zeros(1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+
+        def step():  # enqueue only: no host synchronization inside a fit
+            D.fit_tensors_async(x, y, args.eps, args.min_points, 0, h, cl, fl, nk)
+            return nk
     else:
         from dbscan_amd import node
 
@@ -138,6 +143,7 @@ def main():
 
     for _ in range(args.warmup):
         k = step()
+    h.sync()
     if not args.no_profile:
         h.profile(True)
         h.profile_reset()
@@ -147,6 +153,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         k = step()
+    h.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -156,6 +163,8 @@ def main():
                          device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    if isinstance(k, torch.Tensor):
+        k = int(k.item())
     prof = h.profile_read() if not args.no_profile else {}
     h.profile(False)
     stats = h.stats()

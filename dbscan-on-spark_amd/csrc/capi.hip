@@ -160,6 +160,7 @@ struct dbscan_handle {
     dbscan::FitStats stats;
     dbscan::SlabState slab;
     dbscan::DevBuf hx, hy, hcl, hfl;  // staging for the host-array entry points
+    bool pending = false;             // an asynchronous fit whose stats are not read yet
     std::mutex mu;                    // one fit at a time per handle
 };
 
@@ -267,6 +268,51 @@ void dbscan_destroy(dbscan_handle* h) {
 
 void* dbscan_stream(dbscan_handle* h) { return h ? (void*)h->stream : nullptr; }
 
+namespace {
+// Completes an asynchronous fit on the host side: waits for the stream, reads its stats
+// (raising a device-side error such as an unsizable grid) and accumulates the stage timers.
+void settle(dbscan_handle* h) {
+    if (!h->pending) return;
+    h->pending = false;
+    h->stats = dbscan::read_fit_stats(h->stream, h->ws);
+    h->prof.flush();
+}
+}  // namespace
+
+int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                int64_t n, double eps, int32_t min_points, int32_t mode,
+                                int32_t* d_cluster, uint8_t* d_flag, int32_t* d_n_clusters) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
+        if (h->pending && h->prof.pending.size() > 4096) settle(h);  // bound the event backlog
+        h->pending = false;  // a newer fit replaces the unread stats of an older one
+        dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
+                          nullptr, nullptr};
+        dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+        if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
+        h->pending = true;
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_sync(dbscan_handle* h) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        settle(h);
+        return DBSCAN_OK;
+    });
+}
+
 int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
                           double eps, int32_t min_points, int32_t mode, int32_t* d_cluster,
                           uint8_t* d_flag, int32_t* n_clusters_out) {
@@ -276,6 +322,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
         check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
@@ -295,6 +342,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
         check_fit_args(n, eps, mode, x, y, cluster_out, flag_out);
         if (n == 0) {
             if (n_clusters_out) *n_clusters_out = 0;
@@ -340,6 +388,7 @@ int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
         check_fit_args(n, eps, DBSCAN_MODE_NAIVE, d_x, d_y, d_core, d_root);
         if (n > 0 && !d_zone) throw dbscan::ArgError{"NULL zone pointer"};
         dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
@@ -359,6 +408,7 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
         if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
             throw dbscan::ArgError{"bad mode"};
         if (h->slab.n > 0 && (!d_zone || !d_gid || !d_gs_of_root || !d_label_of_root ||
@@ -373,6 +423,7 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
 
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {
     if (!h || !out) return DBSCAN_EARG;
+    if (h->pending && dbscan_sync(h) != DBSCAN_OK) return DBSCAN_EHIP;
     const int64_t v[11] = {h->stats.n,     h->stats.nf,        h->stats.ncells,
                            h->stats.ncore, h->stats.nclusters, h->stats.nx,
                            h->stats.ny,    h->stats.bits,      h->stats.grid_mode,

@@ -109,10 +109,12 @@ __device__ __forceinline__ void for_candidates(const Seg& s, F f) {
 
 __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ x,
                                                      const double* __restrict__ y, int64_t n,
-                                                     GridParams g, uint32_t* __restrict__ key,
+                                                     const GridParams* __restrict__ gp,
+                                                     uint32_t* __restrict__ key,
                                                      int32_t* __restrict__ perm) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
+    const GridParams g = *gp;
     const double a = x[i], b = y[i];
     uint32_t k = kSentinelKey;
     if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
@@ -154,13 +156,14 @@ __global__ __launch_bounds__(kBlock) void inverse_kernel(int64_t n,
 
 __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __restrict__ x,
                                                             const double* __restrict__ y,
-                                                            int64_t n, int64_t nf,
+                                                            int64_t n,
+                                                            const int32_t* __restrict__ nf_p,
                                                             const int32_t* __restrict__ inv,
                                                             double2* __restrict__ xy) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const int32_t p = inv[i];
-    if (p < nf) xy[p] = make_double2(x[i], y[i]);
+    if (p < *nf_p) xy[p] = make_double2(x[i], y[i]);
 }
 
 // Occupied tiles, eps cells and quarter cells in one pass over the sorted keys (they are
@@ -184,9 +187,11 @@ __device__ __forceinline__ Heads heads_at(const uint32_t* __restrict__ key, int6
 }
 
 __global__ __launch_bounds__(kBlock) void heads_reduce_kernel(const uint32_t* __restrict__ key,
-                                                              int64_t nf, int nb,
+                                                              const int32_t* __restrict__ nf_p,
+                                                              int nb,
                                                               int32_t* __restrict__ partial) {
     __shared__ int wsum[3][kBlock / 64];
+    const int64_t nf = *nf_p;
     const int64_t base = (int64_t)blockIdx.x * kHeadTile;
     int c = 0, q = 0, t = 0;
     for (int r = 0; r < kHeadTile / kBlock; ++r) {
@@ -218,11 +223,13 @@ __global__ __launch_bounds__(kBlock) void heads_reduce_kernel(const uint32_t* __
 // offs: the exclusive scans of the three rows of partial counts.  qidx == nullptr: no quarter
 // tables (quarter cells are not cliques of the predicate).
 __global__ __launch_bounds__(kBlock) void heads_down_kernel(
-    const uint32_t* __restrict__ key, int64_t nf, int nb, const int32_t* __restrict__ offs,
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ nf_p, int nb,
+    const int32_t* __restrict__ offs,
     int32_t* __restrict__ cell, uint32_t* __restrict__ ckey, int32_t* __restrict__ cstart,
     int32_t* __restrict__ qidx, uint32_t* __restrict__ qkey, int32_t* __restrict__ qstart,
     uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart) {
     __shared__ int wcnt[2][3][kBlock / 64];
+    const int64_t nf = *nf_p;
     const int64_t base = (int64_t)blockIdx.x * kHeadTile;
     const int w = threadIdx.x >> 6, lane = __lane_id();
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -284,8 +291,9 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
 __global__ __launch_bounds__(kBlock) void tmap_kernel(const uint32_t* __restrict__ tkey,
                                                       const int32_t* __restrict__ ntiles_p,
                                                       int32_t* __restrict__ tmap) {
-    const int t = blockIdx.x * kBlock + threadIdx.x;
-    if (t < *ntiles_p) tmap[tkey[t]] = t;
+    const int ntiles = *ntiles_p;
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < ntiles; t += gridDim.x * kBlock)
+        tmap[tkey[t]] = t;
 }
 
 // tslot[t][l] = first slot of the first occupied cell of tile t with local index >= l
@@ -297,38 +305,42 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
     const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ cell,
     const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
     const int32_t* __restrict__ ncells_p, const int32_t* __restrict__ qidx,
-    const int32_t* __restrict__ tmap, GridParams g, int32_t* __restrict__ tslot,
+    const int32_t* __restrict__ tmap, const GridParams* __restrict__ gp,
+    int32_t* __restrict__ tslot,
     int32_t* __restrict__ tq, int4* __restrict__ tnb) {
     // one wave per tile, one lane per local cell
-    const int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (t >= *ntiles_p) return;  // wave-uniform; no block barriers below
-    const uint32_t tk = tkey[t];
-    const int ts0 = tstart[t], end = tstart[t + 1];
-    const int c0 = cell[ts0];
-    const int c = c0 + lane;
-    const bool mine = c < *ncells_p && (ckey[c] >> 6) == tk;
-    uint64_t occ = mine ? 1ull << (ckey[c] & 63u) : 0ull;  // occupied local cells
+    const int ntiles = *ntiles_p;
+    for (int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < ntiles;
+         t += gridDim.x * (kBlock / 64)) {  // wave-uniform; no block barriers below
+        const uint32_t tk = tkey[t];
+        const int ts0 = tstart[t], end = tstart[t + 1];
+        const int c0 = cell[ts0];
+        const int c = c0 + lane;
+        const bool mine = c < *ncells_p && (ckey[c] >> 6) == tk;
+        uint64_t occ = mine ? 1ull << (ckey[c] & 63u) : 0ull;  // occupied local cells
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) occ |= __shfl_xor(occ, o, 64);
-    const uint64_t rest = occ >> lane;
-    int st = end;
-    if (rest) {
-        const int nl = lane + __builtin_ctzll(rest);  // first occupied local >= lane
-        const int rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
-        st = cstart[c0 + rank];
-    }
-    int32_t* ts = tslot + (int64_t)t * kTslot;
-    ts[lane] = st;
-    if (lane == 0) ts[64] = end;
-    if (qidx) {
-        int32_t* tqq = tq + (int64_t)t * kTslot;
-        tqq[lane] = st < end ? qidx[st] : qidx[end - 1] + 1;
-        if (lane == 0) {
-            tqq[64] = qidx[end - 1] + 1;
-            const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
-            tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
-                               tile_occ(tmap, g, tx + 1, ty + 1), tile_occ(tmap, g, tx - 1, ty + 1));
+        for (int o = 1; o < 64; o <<= 1) occ |= __shfl_xor(occ, o, 64);
+        const uint64_t rest = occ >> lane;
+        int st = end;
+        if (rest) {
+            const int nl = lane + __builtin_ctzll(rest);  // first occupied local >= lane
+            const int rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
+            st = cstart[c0 + rank];
+        }
+        int32_t* ts = tslot + (int64_t)t * kTslot;
+        ts[lane] = st;
+        if (lane == 0) ts[64] = end;
+        if (qidx) {
+            int32_t* tqq = tq + (int64_t)t * kTslot;
+            tqq[lane] = st < end ? qidx[st] : qidx[end - 1] + 1;
+            if (lane == 0) {
+                tqq[64] = qidx[end - 1] + 1;
+                const GridParams g = *gp;
+                const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
+                tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
+                                   tile_occ(tmap, g, tx + 1, ty + 1), tile_occ(tmap, g, tx - 1, ty + 1));
+            }
         }
     }
 }
@@ -340,9 +352,11 @@ __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict
                                                       const int32_t* __restrict__ ncells_p,
                                                       const int32_t* __restrict__ tmap,
                                                       const int32_t* __restrict__ tslot,
-                                                      GridParams g, Seg* __restrict__ seg) {
+                                                      const GridParams* __restrict__ gp,
+                                                      Seg* __restrict__ seg) {
     const int c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= *ncells_p) return;
+    const GridParams g = *gp;
     uint32_t cx, cy;
     cell_xy(ckey[c], g.ntx, cx, cy);
     const uint32_t lox = cx > 0 ? cx - 1 : cx, hix = cx + 1 < g.nx ? cx + 1 : cx;
@@ -403,23 +417,27 @@ __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restri
                                                         const int32_t* __restrict__ ntiles_p,
                                                         const int32_t* __restrict__ tmap,
                                                         const int32_t* __restrict__ tslot,
-                                                        GridParams g, int2* __restrict__ tstage) {
-    const int t = blockIdx.x * 2 + (threadIdx.x >> 7);
+                                                        const GridParams* __restrict__ gp,
+                                                        int2* __restrict__ tstage) {
     const int k = threadIdx.x & 127;
-    if (t >= *ntiles_p || k >= 100) return;
-    const uint32_t tk = tkey[t];
-    const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
-    const int ey = k / 10 - 1, ex = k % 10 - 1;
-    const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
-    const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
-    const int occ = tile_occ(tmap, g, tx, ty);
-    int b = 0, cnt = 0;
-    if (occ >= 0) {
-        const int l = (ey & 7) * 8 + (ex & 7);
-        b = tslot[(int64_t)occ * kTslot + l];
-        cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
+    if (k >= 100) return;
+    const GridParams g = *gp;
+    const int ntiles = *ntiles_p;
+    for (int t = blockIdx.x * 2 + (threadIdx.x >> 7); t < ntiles; t += gridDim.x * 2) {
+        const uint32_t tk = tkey[t];
+        const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
+        const int ey = k / 10 - 1, ex = k % 10 - 1;
+        const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
+        const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
+        const int occ = tile_occ(tmap, g, tx, ty);
+        int b = 0, cnt = 0;
+        if (occ >= 0) {
+            const int l = (ey & 7) * 8 + (ex & 7);
+            b = tslot[(int64_t)occ * kTslot + l];
+            cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
+        }
+        tstage[(int64_t)t * 100 + k] = make_int2(b, cnt);
     }
-    tstage[(int64_t)t * 100 + k] = make_int2(b, cnt);
 }
 
 struct StageMeta {  // one tile's staging table, held in registers (lanes < 100; lane 0: range)
@@ -722,7 +740,8 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
 
 // Slots outside the grid (non-finite coordinates, or every slot when eps*eps is NaN): no
 // neighbours, not even themselves.
-__global__ __launch_bounds__(kBlock) void count_rest_kernel(int64_t nf, int64_t n,
+__global__ __launch_bounds__(kBlock) void count_rest_kernel(const int32_t* __restrict__ nf_p,
+                                                            int64_t n,
                                                             int32_t min_points,
                                                             const int32_t* __restrict__ perm,
                                                             const uint8_t* __restrict__ zone,
@@ -730,13 +749,13 @@ __global__ __launch_bounds__(kBlock) void count_rest_kernel(int64_t nf, int64_t 
                                                             int32_t* __restrict__ parent,
                                                             int32_t* __restrict__ block_cores) {
     __shared__ int wcores[kBlock / 64];
-    const int64_t p = nf + (int64_t)blockIdx.x * kBlock + threadIdx.x;
     int mine = 0;
-    if (p < n) {
+    for (int64_t p = *nf_p + (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n;
+         p += (int64_t)gridDim.x * kBlock) {
         const bool is_core = min_points <= 0 && !(zone && zone[perm[p]] == 2);
         parent[p] = (int32_t)p;
         core[p] = is_core ? 1 : 0;
-        mine = is_core ? 1 : 0;
+        mine += is_core ? 1 : 0;
     }
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
     if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
@@ -820,13 +839,16 @@ __device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra
 // Each core-core edge once: from the endpoint with the larger slot.
 __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict__ xy,
                                                        const int32_t* __restrict__ cell,
-                                                       const Seg* __restrict__ seg, int64_t nf,
+                                                       const Seg* __restrict__ seg,
+                                                       const int32_t* __restrict__ nf_p,
+                                                       const GridParams* __restrict__ gp,
                                                        double eps2,
                                                        const int32_t* __restrict__ perm,
                                                        const uint8_t* __restrict__ core,
                                                        int32_t* __restrict__ parent) {
+    if (gp->clique) return;  // quarter-cell unions instead
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= nf || !core[p]) return;
+    if (p >= *nf_p || !core[p]) return;
     const double2 me = xy[p];
     const Seg s = load_seg(seg, cell[p]);
     int rp = uf_find(parent, (int)p);
@@ -850,11 +872,14 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void quarter_init_kernel(
     const int32_t* __restrict__ qstart, const uint32_t* __restrict__ qkey,
-    const int32_t* __restrict__ nq_p, GridParams g, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ nq_p, const GridParams* __restrict__ gp,
+    const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, int4* __restrict__ qinfo, int4* __restrict__ qg,
     int32_t* __restrict__ parent) {
+    if (!gp->clique) return;
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
+    const GridParams g = *gp;
     const int b = qstart[q], e = qstart[q + 1];
     int rep = -1, best = 0x7FFFFFFF;
     uint32_t mask = 0;  // cores among the first 32 slots (quarters rarely hold more)
@@ -983,7 +1008,8 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
     const int32_t* __restrict__ ntiles_p, const int4* __restrict__ qinfo,
     const int4* __restrict__ qg, double eps2, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    int32_t* __restrict__ qcomp) {
+    int32_t* __restrict__ qcomp, const GridParams* __restrict__ gp) {
+    if (!gp->clique) return;
     __shared__ int lp[kMaxTileQ];
     __shared__ int4 lqi[kMaxTileQ];
     __shared__ int qmap[kMaxTileQ];  // 16x16 local quarter grid -> local quarter index
@@ -1063,7 +1089,9 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
     const int32_t* __restrict__ tq, const int4* __restrict__ tnb,
     const int4* __restrict__ qinfo, const int4* __restrict__ qg,
     const int32_t* __restrict__ qcomp, double eps2, const int32_t* __restrict__ perm,
-    const uint8_t* __restrict__ core, int32_t* __restrict__ parent) {
+    const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    const GridParams* __restrict__ gp) {
+    if (!gp->clique) return;
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
     __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
     __shared__ int ncomp[kBlock / 64][kEdgeNodes];
@@ -1159,7 +1187,9 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
 // final_kernel is core -> rep -> root.
 __global__ __launch_bounds__(kBlock) void quarter_root_kernel(const int4* __restrict__ qinfo,
                                                               const int32_t* __restrict__ nq_p,
+                                                              const GridParams* __restrict__ gp,
                                                               int32_t* __restrict__ parent) {
+    if (!gp->clique) return;
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
     const int rep = qinfo[q].z;
@@ -1198,14 +1228,15 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
 template <bool SLAB>
 __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, const int32_t* __restrict__ nbr, int nbr_k, int64_t nf,
-    int64_t n, double eps2, int32_t mode, const int32_t* __restrict__ perm,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nbr, int nbr_k,
+    const int32_t* __restrict__ nf_p, int64_t n, double eps2, int32_t mode, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
     const int32_t* __restrict__ rank, const uint8_t* __restrict__ zone,
     const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
     const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
+    const int64_t nf = *nf_p;
     uint32_t v = 0;  // Noise
     if (core[p]) {
         const uint32_t cl = SLAB ? (uint32_t)label_of_root[lab[p]] : (uint32_t)rank[lab[p]] + 1u;
@@ -1283,32 +1314,24 @@ __global__ __launch_bounds__(kBlock) void slab_roots_kernel(int64_t n,
     root_out[i] = c ? lab[p] : -1;
 }
 
-inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
-
-}  // namespace
-
-// ---------------------------------------------------------------------------------------
-// Host orchestration
-// ---------------------------------------------------------------------------------------
-
-// Grid sizing on the host (see DESIGN.md "grid soundness"): cell side >= R*(1+2^-16) with
+// Grid sizing (see DESIGN.md "grid soundness"), on the device so a fit needs no host sync: cell side >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500) bounds |x'-x| for every pair the fp64 predicate accepts;
 // at most 2^23 tiles of 8x8 cells (u32 keys = tile*256 + cell*4 + quadrant, below the
 // sentinel), growing the side (never shrinking it) when the extent would need more.  Quarter
 // cells are cliques only while the side was not grown: clique = side <= |eps|*(1+2^-14).
-static bool make_grid(const double bb[5], double eps, GridParams* g) {
+__device__ bool make_grid(const double* bb, double eps, GridParams* g) {
     const double xmin = bb[0], xmax = bb[1], ymin = bb[2], ymax = bb[3];
-    double R = std::fabs(eps) * (1.0 + 0x1p-40);
+    double R = fabs(eps) * (1.0 + 0x1p-40);
     if (R < 0x1p-500) R = 0x1p-500;
     double hx = R * (1.0 + 0x1p-16), hy = hx;
     const double limit = 8388608.0;  // 2^23 tiles
     auto cells = [](double vmax, double vmin, double h) {
         const double t = (vmax * 0.5 - vmin * 0.5) * (2.0 / h);
-        return std::floor(t) + 1.0;  // may be +inf for absurd extents
+        return floor(t) + 1.0;  // may be +inf for absurd extents
     };
     for (int it = 0; it < 4096; ++it) {
         const double cx = cells(xmax, xmin, hx), cy = cells(ymax, ymin, hy);
-        const double tx = std::ceil(cx / 8.0), ty = std::ceil(cy / 8.0);
+        const double tx = ceil(cx / 8.0), ty = ceil(cy / 8.0);
         if (tx <= limit && ty <= limit && tx * ty <= limit) {
             g->invx = 2.0 / hx;
             g->invy = 2.0 / hy;
@@ -1318,7 +1341,7 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
             g->ny = (uint32_t)cy;
             g->ntx = (uint32_t)tx;
             g->nty = (uint32_t)ty;
-            const double cl = std::fabs(eps) * (1.0 + 0x1p-14);
+            const double cl = fabs(eps) * (1.0 + 0x1p-14);
             g->clique = (hx <= cl && hy <= cl) ? 1 : 0;
             return true;
         }
@@ -1326,6 +1349,58 @@ static bool make_grid(const double bb[5], double eps, GridParams* g) {
     }
     return false;
 }
+
+// One thread: the grid from the bbox of the finite points (bb = xmin, xmax, ymin, ymax, count),
+// the finite count nf, the radix key width and a sizing error flag.  No finite point: nf = 0
+// and a 1x1 dummy grid (every slot is outside the grid).
+__global__ void grid_kernel(const double* __restrict__ bb, double eps, GridParams* __restrict__ gp,
+                            int32_t* __restrict__ st) {
+    GridParams g{0, 0, 1, 1, 1, 1, 1, 1, 0};
+    const int nf = (int)bb[4];
+    int bits = 0;
+    if (nf > 0) {
+        if (!make_grid(bb, eps, &g)) {
+            st[kStError] = 1;
+            g = GridParams{0, 0, 1, 1, 1, 1, 1, 1, 0};
+        }
+        const uint64_t nkeys = 256ull * g.ntx * g.nty;  // valid keys < nkeys <= 2^31
+        bits = 1;
+        while (bits < 32 && (1ull << bits) <= nkeys) ++bits;  // keys < 2^bits - 1 (sentinel)
+    }
+    *gp = g;
+    st[kStNf] = nf;
+    st[kStBits] = bits;
+}
+
+// All-pairs (eps*eps = +inf: one cell holding every point) and no-pairs (eps*eps NaN) fits.
+__global__ void grid_fixed_kernel(int32_t nf, GridParams* __restrict__ gp,
+                                  int32_t* __restrict__ st) {
+    *gp = GridParams{0, 0, 1, 1, 1, 1, 1, 1, 0};
+    st[kStNf] = nf;
+    st[kStBits] = 0;
+}
+
+// tmap = -1 over the whole tile grid (ntx * nty is only known on the device).
+__global__ __launch_bounds__(kBlock) void tmap_clear_kernel(const GridParams* __restrict__ gp,
+                                                            int32_t* __restrict__ tmap) {
+    const int64_t nt = (int64_t)gp->ntx * gp->nty;
+    for (int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x; u < nt;
+         u += (int64_t)gridDim.x * kBlock)
+        tmap[u] = -1;
+}
+
+// The cluster count of a fit into caller memory (asynchronous API).
+__global__ void nclusters_kernel(const int32_t* __restrict__ st, int32_t* __restrict__ out) {
+    *out = st[kStClusters];
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------------------
 
 // LDS staging capacity of the count pass (points of a tile + halo).  DBSCAN_COUNT_CAP
 // (3072/2048/1024) overrides it for measurements; results are identical for every choice
@@ -1348,182 +1423,154 @@ static int count_cap() {
     return v;
 }
 
-int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
-                SlabState* slab) {
+// Enqueues one whole fit on stream s and never waits on the device: the grid, the finite count
+// nf and every table size live in device memory (ws.misc), so launch sizes derive from n alone
+// and kernels bound themselves by the device-side counts.  The grid is sized by grid_kernel
+// from the device bbox (no host readback), the radix sort skips the key digits the grid does
+// not use, and the clique (quarter-cell) and per-point union paths are both enqueued, each
+// exiting at once when the grid selects the other.
+void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
+                 SlabState* slab) {
     if (slab) slab->valid = false;
     const int64_t n = a.n;
-    FitStats stats;
-    stats.n = n;
+    const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
+    const int mode =
+        std::isnan(eps2) ? kGridNoPairs : (std::isinf(eps2) ? kGridAllPairs : kGridEps);
+    ws.fit_n = n;
+    ws.fit_mode = mode;
+    double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
+    GridParams* gp = reinterpret_cast<GridParams*>(misc + 8);
+    int32_t* st = reinterpret_cast<int32_t*>(misc + 16);
+    DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
     if (n == 0) {
-        if (st) *st = stats;
         if (slab) {
             slab->valid = a.zone != nullptr;
             slab->n = 0;
-            slab->nf = 0;
         }
-        return 0;
+        return;
     }
-    const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
-    int mode = std::isnan(eps2) ? kGridNoPairs : (std::isinf(eps2) ? kGridAllPairs : kGridEps);
+    const int32_t* nf_p = &st[kStNf];
 
     uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
     uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
     int32_t* perm = static_cast<int32_t*>(ws.perm.ensure(n * sizeof(int32_t)));
     int32_t* perm2 = static_cast<int32_t*>(ws.perm2.ensure(n * sizeof(int32_t)));
-    double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
-    // misc_i: [0] ncells [1] nclusters [2] ncore [3] nquarters [4] ntiles
-    int32_t* misc_i = reinterpret_cast<int32_t*>(misc + 16);
-
-    DBSCAN_HIP_CHECK(hipMemsetAsync(misc_i, 0, 8 * sizeof(int32_t), s));
-    GridParams g{0, 0, 0, 0, 1, 1, 1, 1, 0};
-    int64_t nf = 0;
-    int bits = 0;
     if (mode == kGridEps) {
-        double bb[5];
         {
             StageTimer t(prof, s, "bbox");
             bbox_finite(s, a.x, a.y, n, misc, ws.scan_tmp);
+            hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
+            DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(bb, misc, sizeof(bb), hipMemcpyDeviceToHost, s));
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-        nf = (int64_t)bb[4];
-        if (nf > 0 && !make_grid(bb, a.eps, &g)) throw ArgError{"cannot size the eps grid"};
-        if (nf == 0) mode = kGridNoPairs;
-    } else if (mode == kGridAllPairs) {
-        nf = n;  // one cell holding every point; the predicate decides (incl. non-finite)
-    }
-    stats.grid_mode = mode;
-    stats.nf = nf;
-    stats.nx = g.nx;
-    stats.ny = g.ny;
-
-    if (mode == kGridEps) {
         {
             StageTimer t(prof, s, "bin");
-            hipLaunchKernelGGL(bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, g, key,
+            hipLaunchKernelGGL(bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key,
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        const uint64_t nkeys = 256ull * g.ntx * g.nty;  // valid keys < nkeys <= 2^31
-        bits = 1;
-        while (bits < 32 && (1ull << bits) <= nkeys) ++bits;  // keys < 2^bits - 1 (sentinel)
-        radix_sort_pairs(s, key, perm, key2, perm2, n, bits, ws.hist, ws.scan_tmp, prof);
+        radix_sort_pairs(s, key, perm, key2, perm2, n, 32, &st[kStBits], ws.hist, ws.scan_tmp,
+                         prof);
     } else {
         StageTimer t(prof, s, "bin");
+        // all pairs: one cell holding every point, the predicate decides (incl. non-finite)
+        hipLaunchKernelGGL(grid_fixed_kernel, dim3(1), dim3(1), 0, s,
+                           mode == kGridAllPairs ? (int32_t)n : 0, gp, st);
         hipLaunchKernelGGL(iota_key_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
                            mode == kGridAllPairs ? 0u : kSentinelKey, key, perm);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
-    stats.bits = bits;
     ws.perm_sorted = perm;
     ws.key_sorted = key;
 
-    bool have_inv = false;  // inverse permutation (input index -> sorted slot)
-    auto ensure_inv = [&]() -> const int32_t* {
-        int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
-        if (!have_inv) {
-            hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, inv);
-            have_inv = true;
-        }
-        return inv;
-    };
-    const int64_t nfa = nf > 0 ? nf : 1;
-    const int64_t ntile_bound = std::min<int64_t>(nfa, (int64_t)g.ntx * g.nty);
-    double2* xy = static_cast<double2*>(ws.xy.ensure(nfa * sizeof(double2)));
-    int32_t* cell = static_cast<int32_t*>(ws.cell.ensure(nfa * sizeof(int32_t)));
-    uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(nfa * sizeof(uint32_t)));
-    int32_t* cstart = static_cast<int32_t*>(ws.cstart.ensure((nfa + 1) * sizeof(int32_t)));
-    Seg* seg = static_cast<Seg*>(ws.seg.ensure(nfa * sizeof(Seg)));
-    uint32_t* tkey = static_cast<uint32_t*>(ws.tkey.ensure(nfa * sizeof(uint32_t)));
-    int32_t* tstart = static_cast<int32_t*>(ws.tstart.ensure((nfa + 1) * sizeof(int32_t)));
-    int32_t* tmap =
-        static_cast<int32_t*>(ws.tmap.ensure((size_t)g.ntx * g.nty * sizeof(int32_t)));
+    // Sizes: every nf-sized table is allocated for n; the tile grid holds <= 2^23 tiles.
+    const int64_t ntile_bound = std::min<int64_t>(n, kMaxGridTiles);
+    int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
+    double2* xy = static_cast<double2*>(ws.xy.ensure(n * sizeof(double2)));
+    int32_t* cell = static_cast<int32_t*>(ws.cell.ensure(n * sizeof(int32_t)));
+    uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(n * sizeof(uint32_t)));
+    int32_t* cstart = static_cast<int32_t*>(ws.cstart.ensure((n + 1) * sizeof(int32_t)));
+    Seg* seg = static_cast<Seg*>(ws.seg.ensure(n * sizeof(Seg)));
+    uint32_t* tkey = static_cast<uint32_t*>(ws.tkey.ensure(n * sizeof(uint32_t)));
+    int32_t* tstart = static_cast<int32_t*>(ws.tstart.ensure((n + 1) * sizeof(int32_t)));
+    int32_t* tmap = static_cast<int32_t*>(ws.tmap.ensure(kMaxGridTiles * sizeof(int32_t)));
     int32_t* tslot =
         static_cast<int32_t*>(ws.tslot.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
     int2* tstage = static_cast<int2*>(ws.tstage.ensure((size_t)ntile_bound * 100 * sizeof(int2)));
     uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
     int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
     int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
-    const bool clique = mode == kGridEps && g.clique;
-    stats.clique = clique ? 1 : 0;
-    int32_t* qidx = nullptr;
-    uint32_t* qkey = nullptr;
-    int32_t* qstart = nullptr;
-    int4* qinfo = nullptr;
-    int4* qg = nullptr;
-    int32_t* qcomp = nullptr;
-    int32_t* tq = nullptr;
-    int4* tnb = nullptr;
-    if (clique) {
-        tq = static_cast<int32_t*>(ws.tq.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
-        tnb = static_cast<int4*>(ws.tnb.ensure((size_t)ntile_bound * sizeof(int4)));
-        qcomp = static_cast<int32_t*>(ws.qcomp.ensure(nfa * sizeof(int32_t)));
-        qidx = static_cast<int32_t*>(ws.qidx.ensure(nfa * sizeof(int32_t)));
-        qkey = static_cast<uint32_t*>(ws.qkey.ensure(nfa * sizeof(uint32_t)));
-        qstart = static_cast<int32_t*>(ws.qstart.ensure((nfa + 1) * sizeof(int32_t)));
-        qinfo = static_cast<int4*>(ws.qrep.ensure(nfa * sizeof(int4)));
-        qg = static_cast<int4*>(ws.qmask.ensure(nfa * sizeof(int4)));
-    }
+    int32_t* tq = static_cast<int32_t*>(ws.tq.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
+    int4* tnb = static_cast<int4*>(ws.tnb.ensure((size_t)ntile_bound * sizeof(int4)));
+    int32_t* qcomp = static_cast<int32_t*>(ws.qcomp.ensure(n * sizeof(int32_t)));
+    int32_t* qidx = static_cast<int32_t*>(ws.qidx.ensure(n * sizeof(int32_t)));
+    uint32_t* qkey = static_cast<uint32_t*>(ws.qkey.ensure(n * sizeof(uint32_t)));
+    int32_t* qstart = static_cast<int32_t*>(ws.qstart.ensure((n + 1) * sizeof(int32_t)));
+    int4* qinfo = static_cast<int4*>(ws.qrep.ensure(n * sizeof(int4)));
+    int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
 
-    if (nf > 0) {
-        {
-            StageTimer t(prof, s, "gather");
-            const int32_t* inv = ensure_inv();
+    {
+        StageTimer t(prof, s, "gather");
+        hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, inv);
+        if (mode != kGridNoPairs)
             hipLaunchKernelGGL(scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
-                               nf, inv, xy);
-            DBSCAN_HIP_CHECK(hipGetLastError());
-        }
+                               nf_p, inv, xy);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+    if (mode != kGridNoPairs) {
         {
             StageTimer t(prof, s, "cells");
-            const int nb = (int)((nf + kHeadTile - 1) / kHeadTile);
+            const int nb = (int)((n + kHeadTile - 1) / kHeadTile);
             int32_t* part =
                 static_cast<int32_t*>(ws.heads.ensure(6 * (size_t)nb * sizeof(int32_t)));
             int32_t* offs = part + 3 * nb;
-            hipLaunchKernelGGL(heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf, nb,
+            hipLaunchKernelGGL(heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                part);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            exclusive_scan(s, 0, part, offs, nb, &misc_i[0], ws.scan_tmp);
-            if (clique) exclusive_scan(s, 0, part + nb, offs + nb, nb, &misc_i[3], ws.scan_tmp);
-            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &misc_i[4], ws.scan_tmp);
-            hipLaunchKernelGGL(heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf, nb, offs,
-                               cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
+            exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan_tmp);
+            exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan_tmp);
+            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan_tmp);
+            hipLaunchKernelGGL(heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
+                               offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "tables");
-            DBSCAN_HIP_CHECK(
-                hipMemsetAsync(tmap, 0xFF, (size_t)g.ntx * g.nty * sizeof(int32_t), s));
-            hipLaunchKernelGGL(tmap_kernel, dim3(nblk(ntile_bound)), dim3(kBlock), 0, s, tkey,
-                               &misc_i[4], tmap);
+            hipLaunchKernelGGL(tmap_clear_kernel, dim3(1024), dim3(kBlock), 0, s, gp, tmap);
+            const unsigned tgrid = (unsigned)std::min<int64_t>(nblk(ntile_bound), 1024);
+            hipLaunchKernelGGL(tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
+                               &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(tslot_kernel, dim3((unsigned)((ntile_bound + 3) / 4)), dim3(kBlock),
-                               0, s, tstart,
-                               tkey, &misc_i[4], cell, ckey, cstart, &misc_i[0], qidx, tmap, g,
-                               tslot, tq, tnb);
+            hipLaunchKernelGGL(tslot_kernel,
+                               dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
+                               dim3(kBlock),
+                               0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
+                               &st[kStCells], qidx, tmap, gp, tslot, tq, tnb);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(tstage_kernel, dim3((unsigned)((ntile_bound + 1) / 2)), dim3(kBlock),
-                               0, s, tkey, &misc_i[4], tmap, tslot, g, tstage);
+            hipLaunchKernelGGL(tstage_kernel,
+                               dim3((unsigned)std::min<int64_t>((ntile_bound + 1) / 2, kTileGrid)),
+                               dim3(kBlock),
+                               0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "segs");
-            hipLaunchKernelGGL(segs_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, ckey, cstart,
-                               &misc_i[0], tmap, tslot, g, seg);
+            hipLaunchKernelGGL(segs_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, ckey, cstart,
+                               &st[kStCells], tmap, tslot, gp, seg);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     }
     // per-tile kernels: grid stride over occupied tiles (their count stays on the device)
-    const unsigned tile_grid = nf > 0 ? (unsigned)std::min<int64_t>(ntile_bound, kTileGrid) : 0u;
-    const unsigned rest_grid = nblk(n - nf);
+    const unsigned tile_grid = (unsigned)std::min<int64_t>(ntile_bound, kTileGrid);
+    const unsigned rest_grid = std::min(nblk(n), 1024u);  // slots [nf, n): outside the grid
     int32_t* block_cores = static_cast<int32_t*>(
         ws.blockcnt.ensure(2 * ((size_t)tile_grid + rest_grid + 1) * sizeof(int32_t)));
     const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
-    int32_t* nbr = (nf > 0 && nbr_k > 0)
-                       ? static_cast<int32_t*>(ws.nbr.ensure((size_t)nf * nbr_k * sizeof(int32_t)))
+    int32_t* nbr = nbr_k > 0
+                       ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
     {
         StageTimer t(prof, s, "count");
-        if (tile_grid) {
+        if (mode != kGridNoPairs) {
             auto kern = count_tile_kernel<2048>;
             switch (count_cap()) {
                 case 3072: kern = count_tile_kernel<3072>; break;
@@ -1531,47 +1578,48 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
                 default: break;
             }
             hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
-                               tstage, &misc_i[4], eps2, a.min_points, perm, a.zone,
-                               core, parent, block_cores, nbr, nbr_k, count_ablate());
+                               tstage, &st[kStTiles], eps2, a.min_points, perm, a.zone, core,
+                               parent, block_cores, nbr, nbr_k, count_ablate());
+        } else {
+            DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
-        if (rest_grid)
-            hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf, n,
-                               a.min_points, perm, a.zone, core, parent,
-                               block_cores + tile_grid);
+        hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
+                           a.min_points, perm, a.zone, core, parent, block_cores + tile_grid);
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = (int64_t)tile_grid + rest_grid;
-        exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &misc_i[2], ws.scan_tmp);
+        exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan_tmp);
     }
-    if (clique) {
+    if (mode == kGridEps) {  // quarter-cell unions (no-ops unless the grid made them cliques)
         {
             StageTimer t(prof, s, "quarter_init");
-            hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qstart,
-                               qkey, &misc_i[3], g, perm, core, qinfo, qg, parent);
+            hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
+                               qkey, &st[kStQuarters], gp, perm, core, qinfo, qg, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_tile");
             hipLaunchKernelGGL(tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
-                               &misc_i[4], qinfo, qg, eps2, perm, core, parent, qcomp);
+                               &st[kStTiles], qinfo, qg, eps2, perm, core, parent, qcomp, gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_edge");
             hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
-                               &misc_i[4], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent);
+                               &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent,
+                               gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
-        hipLaunchKernelGGL(quarter_root_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, qinfo,
-                           &misc_i[3], parent);
+        hipLaunchKernelGGL(quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
+                           &st[kStQuarters], gp, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
-    } else if (nf > 0) {
+    }
+    if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
         StageTimer t(prof, s, "union");
-        hipLaunchKernelGGL(union_kernel, dim3(nblk(nf)), dim3(kBlock), 0, s, xy, cell, seg, nf,
+        hipLaunchKernelGGL(union_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
                            eps2, perm, core, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
-    int64_t k = 0;
     if (!a.zone) {
         uint8_t* is_root = static_cast<uint8_t*>(ws.is_root.ensure(n));
         int32_t* rank = static_cast<int32_t*>(ws.rank.ensure(n * sizeof(int32_t)));
@@ -1584,26 +1632,19 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "rank");
-            exclusive_scan(s, 1, is_root, rank, n, &misc_i[1], ws.scan_tmp);
+            exclusive_scan(s, 1, is_root, rank, n, &st[kStClusters], ws.scan_tmp);
         }
         {
             StageTimer t(prof, s, "output");
             uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
             hipLaunchKernelGGL(label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
-                               cell, seg, nbr, nbr_k, nf, n, eps2, a.mode, perm, core, lab, rank,
-                               (const uint8_t*)nullptr, (const int64_t*)nullptr,
+                               cell, seg, nbr, nbr_k, nf_p, n, eps2, a.mode, perm, core, lab,
+                               rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
                                (const int64_t*)nullptr, (const int32_t*)nullptr, packed);
-            hipLaunchKernelGGL(permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n,
-                               ensure_inv(), packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+            hipLaunchKernelGGL(permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
+                               packed, (const uint8_t*)nullptr, a.cluster, a.flag);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        int32_t hv[5];
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-        k = hv[1];
-        stats.ncells = nf > 0 ? hv[0] : 0;
-        stats.ncore = hv[2];
-        stats.ntiles = nf > 0 ? hv[4] : 0;
     } else {
         {
             StageTimer t(prof, s, "final");
@@ -1613,29 +1654,64 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
         }
         {
             StageTimer t(prof, s, "output");
-            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
-                               ensure_inv(), core, lab, a.core_out, a.root_out);
+            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv, core,
+                               lab, a.core_out, a.root_out);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        int32_t hv[5];
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(hv, misc_i, sizeof(hv), hipMemcpyDeviceToHost, s));
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-        stats.ncells = nf > 0 ? hv[0] : 0;
-        stats.ncore = hv[2];
-        stats.ntiles = nf > 0 ? hv[4] : 0;
     }
-    stats.nclusters = k;
-    if (st) *st = stats;
     if (slab) {
         slab->valid = a.zone != nullptr;
         slab->n = n;
-        slab->nf = nf;
         slab->eps2 = eps2;
-        slab->g = g;
         slab->nbr = nbr;
         slab->nbr_k = nbr_k;
     }
-    return k;
+}
+
+void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
+    if (ws.fit_n == 0) {
+        DBSCAN_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(int32_t), s));
+        return;
+    }
+    const int32_t* st = reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16);
+    hipLaunchKernelGGL(nclusters_kernel, dim3(1), dim3(1), 0, s, st, d_out);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+FitStats read_fit_stats(hipStream_t s, Workspace& ws) {
+    FitStats stats;
+    stats.n = ws.fit_n;
+    stats.grid_mode = ws.fit_mode;
+    if (ws.fit_n == 0) return stats;
+    double buf[24];
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(buf, ws.misc.p, sizeof(buf), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    GridParams g;
+    memcpy(&g, buf + 8, sizeof(g));
+    int32_t v[kStCount];
+    memcpy(v, buf + 16, sizeof(v));
+    if (v[kStError]) throw ArgError{"cannot size the eps grid"};
+    stats.nf = v[kStNf];
+    if (ws.fit_mode == kGridEps && stats.nf == 0) stats.grid_mode = kGridNoPairs;
+    const bool grid = stats.nf > 0 && ws.fit_mode != kGridNoPairs;
+    stats.nx = grid ? g.nx : 0;
+    stats.ny = grid ? g.ny : 0;
+    stats.clique = grid ? g.clique : 0;
+    stats.bits = v[kStBits];
+    stats.ncells = grid ? v[kStCells] : 0;
+    stats.ntiles = grid ? v[kStTiles] : 0;
+    stats.ncore = v[kStCore];
+    stats.nclusters = v[kStClusters];
+    return stats;
+}
+
+int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
+                SlabState* slab) {
+    enqueue_fit(s, ws, prof, a, slab);
+    const FitStats stats = read_fit_stats(s, ws);
+    if (slab) slab->nf = stats.nf;
+    if (st) *st = stats;
+    return a.zone ? 0 : stats.nclusters;
 }
 
 void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
@@ -1648,7 +1724,10 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
     hipLaunchKernelGGL(label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
-                       static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k, st.nf, st.n, st.eps2,
+                       static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
+                       reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) +
+                           kStNf,
+                       st.n, st.eps2,
                        mode, static_cast<const int32_t*>(ws.perm_sorted),
                        static_cast<const uint8_t*>(ws.core.p),
                        static_cast<const int32_t*>(ws.lab.p), (const int32_t*)nullptr, zone, gid,

@@ -34,6 +34,21 @@ namespace dbscan {
 
 constexpr uint32_t kSentinelKey = 0xFFFFFFFFu;
 constexpr int kBlock = 256;
+constexpr int64_t kMaxGridTiles = int64_t(1) << 23;  // 8x8-cell tiles per grid (u32 keys)
+
+// Device-side fit state (ints after the grid in the handle's misc buffer), written by kernels
+// and read back by the host only when it synchronizes.
+enum FitState {
+    kStCells = 0,     // occupied eps cells
+    kStClusters = 1,  // clusters of a full fit
+    kStCore = 2,      // core points
+    kStQuarters = 3,  // occupied quarter cells
+    kStTiles = 4,     // occupied tiles
+    kStNf = 6,        // points inside the grid (finite coordinates)
+    kStBits = 7,      // radix key width
+    kStError = 8,     // the eps grid could not be sized
+    kStCount = 16
+};
 
 #define DBSCAN_HIP_CHECK(expr)                                                              \
     do {                                                                                    \
@@ -98,6 +113,8 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed;
+    int64_t fit_n = 0;               // the last enqueued fit
+    int fit_mode = 0;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
@@ -150,6 +167,12 @@ struct SlabState {
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
                 SlabState* slab);
+// The same fit, enqueued without any host synchronization; read_fit_stats (which synchronizes)
+// returns its stats, write_nclusters enqueues a copy of its cluster count to device memory.
+void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
+                 SlabState* slab);
+FitStats read_fit_stats(hipStream_t s, Workspace& ws);
+void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);
 void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
                     const int32_t* label_of_root, int32_t mode, int32_t* cluster, uint8_t* flag);
@@ -164,11 +187,13 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
                     int32_t* total_dev, DevBuf& tmp);
 
-// LSD radix sort of (key, val) pairs on the low `bits` bits; results end in key/val
+// LSD radix sort of (key, val) pairs on the low bits; results end in key/val
 // (ping-pong through key2/val2).  Stable.
+// max_bits bounds the key width on the host (the pass count); bits_dev holds the actual width
+// on the device: passes at or beyond it copy instead of sorting.
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
-                      int32_t*& val2, int64_t n, int bits, DevBuf& hist, DevBuf& scan_tmp,
-                      Profiler* prof);
+                      int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
+                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

@@ -148,8 +148,10 @@ size_t scan_tmp_elems(int64_t n) {
 
 __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* __restrict__ key,
                                                                int64_t n, int shift,
+                                                               const int32_t* __restrict__ bits_p,
                                                                int64_t nblocks,
                                                                int32_t* __restrict__ hist) {
+    if (shift >= *bits_p) return;  // digit beyond the key width: the downsweep copies
     __shared__ uint32_t h[kWaves][256];
     const int w = threadIdx.x >> 6;
     for (int d = threadIdx.x; d < kWaves * 256; d += kBlock) (&h[0][0])[d] = 0;
@@ -180,11 +182,19 @@ struct DownsweepSmem {
 __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
     uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, int64_t n, int shift,
-    int64_t nblocks, const int32_t* __restrict__ hist_scanned) {
+    const int32_t* __restrict__ bits_p, int64_t nblocks,
+    const int32_t* __restrict__ hist_scanned) {
     __shared__ DownsweepSmem sm;
     const int t = threadIdx.x, w = t >> 6, lane = lane_id();
     const int64_t base = (int64_t)blockIdx.x * kTile;
     const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+    if (shift >= *bits_p) {  // every key has this digit 0 (or all ones: the sentinel): copy
+        for (int j = t; j < tile_n; j += kBlock) {
+            key_out[base + j] = key[base + j];
+            val_out[base + j] = val[base + j];
+        }
+        return;
+    }
 
     {  // zero the count table (32 KB): 8 x 16 B per thread
         uint4* z = reinterpret_cast<uint4*>(&sm.wcnt[0][0]);
@@ -364,16 +374,16 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 }
 
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
-                      int32_t*& val2, int64_t n, int bits, DevBuf& hist, DevBuf& scan_tmp,
-                      Profiler* prof) {
-    if (n <= 1 || bits <= 0) return;
+                      int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
+                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof) {
+    if (n <= 0 || max_bits <= 0) return;
     const int64_t nb = (n + kTile - 1) / kTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
-    for (int shift = 0; shift < bits; shift += 8) {
+    for (int shift = 0; shift < max_bits; shift += 8) {
         {
             StageTimer st(prof, s, "sort_upsweep");
             hipLaunchKernelGGL(radix_upsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, key,
-                               n, shift, nb, h);
+                               n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -383,7 +393,7 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         {
             StageTimer st(prof, s, "sort_downsweep");
             hipLaunchKernelGGL(radix_downsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s,
-                               key, val, key2, val2, n, shift, nb, h);
+                               key, val, key2, val2, n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         uint32_t* tk = key;

@@ -29,6 +29,8 @@ SIGNATURES = [
     ("dbscan_fit", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_fit_h", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_fit_device", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_fit_device_async", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_sync", _i32, [_vp]),
     ("dbscan_stream", _vp, [_vp]),
     ("dbscan_last_stats", _i32, [_vp, _vp, _i32]),
     ("dbscan_profile_enable", _i32, [_vp, _i32]),
@@ -108,6 +110,10 @@ class Handle:
             self.close()
         except Exception:
             pass
+
+    def sync(self) -> None:
+        """Wait for the handle's stream; settles an asynchronous fit (stats, errors)."""
+        check(load().dbscan_sync(self._h))
 
     @property
     def stream(self) -> int:

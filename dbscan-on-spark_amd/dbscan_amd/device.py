@@ -35,6 +35,24 @@ def fit_tensors(x: torch.Tensor, y: torch.Tensor, eps: float, min_points: int, m
     return cluster, flag, int(k.value)
 
 
+def fit_tensors_async(x: torch.Tensor, y: torch.Tensor, eps: float, min_points: int, mode: int,
+                      handle: _lib.Handle, cluster: torch.Tensor, flag: torch.Tensor,
+                      n_clusters: torch.Tensor = None) -> None:
+    """Enqueue a fit on the handle's stream and return at once (dbscan_fit_device_async).
+    n_clusters (int32 device tensor of one element) receives the cluster count; call
+    handle.sync() (or synchronize the device) before reading any output.  x/y must not be
+    written by other streams until then."""
+    assert x.is_cuda and y.is_cuda and x.dtype == torch.float64 and y.dtype == torch.float64
+    assert x.shape == y.shape and x.dim() == 1 and x.is_contiguous() and y.is_contiguous()
+    n = x.numel()
+    assert cluster.numel() == n and flag.numel() == n and cluster.dtype == torch.int32 \
+        and flag.dtype == torch.uint8
+    nk = _p(n_clusters) if n_clusters is not None else None
+    _lib.check(_lib.load().dbscan_fit_device_async(handle.ptr, _p(x), _p(y), n, float(eps),
+                                                   int(min_points), int(mode), _p(cluster),
+                                                   _p(flag), nk))
+
+
 def generate_blobs(n: int, noise: float, dense: float, seed: int, handle: _lib.Handle,
                    device=None):
     """SURVEY §8d generator on the device (no PCIe): returns (x, y) float64 tensors."""

@@ -82,10 +82,22 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
 
 /* Device-resident form: d_x, d_y, d_cluster, d_flag are device pointers on the handle's
  * device.  All work is enqueued on the handle's stream; the call returns after the stream has
- * drained (the cluster count is read back).  This is the form bench.py times. */
+ * drained (the cluster count is read back). */
 int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
                           double eps, int32_t min_points, int32_t mode, int32_t* d_cluster,
                           uint8_t* d_flag, int32_t* n_clusters_out);
+
+/* Asynchronous device-resident form: enqueues the whole fit on the handle's stream and returns
+ * without waiting (no host synchronization anywhere inside a fit: the eps grid is sized on the
+ * device).  The cluster count is written to DEVICE memory at d_n_clusters (may be NULL).
+ * dbscan_sync waits for the stream, then makes the fit's statistics available and reports
+ * device-side errors (an eps grid that cannot be sized) as DBSCAN_EARG.  Any synchronous entry
+ * point on the same handle settles a pending asynchronous fit first.  bench.py times this form:
+ * K fits back to back, one synchronization. */
+int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                int64_t n, double eps, int32_t min_points, int32_t mode,
+                                int32_t* d_cluster, uint8_t* d_flag, int32_t* d_n_clusters);
+int32_t dbscan_sync(dbscan_handle* h);
 
 /* The handle's hipStream_t (as void*), for callers that order their own work around it. */
 void* dbscan_stream(dbscan_handle* h);

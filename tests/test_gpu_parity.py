@@ -180,3 +180,38 @@ def test_argument_errors(dm, handle):
         == _lib.DBSCAN_EARG
     assert L.dbscan_fit_h(handle.ptr, p(a), p(a), 0, 0.3, 1, 0, p(c), p(f), ctypes.byref(k)) \
         == _lib.DBSCAN_OK and k.value == 0
+
+
+def test_async_fits_back_to_back(dm, handle):
+    """dbscan_fit_device_async: several fits of different inputs (grid, all-pairs, no-finite)
+    enqueued without any host synchronization, each output buffer equal to the oracle after
+    one dbscan_sync; the cluster count lands in device memory."""
+    import torch
+    from dbscan_amd import device as D
+
+    cases = []
+    x, y = gen_blobs(20000, noise=0.2, seed=5)
+    cases.append((x, y, 2.55 * 0.9, 10, 0))
+    xs, ys = gen_blobs(3000, seed=6)
+    cases.append((xs, ys, 1e200, 4, 1))  # eps*eps = +inf: all pairs
+    cases.append((np.full(500, np.nan), np.zeros(500), 1.0, 1, 0))  # nothing in the grid
+    cases.append((x, y, 2.55, 10, 1))
+    outs = []
+    for cx, cy, eps, mp, mode in cases:
+        tx = torch.tensor(cx, dtype=torch.float64, device="cuda")
+        ty = torch.tensor(cy, dtype=torch.float64, device="cuda")
+        cl = torch.empty(cx.size, dtype=torch.int32, device="cuda")
+        fl = torch.empty(cx.size, dtype=torch.uint8, device="cuda")
+        nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        D.fit_tensors_async(tx, ty, eps, mp, mode, handle, cl, fl, nk)
+        outs.append((tx, ty, cl, fl, nk))
+    handle.sync()
+    torch.cuda.synchronize()
+    for (cx, cy, eps, mp, mode), (_, _, cl, fl, nk) in zip(cases, outs):
+        rc, rf, rk = O.fit_grid(cx, cy, eps, mp, mode)
+        assert int(nk.item()) == rk
+        np.testing.assert_array_equal(cl.cpu().numpy(), rc)
+        np.testing.assert_array_equal(fl.cpu().numpy(), rf)
+    st = handle.stats()  # the last fit's
+    assert st["n"] == 20000 and st["finite"] == 20000
