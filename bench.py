@@ -207,7 +207,7 @@ def main():
                 "parallelism": ("single GPU" if world == 1 and not args.node else
                                 f"slab x{world} + {'RCCL' if args.backend == 'nccl' else args.backend} merge"),
                 "clusters": k, "core_points": stats.get("core"),
-                "occupied_cells": stats.get("cells")},
+                "occupied_cells": stats.get("cells"), "occupied_tiles": stats.get("tiles")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {k2: round(v, 4) for k2, v in stages.items()},

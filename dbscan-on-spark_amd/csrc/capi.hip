@@ -172,6 +172,12 @@ thread_local std::unique_ptr<dbscan_handle, void (*)(dbscan_handle*)> g_tls_hand
 
 void set_err(const std::string& s) { g_err = s; }
 
+}  // namespace
+
+void dbscan::set_last_error(const std::string& s) { set_err(s); }
+
+namespace {
+
 template <class F>
 int32_t guarded(dbscan_handle* h, F&& f) {
     g_err.clear();
@@ -399,9 +405,30 @@ int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double
     });
 }
 
+int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
+                                       const int64_t* d_gid, const int32_t* d_root,
+                                       const int32_t* d_parent, int64_t* d_gs_of_root,
+                                       int64_t* d_own_roots, int64_t* n_own_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
+        if (n < 0 || !n_own_out) throw dbscan::ArgError{"bad merge-roots arguments"};
+        if (n > 0 && (!d_zone || !d_gid || !d_root || !d_parent || !d_gs_of_root || !d_own_roots))
+            throw dbscan::ArgError{"NULL array pointer"};
+        *n_own_out = dbscan::run_slab_merge_roots(h->stream, h->ws, n, d_zone, d_gid, d_root,
+                                                  d_parent, d_gs_of_root, d_own_roots);
+        return DBSCAN_OK;
+    });
+}
+
 int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
-                                 const int64_t* d_gs_of_root, const int32_t* d_label_of_root,
-                                 int32_t mode, int32_t* d_cluster, uint8_t* d_flag) {
+                                 const int64_t* d_gs_of_root, const int64_t* d_all_roots,
+                                 int64_t n_all_roots, int32_t mode, int32_t* d_cluster,
+                                 uint8_t* d_flag) {
     if (!h) {
         set_err("NULL handle");
         return DBSCAN_EARG;
@@ -411,11 +438,12 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
         settle(h);
         if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
             throw dbscan::ArgError{"bad mode"};
-        if (h->slab.n > 0 && (!d_zone || !d_gid || !d_gs_of_root || !d_label_of_root ||
-                              !d_cluster || !d_flag))
+        if (n_all_roots < 0) throw dbscan::ArgError{"n_all_roots < 0"};
+        if (h->slab.n > 0 && (!d_zone || !d_gid || !d_gs_of_root || !d_cluster || !d_flag ||
+                              (n_all_roots > 0 && !d_all_roots)))
             throw dbscan::ArgError{"NULL array pointer"};
         dbscan::run_slab_label(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gid, d_gs_of_root,
-                               d_label_of_root, mode, d_cluster, d_flag);
+                               d_all_roots, n_all_roots, mode, d_cluster, d_flag);
         h->prof.flush();
         return DBSCAN_OK;
     });

@@ -655,8 +655,7 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
-    int32_t min_points, const int32_t* __restrict__ perm,
-    const uint8_t* __restrict__ zone, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
     int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate) {
     __shared__ TileStage st;
     __shared__ double2 buf[CAP];
@@ -694,9 +693,7 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core;
-                if (zone && zone[perm[p]] == 2) {
-                    is_core = false;  // outer halo of a slab fit: a count candidate only
-                } else if (min_points <= 0) {
+                if (min_points <= 0) {
                     is_core = true;
                 } else if (ablate == 1) {
                     is_core = false;
@@ -712,9 +709,7 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
         } else {
             for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
                 bool is_core;
-                if (zone && zone[perm[p]] == 2) {
-                    is_core = false;
-                } else if (min_points <= 0) {
+                if (min_points <= 0) {
                     is_core = true;
                 } else {
                     is_core = count_point<false>(st, buf, xy, cell, seg, 0, 0, p, eps2,
@@ -738,13 +733,23 @@ __global__ __launch_bounds__(kBlock) void count_tile_kernel(
     }
 }
 
+// Slab fits: outer-halo points (zone 2) are count candidates only, never core.  The count
+// kernels treat every point alike; this clears the zone-2 core flags afterwards, reading the
+// zones coalesced in slab order (a random write only per zone-2 point, a thin band) instead of
+// a random zone read per point inside the count.
+__global__ __launch_bounds__(kBlock) void zone_fix_kernel(int64_t n,
+                                                          const uint8_t* __restrict__ zone,
+                                                          const int32_t* __restrict__ inv,
+                                                          uint8_t* __restrict__ core) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && zone[i] == 2) core[inv[i]] = 0;
+}
+
 // Slots outside the grid (non-finite coordinates, or every slot when eps*eps is NaN): no
 // neighbours, not even themselves.
 __global__ __launch_bounds__(kBlock) void count_rest_kernel(const int32_t* __restrict__ nf_p,
                                                             int64_t n,
                                                             int32_t min_points,
-                                                            const int32_t* __restrict__ perm,
-                                                            const uint8_t* __restrict__ zone,
                                                             uint8_t* __restrict__ core,
                                                             int32_t* __restrict__ parent,
                                                             int32_t* __restrict__ block_cores) {
@@ -752,7 +757,7 @@ __global__ __launch_bounds__(kBlock) void count_rest_kernel(const int32_t* __res
     int mine = 0;
     for (int64_t p = *nf_p + (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n;
          p += (int64_t)gridDim.x * kBlock) {
-        const bool is_core = min_points <= 0 && !(zone && zone[perm[p]] == 2);
+        const bool is_core = min_points <= 0;
         parent[p] = (int32_t)p;
         core[p] = is_core ? 1 : 0;
         mine += is_core ? 1 : 0;
@@ -1298,20 +1303,46 @@ __global__ __launch_bounds__(kBlock) void permute_out_kernel(
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
 
-// Slab fit, phase 1 output (multi-GPU node path): core flag and local root (slab index of the
-// minimum-index core of the local component), in slab order (gathered through inv).
+// Slab fit, phase 1 output (multi-GPU node path): per sorted slot, the slab index of the
+// minimum-index core of its local component (lab) or -1 for a non-core, packed coalesced, then
+// moved to slab order through inv (one random read per point): root_out, core_out = root >= 0.
+__global__ __launch_bounds__(kBlock) void slab_pack_kernel(int64_t n,
+                                                           const uint8_t* __restrict__ core,
+                                                           const int32_t* __restrict__ lab,
+                                                           int32_t* __restrict__ packed) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p < n) packed[p] = core[p] ? lab[p] : -1;
+}
+
 __global__ __launch_bounds__(kBlock) void slab_roots_kernel(int64_t n,
                                                             const int32_t* __restrict__ inv,
-                                                            const uint8_t* __restrict__ core,
-                                                            const int32_t* __restrict__ lab,
+                                                            const int32_t* __restrict__ packed,
                                                             uint8_t* __restrict__ core_out,
                                                             int32_t* __restrict__ root_out) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const int32_t p = inv[i];
-    const uint8_t c = core[p];
-    core_out[i] = c;
-    root_out[i] = c ? lab[p] : -1;
+    const int32_t v = packed[inv[i]];
+    core_out[i] = v >= 0 ? 1 : 0;
+    root_out[i] = v;
+}
+
+// Slab label, phase 2 prologue: the global cluster id of every local root r (a sorted slot whose
+// lab is its own visit index): 1 + rank of its global s(K) among all ranks' global roots
+// (all_roots sorted ascending; every s(K) is in it).
+__global__ __launch_bounds__(kBlock) void slab_root_labels_kernel(
+    int64_t n, const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    const int32_t* __restrict__ lab, const int64_t* __restrict__ gs_of_root,
+    const int64_t* __restrict__ all_roots, int64_t n_roots, int32_t* __restrict__ label_of_root) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n || !core[p] || lab[p] != perm[p]) return;
+    const int32_t r = lab[p];
+    const int64_t g = gs_of_root[r];
+    int64_t lo = 0, hi = n_roots;  // first index with all_roots[idx] >= g
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (all_roots[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    label_of_root[r] = (int32_t)(lo + 1);
 }
 
 // Grid sizing (see DESIGN.md "grid soundness"), on the device so a fit needs no host sync: cell side >= R*(1+2^-16) with
@@ -1578,16 +1609,19 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 default: break;
             }
             hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
-                               tstage, &st[kStTiles], eps2, a.min_points, perm, a.zone, core,
+                               tstage, &st[kStTiles], eps2, a.min_points, core,
                                parent, block_cores, nbr, nbr_k, count_ablate());
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
         hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
-                           a.min_points, perm, a.zone, core, parent, block_cores + tile_grid);
+                           a.min_points, core, parent, block_cores + tile_grid);
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = (int64_t)tile_grid + rest_grid;
         exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan_tmp);
+        if (a.zone)  // (the core count above then includes zone-2 points: a statistic only)
+            hipLaunchKernelGGL(zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
+                               core);
     }
     if (mode == kGridEps) {  // quarter-cell unions (no-ops unless the grid made them cliques)
         {
@@ -1654,8 +1688,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         {
             StageTimer t(prof, s, "output");
-            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv, core,
-                               lab, a.core_out, a.root_out);
+            int32_t* packed = static_cast<int32_t*>(ws.packed.ensure(n * sizeof(int32_t)));
+            hipLaunchKernelGGL(slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, core, lab,
+                               packed);
+            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
+                               packed, a.core_out, a.root_out);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     }
@@ -1716,21 +1753,24 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
 
 void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
-                    const int32_t* label_of_root, int32_t mode, int32_t* cluster,
+                    const int64_t* all_roots, int64_t n_roots, int32_t mode, int32_t* cluster,
                     uint8_t* flag) {
     if (!st.valid) throw ArgError{"dbscan_slab_label_device: no slab fit on this handle"};
     if (st.n == 0) return;
     StageTimer t(prof, s, "slab_label");
+    const int32_t* perm = static_cast<const int32_t*>(ws.perm_sorted);
+    const uint8_t* core = static_cast<const uint8_t*>(ws.core.p);
+    const int32_t* lab = static_cast<const int32_t*>(ws.lab.p);
+    int32_t* label_of_root = static_cast<int32_t*>(ws.slab_lor.ensure(st.n * sizeof(int32_t)));
+    hipLaunchKernelGGL(slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n, perm,
+                       core, lab, gs_of_root, all_roots, n_roots, label_of_root);
     uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
     hipLaunchKernelGGL(label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
                        static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
                        reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) +
                            kStNf,
-                       st.n, st.eps2,
-                       mode, static_cast<const int32_t*>(ws.perm_sorted),
-                       static_cast<const uint8_t*>(ws.core.p),
-                       static_cast<const int32_t*>(ws.lab.p), (const int32_t*)nullptr, zone, gid,
+                       st.n, st.eps2, mode, perm, core, lab, (const int32_t*)nullptr, zone, gid,
                        gs_of_root, label_of_root, packed);
     hipLaunchKernelGGL(permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);

@@ -66,6 +66,9 @@ struct ArgError {
     std::string what;
 };
 
+// The thread-local message behind dbscan_last_error().
+void set_last_error(const std::string& s);
+
 // Grow-only device buffer (owned by one handle; never copied).
 struct DevBuf {
     void* p = nullptr;
@@ -112,7 +115,7 @@ struct StageTimer {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed;
+        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
@@ -121,7 +124,8 @@ struct Workspace {
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
-                          &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed})
+                          &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
+                          &own_flag})
             b->release();
     }
 };
@@ -175,7 +179,13 @@ FitStats read_fit_stats(hipStream_t s, Workspace& ws);
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);
 void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
-                    const int32_t* label_of_root, int32_t mode, int32_t* cluster, uint8_t* flag);
+                    const int64_t* all_roots, int64_t n_roots, int32_t mode, int32_t* cluster,
+                    uint8_t* flag);
+// Node-path merge (merge.hip): every local root's global s(K) (gs_of_root, slab index) and the
+// zone-0 global roots owned here, compacted in slab (= gid) order; returns their count (syncs).
+int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
+                             const int64_t* gid, const int32_t* root, const int32_t* parent,
+                             int64_t* gs_of_root, int64_t* own_roots);
 
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:

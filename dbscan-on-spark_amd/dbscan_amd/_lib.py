@@ -37,7 +37,10 @@ SIGNATURES = [
     ("dbscan_profile_reset", _i32, [_vp]),
     ("dbscan_profile_read", _i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
-    ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
+    ("dbscan_merge_union_device", _i32, [_vp, _vp, _i64, _vp, _vp]),
+    ("dbscan_merge_reset_device", _i32, [_vp, _vp, _i64, _vp, _vp]),
+    ("dbscan_slab_merge_roots_device", _i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
 ]
 

@@ -78,18 +78,34 @@ def slab_fit(x: torch.Tensor, y: torch.Tensor, zone: torch.Tensor, eps: float, m
     return core, root
 
 
+def slab_merge_roots(zone: torch.Tensor, gid: torch.Tensor, root: torch.Tensor,
+                     parent: torch.Tensor, gs_of_root: torch.Tensor, own_roots: torch.Tensor,
+                     handle: _lib.Handle) -> int:
+    """After a slab fit and the merge union: gs_of_root[p] for every local root p; the global
+    roots owned here into own_roots (increasing gid); returns their count."""
+    k = ctypes.c_int64(0)
+    torch.cuda.current_stream(zone.device).synchronize()
+    _lib.check(_lib.load().dbscan_slab_merge_roots_device(handle.ptr, zone.numel(), _p(zone),
+                                                          _p(gid), _p(root), _p(parent),
+                                                          _p(gs_of_root), _p(own_roots),
+                                                          ctypes.byref(k)))
+    return int(k.value)
+
+
 def slab_label(zone: torch.Tensor, gid: torch.Tensor, gs_of_root: torch.Tensor,
-               label_of_root: torch.Tensor, mode: int, handle: _lib.Handle, cluster=None,
+               all_roots: torch.Tensor, mode: int, handle: _lib.Handle, cluster=None,
                flag=None):
     """Slab fit phase 2 (after the global merge): (cluster int32, flag uint8) in slab order;
-    only zone-0 entries are written."""
+    only zone-0 entries are written.  all_roots: every global component's s(K), sorted."""
     n = zone.numel()
     if cluster is None:
         cluster = torch.zeros(n, dtype=torch.int32, device=zone.device)
     if flag is None:
         flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
+    all_roots = all_roots.to(torch.int64).contiguous()
     torch.cuda.current_stream(zone.device).synchronize()
     _lib.check(_lib.load().dbscan_slab_label_device(handle.ptr, _p(zone), _p(gid),
-                                                    _p(gs_of_root), _p(label_of_root),
-                                                    int(mode), _p(cluster), _p(flag)))
+                                                    _p(gs_of_root), _p(all_roots),
+                                                    all_roots.numel(), int(mode), _p(cluster),
+                                                    _p(flag)))
     return cluster, flag

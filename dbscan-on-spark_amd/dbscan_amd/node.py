@@ -16,8 +16,10 @@ Naive noise rule and the cluster numbering -- unlike the reference's merge, SURV
     core flags are the global ones.
   * every global core-core edge (p, q) has p owned by some rank g and q in g's zone 0/1, so it
     is an edge of g's local graph: global components are unions of local components that share
-    a core point.  Shared core points (present in zones 0/1 of two ranks) are all-gathered as
-    (gid, local root gid) records; a min-label merge gives each local root its global s(K)
+    a core point.  Shared points (present in zones 0/1 of two ranks: a set fixed per job) are
+    all-gathered each step as (gid, local root gid or -1) records -- fixed sizes, one RCCL
+    all-gather, no size exchange; every rank runs the same lock-free union-find over the
+    records' gids on its GPU (csrc/merge.hip), which gives each local root its global s(K)
     (= min visit index of the component, the reference's cluster-opening order).
   * owned global roots are all-gathered; cluster id = 1 + rank of s(K) among them.
   * border/noise needs min over core neighbours of s(K): done after the merge on the GPU
@@ -25,12 +27,18 @@ Naive noise rule and the cluster numbering -- unlike the reference's merge, SURV
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import List, Optional
 
 import torch
 
 from . import _lib
+
+
+def _p(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
 
 OUT = 255  # point not in this rank's slab
 
@@ -118,16 +126,29 @@ class Comm:
         else:
             self.dist, self.world, self.rank, self.host = None, 1, 0, True
 
+    def sizes(self, k: int) -> List[int]:
+        """Every rank's k, in rank order."""
+        if self.world == 1:
+            return [k]
+        n = torch.tensor([k], dtype=torch.int64,
+                         device="cpu" if self.host else torch.device("cuda",
+                                                                      torch.cuda.current_device()))
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n)
+        return [int(v) for v in torch.cat(ns).cpu().tolist()]
+
     def allgather_varlen(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate every rank's t along its last dim, in rank order."""
         if self.world == 1:
             return t
+        return self.allgather_fixed(t, self.sizes(t.shape[-1]))
+
+    def allgather_fixed(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
+        """allgather_varlen when every rank's length is already known (no size exchange)."""
+        if self.world == 1:
+            return t
         dev = t.device
         tt = t.cpu() if self.host else t.contiguous()
-        n = torch.tensor([tt.shape[-1]], dtype=torch.int64, device=tt.device)
-        ns = [torch.zeros_like(n) for _ in range(self.world)]
-        self.dist.all_gather(ns, n)
-        sizes = [int(v.item()) for v in ns]
         mx = max(sizes)
         pad = torch.zeros(tt.shape[:-1] + (mx,), dtype=tt.dtype, device=tt.device)
         pad[..., :tt.shape[-1]] = tt
@@ -138,50 +159,64 @@ class Comm:
 
 
 class HipSlabOps:
-    """The product slab fit: libdbscan_hip.so through device tensors."""
+    """The product slab fit and merge: libdbscan_hip.so through device tensors (the merge
+    kernels run on torch's current stream)."""
 
     def __init__(self, handle: _lib.Handle):
         self.h = handle
+        self._bufs = None
 
     def fit(self, x, y, zone, eps, min_points):
         from . import device as D
 
         return D.slab_fit(x, y, zone, eps, min_points, self.h)
 
-    def label(self, zone, gid, gs_of_root, label_of_root, mode):
+    @staticmethod
+    def _stream():
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def merge(self, a, b, parent):
+        _lib.check(_lib.load().dbscan_merge_union_device(_p(a), _p(b), a.numel(), _p(parent),
+                                                         self._stream()))
+
+    def merge_reset(self, a, b, parent):
+        _lib.check(_lib.load().dbscan_merge_reset_device(_p(a), _p(b), a.numel(), _p(parent),
+                                                         self._stream()))
+
+    def merge_roots(self, zone, gid, root, parent, gs_of_root):
         from . import device as D
 
-        return D.slab_label(zone, gid, gs_of_root, label_of_root, mode, self.h)
+        n = zone.numel()
+        if self._bufs is None or self._bufs.numel() < max(1, n):
+            self._bufs = torch.empty(max(1, n), dtype=torch.int64, device=zone.device)
+        k = D.slab_merge_roots(zone, gid, root, parent, gs_of_root, self._bufs, self.h)
+        return self._bufs[:k]
 
+    def label(self, zone, gid, gs_of_root, all_roots, mode):
+        from . import device as D
 
-def merge_min_labels(a: torch.Tensor, b: torch.Tensor):
-    """Connected components of the graph with edges (a_i, b_i) over int64 node ids; returns
-    (nodes sorted, min node id of each node's component).  Min-label propagation with pointer
-    jumping (each round: scatter-min over edges, then label = label[label])."""
-    nodes = torch.unique(torch.cat([a, b]))
-    ia = torch.searchsorted(nodes, a)
-    ib = torch.searchsorted(nodes, b)
-    lab = nodes.clone()
-    for _ in range(64):
-        m = torch.minimum(lab[ia], lab[ib])
-        new = lab.scatter_reduce(0, ia, m, reduce="amin").scatter_reduce(0, ib, m,
-                                                                          reduce="amin")
-        new = new[torch.searchsorted(nodes, new)]  # pointer jump
-        if torch.equal(new, lab):
-            break
-        lab = new
-    return nodes, lab
+        return D.slab_label(zone, gid, gs_of_root, all_roots, mode, self.h)
 
 
 class NodeJob:
     """One rank's share of a whole-node fit.  run() is one step (timed by bench.py)."""
 
-    def __init__(self, x, y, zone, gid, shared, eps, min_points, mode, comm: Comm, ops):
+    def __init__(self, x, y, zone, gid, shared, eps, min_points, mode, comm: Comm, ops,
+                 n_total: int):
         self.x, self.y, self.zone, self.gid, self.shared = x, y, zone, gid, shared
         self.eps, self.min_points, self.mode = float(eps), int(min_points), int(mode)
         self.comm, self.ops = comm, ops
         self.cluster = self.flag = None
         self.n_clusters = 0
+        # Static per job: the shared points (slab indices), the a-side of every rank's records
+        # and the record counts, so each step exchanges only the b-side at known sizes.
+        dev = x.device
+        self.sh_idx = torch.nonzero(shared).flatten()
+        a = gid[self.sh_idx]
+        self.rec_sizes = comm.sizes(a.numel())
+        self.all_a = comm.allgather_fixed(a, self.rec_sizes)
+        self.parent = torch.full((max(1, int(n_total)),), -1, dtype=torch.int32, device=dev)
+        self.gs_of_root = torch.zeros(max(1, x.numel()), dtype=torch.int64, device=dev)
 
     @classmethod
     def from_global(cls, x_all, y_all, eps, min_points, mode, comm: Comm, ops,
@@ -201,7 +236,7 @@ class NodeJob:
         idx = torch.nonzero(z != OUT).flatten()  # ascending: global visit order preserved
         job = cls(x_all[idx].contiguous(), y_all[idx].contiguous(), z[idx].contiguous(),
                   idx.to(torch.int64).contiguous(), sh[idx].contiguous(), eps, min_points, mode,
-                  comm, ops)
+                  comm, ops, x_all.numel())
         job.cuts = cuts
         return job
 
@@ -219,35 +254,30 @@ class NodeJob:
         torch.cuda.empty_cache()
         return job
 
-    def run(self) -> int:
-        n = self.x.numel()
-        dev = self.x.device
+    def run(self, tick=None) -> int:
+        """One step.  tick(name), if given, is called after each phase (tools/node_breakdown.py
+        synchronizes and times there)."""
+        tick = tick or (lambda name: None)
         core, root = self.ops.fit(self.x, self.y, self.zone, self.eps, self.min_points)
-        corb = core.bool()
-        rootl = root.long()
-        # records: shared core points -> their local root, as global visit indices
-        sel = self.shared & corb
-        rec = torch.stack([self.gid[sel], self.gid[rootl[sel]]])
-        allrec = self.comm.allgather_varlen(rec)
-        ar = torch.arange(n, device=dev)
-        lmask = corb & (rootl == ar)  # local roots (zones 0/1)
-        lroots = torch.nonzero(lmask).flatten()
-        gs_of_root = torch.full((n,), -1, dtype=torch.int64, device=dev)
-        gs_of_root[lroots] = self.gid[lroots]
-        if allrec.shape[-1] > 0:
-            nodes, lab = merge_min_labels(allrec[0], allrec[1])
-            g = self.gid[lroots]
-            pos = torch.searchsorted(nodes, g).clamp(max=nodes.numel() - 1)
-            hit = nodes[pos] == g
-            gs_of_root[lroots[hit]] = lab[pos[hit]]
-        # global roots owned here: s(K) is a zone-0 core that is its own local root
-        own = lmask & (self.zone == 0) & (gs_of_root == self.gid)
-        all_roots, _ = torch.sort(self.comm.allgather_varlen(self.gid[own]))
-        label_of_root = torch.zeros(n, dtype=torch.int32, device=dev)
-        label_of_root[lroots] = (torch.searchsorted(all_roots, gs_of_root[lroots]) + 1).to(
-            torch.int32)
-        self.cluster, self.flag = self.ops.label(self.zone, self.gid, gs_of_root,
-                                                 label_of_root, self.mode)
+        tick("slab_fit")
+        # records: (gid of each shared point, gid of its local root, or -1 if not core here)
+        rs = root[self.sh_idx].long().clamp(min=0)
+        b = torch.where(core[self.sh_idx] != 0, self.gid[rs], torch.full_like(rs, -1))
+        all_b = self.comm.allgather_fixed(b, self.rec_sizes)
+        tick("records")
+        self.ops.merge(self.all_a, all_b, self.parent)
+        tick("merge")
+        # every local root's global s(K); the zone-0 global roots owned here
+        own = self.ops.merge_roots(self.zone, self.gid, root, self.parent, self.gs_of_root)
+        tick("roots")
+        # cluster id = 1 + rank of s(K) among all ranks' global roots (each rank's list is
+        # already in gid order)
+        all_roots, _ = torch.sort(self.comm.allgather_varlen(own))
+        self.ops.merge_reset(self.all_a, all_b, self.parent)
+        tick("numbering")
+        self.cluster, self.flag = self.ops.label(self.zone, self.gid, self.gs_of_root, all_roots,
+                                                 self.mode)
+        tick("slab_label")
         self.n_clusters = int(all_roots.numel())
         return self.n_clusters
 

@@ -132,16 +132,40 @@ int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, do
  * global min-label union; replaces DBSCAN.scala:158-222) and numbers global clusters.
  * Phase 2, dbscan_slab_label_device (same handle, no fit in between): labels of the zone-0
  *   points in slab order.  d_gid[i] = global visit index of slab point i; for every local root
- *   r: d_gs_of_root[r] = global s(K) of its component, d_label_of_root[r] = global cluster id.
- *   Cores get label_of_root[root]; a non-core takes the neighbour root with the smallest
- *   gs_of_root (Naive: only if that is < its own gid).  Zone 1/2 entries are left untouched.
- *   This replaces the relabel of DBSCAN.scala:232-270.                                      */
+ *   r: d_gs_of_root[r] = global s(K) of its component (dbscan_slab_merge_roots_device);
+ *   d_all_roots = the s(K) of every global component, all ranks, sorted ascending: a cluster
+ *   id is 1 + the rank of s(K) in it.  Cores get the id of their root's component; a non-core
+ *   takes the neighbour root with the smallest gs_of_root (Naive: only if that is < its own
+ *   gid).  Zone 1/2 entries are left untouched.  Replaces the relabel of DBSCAN.scala:232-270. */
 int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
                                int32_t min_points, uint8_t* d_core, int32_t* d_root);
 int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
-                                 const int64_t* d_gs_of_root, const int32_t* d_label_of_root,
-                                 int32_t mode, int32_t* d_cluster, uint8_t* d_flag);
+                                 const int64_t* d_gs_of_root, const int64_t* d_all_roots,
+                                 int64_t n_all_roots, int32_t mode, int32_t* d_cluster,
+                                 uint8_t* d_flag);
+
+/* Cross-slab merge of the node path (replaces DBSCAN.scala:158-222: band points,
+ * findAdjacencies, DBSCANGraph components, global ids), enqueued on the CALLER's stream
+ * (a hipStream_t passed as void*; the caller's current device).  Records (d_a[i], d_b[i]) are
+ * (gid of a shared core point, gid of its local root on the emitting rank), gathered from all
+ * ranks; d_b[i] < 0 marks a record to skip.  d_parent is a dense int32 array over all gids of
+ * the job, initialised to -1 once; the union leaves parent[x] = s(K) (smallest gid of x's
+ * global component) for every node x of a valid record, and dbscan_merge_reset_device restores
+ * those entries to -1 (O(records) per step).
+ * dbscan_slab_merge_roots_device (handle stream; synchronizes), after a slab fit and the union
+ * (d_root as returned by the slab fit: a local root p has d_root[p] == p): for every local root
+ * p, d_gs_of_root[p] = the global s(K) of its component; the zone-0 local roots whose s(K) is
+ * their own gid -- the global roots owned by this rank -- are written to d_own_roots in
+ * increasing gid order, their count to *n_own_out (host). */
+int32_t dbscan_merge_union_device(const int64_t* d_a, const int64_t* d_b, int64_t m,
+                                  int32_t* d_parent, void* stream);
+int32_t dbscan_merge_reset_device(const int64_t* d_a, const int64_t* d_b, int64_t m,
+                                  int32_t* d_parent, void* stream);
+int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
+                                       const int64_t* d_gid, const int32_t* d_root,
+                                       const int32_t* d_parent, int64_t* d_gs_of_root,
+                                       int64_t* d_own_roots, int64_t* n_own_out);
 
 /* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
  * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the

@@ -28,12 +28,49 @@ class OracleSlabOps:
         self.state = (xs, ys, zs, eps, core, root)
         return torch.from_numpy(core), torch.from_numpy(root)
 
-    def label(self, zone, gid, gs_of_root, label_of_root, mode):
+    # The merge of csrc/merge.hip restated in numpy: union-find over the records' gids, root =
+    # smallest gid of the component; parent is the dense gid-indexed array (-1 = untouched).
+    def merge(self, a, b, parent):
+        a, b, par = a.numpy(), b.numpy(), parent.numpy()
+        ok = b >= 0
+        up = {}
+
+        def find(v):
+            while up.get(v, v) != v:
+                v = up[v]
+            return v
+
+        for u, v in zip(a[ok].tolist(), b[ok].tolist()):
+            ru, rv = find(u), find(v)
+            if ru != rv:
+                up[max(ru, rv)] = min(ru, rv)
+        for v in set(a[ok].tolist()) | set(b[ok].tolist()):
+            par[v] = find(v)
+
+    def merge_reset(self, a, b, parent):
+        ok = b >= 0
+        parent[a[ok]] = -1
+        parent[b[ok]] = -1
+
+    def merge_roots(self, zone, gid, root, parent, gs_of_root):
+        n = zone.numel()
+        lroots = torch.nonzero(root == torch.arange(n, dtype=root.dtype)).flatten()
+        g = gid[lroots]
+        pg = parent[g].to(torch.int64)
+        gs = torch.where(pg >= 0, pg, g)
+        gs_of_root[lroots] = gs
+        self.lroots = lroots
+        return g[(zone[lroots] == 0) & (gs == g)]
+
+    def label(self, zone, gid, gs_of_root, all_roots, mode):
         import oracle as O
 
         xs, ys, zs, eps, core, root = self.state
+        label_of_root = np.zeros(xs.size, np.int32)
+        lr = self.lroots.numpy()
+        label_of_root[lr] = np.searchsorted(all_roots.numpy(), gs_of_root.numpy()[lr]) + 1
         cl, fl = O.slab_label(xs, ys, zs, eps, core, root, gid.numpy(), gs_of_root.numpy(),
-                              label_of_root.numpy(), mode)
+                              label_of_root, mode)
         return torch.from_numpy(cl), torch.from_numpy(fl)
 
 

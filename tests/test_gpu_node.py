@@ -30,3 +30,50 @@ def test_gpu_node_single_rank(tmp_path):
     rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
     np.testing.assert_array_equal(cl, rc)
     np.testing.assert_array_equal(fl, rf)
+
+
+def test_gpu_merge_kernels_vs_double():
+    """dbscan_merge_union_device / dbscan_slab_merge_roots_device / dbscan_merge_reset_device
+    against the numpy restatement (tests/node_worker.py) on random record graphs with long
+    chains, repeated nodes and skipped records."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import node
+    from node_worker import OracleSlabOps
+
+    dbscan_amd.load()
+    h = dbscan_amd.Handle(0)
+    ops = node.HipSlabOps(h)
+    ref = OracleSlabOps()
+    rng = np.random.default_rng(3)
+    n_total = 200_000
+    par = torch.full((n_total,), -1, dtype=torch.int32, device="cuda")
+    for trial in range(3):
+        m = 50_000
+        a = rng.integers(0, n_total, m)
+        b = np.minimum(a, rng.integers(0, n_total, m))  # b <= a, like a local root
+        b[rng.random(m) < 0.1] = -1
+        ta, tb = torch.tensor(a, device="cuda"), torch.tensor(b, device="cuda")
+        ops.merge(ta, tb, par)
+        rpar = torch.full((n_total,), -1, dtype=torch.int32)
+        ref.merge(torch.tensor(a), torch.tensor(b), rpar)
+        np.testing.assert_array_equal(par.cpu().numpy(), rpar.numpy())
+        # local roots of a synthetic slab: every 7th point (if core) roots its 7-run
+        n = 30_000
+        gid = torch.arange(n, dtype=torch.int64, device="cuda") * 5
+        core = torch.tensor((rng.random(n) < 0.7).astype(np.uint8), device="cuda")
+        ar = torch.arange(n, device="cuda")
+        root = torch.where(core != 0, torch.where(ar % 7 == 0, ar, ar // 7 * 7),
+                           torch.full_like(ar, -1)).to(torch.int32)
+        zone = torch.tensor(rng.integers(0, 2, n).astype(np.uint8), device="cuda")
+        gs = torch.zeros(n, dtype=torch.int64, device="cuda")
+        own = ops.merge_roots(zone, gid, root, par, gs)
+        rgs = torch.zeros(n, dtype=torch.int64)
+        rown = ref.merge_roots(zone.cpu(), gid.cpu(), root.cpu(), rpar, rgs)
+        rlr = ref.lroots.numpy()
+        assert own.cpu().tolist() == rown.tolist()  # increasing gid order
+        np.testing.assert_array_equal(gs.cpu().numpy()[rlr], rgs.numpy()[rlr])
+        ops.merge_reset(ta, tb, par)
+        assert bool((par == -1).all())
+    h.close()

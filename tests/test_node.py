@@ -134,12 +134,18 @@ def test_zone_margins_cover_the_predicate():
     assert torch.equal(s1 & (z1 <= 1), both & (z1 <= 1))
 
 
-def test_merge_min_labels():
-    import dbscan_amd.node as node
+def test_merge_double_components():
+    """The numpy restatement of the merge kernels (test double) on a known record graph:
+    roots are the smallest gid of each component; untouched entries stay -1; reset restores."""
+    from node_worker import OracleSlabOps
 
-    a = torch.tensor([10, 11, 12, 30, 31], dtype=torch.int64)
-    b = torch.tensor([11, 12, 13, 31, 5], dtype=torch.int64)
-    nodes, lab = node.merge_min_labels(a, b)
-    d = dict(zip(nodes.tolist(), lab.tolist()))
-    assert d[10] == d[11] == d[12] == d[13] == 10
-    assert d[30] == d[31] == d[5] == 5
+    ops = OracleSlabOps()
+    a = torch.tensor([10, 11, 12, 30, 31, 40], dtype=torch.int64)
+    b = torch.tensor([11, 12, 13, 31, 5, -1], dtype=torch.int64)
+    par = torch.full((64,), -1, dtype=torch.int32)
+    ops.merge(a, b, par)
+    assert par[[10, 11, 12, 13]].tolist() == [10] * 4
+    assert par[[30, 31, 5]].tolist() == [5] * 3
+    assert par[40] == -1 and par[0] == -1
+    ops.merge_reset(a, b, par)
+    assert bool((par == -1).all())

@@ -1,0 +1,46 @@
+"""Phase timing of one NodeJob.run() at N = 1 (node path overheads), synchronizing between
+phases.  python tools/node_breakdown.py [n]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
+import torch  # noqa: E402
+
+import dbscan_amd  # noqa: E402
+from dbscan_amd import node  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+h = dbscan_amd.Handle(0)
+job = node.NodeJob.synthetic(n, 0.0, 1.0, 1, 2.55, 10, h, None)
+T = {}
+
+
+last = [0.0]
+
+
+def tick(name):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    T[name] = T.get(name, 0.0) + (t - last[0]) * 1e3
+    last[0] = t
+
+
+def run():
+    torch.cuda.synchronize()
+    last[0] = time.perf_counter()
+    job.run(tick)
+
+
+for _ in range(3):
+    run()
+T.clear()
+K = 10
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(K):
+    run()
+torch.cuda.synchronize()
+tot = (time.perf_counter() - t0) * 1e3 / K
+print({k: round(v / K, 3) for k, v in T.items()}, "total_ms", round(tot, 3))
