@@ -979,6 +979,14 @@ __device__ bool pair_found_generic(const Src* __restrict__ src, int off, int4 a,
     return false;
 }
 
+// Orders one wave's LDS accesses across its lanes (a wave executes in lockstep; this keeps the
+// compiler from reordering LDS reads above another lane's earlier writes).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // LDS union-find over the tile's quarter cells (local indices; hook larger under smaller).
 __device__ __forceinline__ int lfind(int* lp, int x) {
     while (true) {
@@ -1078,7 +1086,8 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
     }
 }
 
-// Quarter pairs that cross a tile edge.  One wave per (tile, side): side 0 pairs the tile's
+// Quarter pairs that cross a tile edge.  One wave per (tile, side), each wave looping on its
+// own (no block barriers): side 0 pairs the tile's
 // east cell column with the E tile's west column plus the SE tile's corner cell; side 1 its
 // south row with the S tile's north row plus the SW tile's corner cell.  With the mirrored
 // sides of the other tiles, every pair of adjacent cells in different tiles is covered once.
@@ -1102,14 +1111,14 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
     __shared__ int ncomp[kBlock / 64][kEdgeNodes];
     __shared__ int nlp[kBlock / 64][kEdgeNodes];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int side = w & 1;
     const int ntiles = *ntiles_p;
-    const int npairs = (ntiles + 1) >> 1;
     int* lp = nlp[w];
-    for (int tp = blockIdx.x; tp < npairs; tp += gridDim.x) {
-        const int t = 2 * tp + (w >> 1);
+    // one (tile, side) per wave and loop trip: waves never wait for each other
+    for (int tw = blockIdx.x * (kBlock / 64) + w; tw < 2 * ntiles;
+         tw += gridDim.x * (kBlock / 64)) {
+        const int t = tw >> 1, side = tw & 1;
         int nA = 0, ntot = 0;
-        if (t < ntiles) {  // wave-uniform
+        {
             const int4 nb = tnb[t];
             const int occB = side ? nb.y : nb.x, occC = side ? nb.w : nb.z;
             const int k = lane & 7;
@@ -1145,7 +1154,7 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
                 ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
             }
         }
-        __syncthreads();
+        wave_sync();
         for (int i = lane; i < ntot; i += 64) {  // pre-join nodes sharing a tile component
             const int c = ncomp[w][i];
             int r = i;
@@ -1157,7 +1166,7 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
                     }
             lp[i] = r;
         }
-        __syncthreads();
+        wave_sync();
         const int a = lane & 31, half = lane >> 5;  // two lanes per own-strip quarter
         if (a < nA) {
             const int4 me = nqi[w][a];
@@ -1184,7 +1193,7 @@ __global__ __launch_bounds__(kBlock) void edge_union_kernel(
                     }
             }
         }
-        __syncthreads();
+        wave_sync();
     }
 }
 

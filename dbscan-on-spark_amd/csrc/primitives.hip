@@ -4,8 +4,8 @@
 //                      wave64 shuffle scans, recursive over the tile sums
 //   radix_sort_pairs   stable LSD radix sort, 8-bit digits, 4096-key tiles:
 //                      upsweep (per-wave LDS histograms) -> scan -> downsweep that ranks keys
-//                      with 64-bit wave ballots (match-any over the 8 digit bits), scans the
-//                      per-(round,wave,digit) counts in LDS, sorts the tile in LDS and writes
+//                      with 64-bit wave ballots (match-any over the 8 digit bits) against
+//                      per-wave running digit counters, sorts the tile in LDS and writes
 //                      each digit run contiguously (coalesced) to its global offset
 //   bbox_finite        min/max of finite coordinates + finite count (grid sizing)
 #include "internal.h"
@@ -170,11 +170,18 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
     hist[(int64_t)d * nblocks + blockIdx.x] = (int32_t)c;
 }
 
+// Downsweep: wave w ranks the contiguous quarter [w*1024, (w+1)*1024) of the 4096-key tile in
+// 16 rounds of 64 keys (coalesced), so (wave, round, lane) order IS tile order and per-wave
+// running digit counters give stable ranks: per round, lanes with equal digits are matched by 8
+// ballots, the lowest such lane (the leader) bumps the wave's counter for that digit, and each
+// lane's rank = counter before the bump (read from its leader) + its rank among the matches.
+// Then per digit a 4-wave prefix and a block scan of the digit totals place every key in LDS
+// (tile sorted by digit), and each digit run is written coalesced to its global offset.
 struct DownsweepSmem {
-    uint16_t wcnt[kItems * kWaves][256];  // per (round, wave) digit counts -> prefixes
+    int32_t cnt[kWaves][256];  // per-wave digit counters -> wave offsets within a digit
     uint32_t keys[kTile];
     int32_t vals[kTile];
-    int32_t tile_start[256];
+    int32_t tile_start[257];
     int32_t gofs[256];
     int32_t wsum[kWaves];
 };
@@ -195,21 +202,19 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         }
         return;
     }
-
-    {  // zero the count table (32 KB): 8 x 16 B per thread
-        uint4* z = reinterpret_cast<uint4*>(&sm.wcnt[0][0]);
-        for (int k = t; k < (int)(sizeof(sm.wcnt) / 16); k += kBlock) z[k] = make_uint4(0, 0, 0, 0);
-    }
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) sm.cnt[k][t] = 0;
     __syncthreads();
 
     uint32_t k_r[kItems];
     int32_t v_r[kItems];
-    uint32_t dr[kItems];  // digit | (rank_in_wave << 16); digit 256 = invalid
+    uint32_t dr[kItems];  // digit | (rank within the wave's digit run << 8); 0xFFFFFFFF invalid
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t wbase = base + (int64_t)w * (kTile / kWaves);
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const int64_t i = base + r * kBlock + t;
-        const bool valid = i < n;
+        const int64_t i = wbase + r * 64 + lane;
+        const bool valid = i < base + tile_n;
         const uint32_t k = valid ? key[i] : kSentinelKey;
         const int32_t v = valid ? val[i] : 0;
         const uint32_t d = (k >> shift) & 255u;
@@ -220,22 +225,27 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
             const uint64_t bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t rk = (uint32_t)__popcll(peers & lt_mask);
-        if (valid && rk == 0) sm.wcnt[r * kWaves + w][d] = (uint16_t)__popcll(peers);
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        int old = 0;
+        if (valid && lane == leader) {
+            old = sm.cnt[w][d];
+            sm.cnt[w][d] = old + __popcll(peers);
+        }
+        old = __shfl(old, leader, 64);
         k_r[r] = k;
         v_r[r] = v;
-        dr[r] = valid ? (d | (rk << 16)) : 256u;
+        dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 8)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    {  // per digit: exclusive prefix over (round, wave) slots in tile order
+    {  // per digit t: wave offsets (prefix over the 4 waves) and the digit's tile total
         int running = 0;
-        for (int sidx = 0; sidx < kItems * kWaves; ++sidx) {
-            const int c = sm.wcnt[sidx][t];
-            sm.wcnt[sidx][t] = (uint16_t)running;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) {
+            const int c = sm.cnt[k][t];
+            sm.cnt[k][t] = running;
             running += c;
         }
-        // block exclusive scan of the tile digit counts -> tile_start
-        const int incl = wave_incl_scan(running);
+        const int incl = wave_incl_scan(running);  // block exclusive scan of the totals
         if (lane == 63) sm.wsum[w] = incl;
         __syncthreads();
         int woff = 0;
@@ -246,9 +256,9 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const uint32_t d = dr[r] & 0xFFFFu;
-        if (d < 256u) {
-            const int lpos = sm.tile_start[d] + sm.wcnt[r * kWaves + w][d] + (int)(dr[r] >> 16);
+        if (dr[r] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[r] & 255u;
+            const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 8);
             sm.keys[lpos] = k_r[r];
             sm.vals[lpos] = v_r[r];
         }
