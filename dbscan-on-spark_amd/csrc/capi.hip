@@ -385,6 +385,22 @@ int32_t dbscan_fit(const double* x, const double* y, int64_t n, double eps, int3
                         flag_out, n_clusters_out);
 }
 
+int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double eps,
+                          int32_t min_points, int32_t mode, int32_t n_shards,
+                          int32_t* cluster_out, uint8_t* flag_out, int64_t* n_clusters_out) {
+    return guarded(nullptr, [&]() -> int32_t {
+        check_fit_args(n, eps, mode, x, y, cluster_out, flag_out);
+        if (!n_clusters_out) throw dbscan::ArgError{"NULL n_clusters_out"};
+        *n_clusters_out = 0;
+        if (n == 0) return DBSCAN_OK;
+        std::string err;
+        const int32_t rc = dbscan::train_node(x, y, n, eps, min_points, mode, n_shards,
+                                              cluster_out, flag_out, n_clusters_out, &err);
+        if (rc != DBSCAN_OK) set_err(err);
+        return rc;
+    });
+}
+
 int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
                                int32_t min_points, uint8_t* d_core, int32_t* d_root) {

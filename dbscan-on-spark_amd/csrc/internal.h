@@ -181,6 +181,10 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
                     const int64_t* all_roots, int64_t n_roots, int32_t mode, int32_t* cluster,
                     uint8_t* flag);
+// Whole-node fit in one process (node.hip): n_shards slabs over the visible GPUs.
+int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
+                   int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
+                   int64_t* n_clusters_out, std::string* err);
 // Node-path merge (merge.hip): every local root's global s(K) (gs_of_root, slab index) and the
 // zone-0 global roots owned here, compacted in slab (= gid) order; returns their count (syncs).
 int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,

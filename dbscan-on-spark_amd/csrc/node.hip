@@ -1,0 +1,334 @@
+// node.hip -- dbscan_train_node: the whole-node entry of SURVEY.md §8b, one process driving
+// every GPU of the node.  The C++ twin of dbscan_amd/node.py (which runs one process per GPU
+// over RCCL); the same slab plan, the same exact merge:
+//   DBSCAN.scala:91-137    partition the plane, grow partitions by eps, duplicate points
+//                          -> n_shards x-slabs at count quantiles snapped to the 2*eps grid,
+//                             each with its 2-zone halo (node.py: make_cuts, zones)
+//   DBSCAN.scala:150-155   LocalDBSCANNaive.fit per partition
+//                          -> dbscan_slab_fit_device per shard, one host thread and one handle
+//                             (HIP stream) per shard, shard s on device s % device_count
+//   DBSCAN.scala:158-222   band points, findAdjacencies, DBSCANGraph, global ids
+//                          -> records (gid of a shared core, gid of its local root) merged by a
+//                             host union-find (the records are a thin band: O(1e5) at 1e8 pts),
+//                             global s(K) per local root, cluster id = rank of s(K)
+//   DBSCAN.scala:232-270   relabel                  -> dbscan_slab_label_device per shard
+// The result equals ONE fit of all points, bit for bit.
+#include "../../include/dbscan_hip.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace dbscan {
+namespace {
+
+constexpr uint8_t kOut = 255;
+
+double reach(double eps) { return std::max(std::fabs(eps) * (1.0 + 0x1p-40), 0x1p-500); }
+double ulp(double c) {
+    c = std::fabs(c);
+    return std::nextafter(c, INFINITY) - c;
+}
+double margin1(double c, double R) { return R * (1.0 + 0x1p-10) + 16.0 * ulp(c); }
+double margin2(double c, double R) { return 2.0 * margin1(c, R) + 16.0 * ulp(c); }
+
+// node.py make_cuts: world-1 cuts at count quantiles of a strided sample of the finite x,
+// snapped down to the 2*eps grid, non-decreasing.
+std::vector<double> make_cuts(const double* x, int64_t n, int world, double eps) {
+    std::vector<double> cuts;
+    if (world <= 1 || !std::isfinite(eps * eps)) return cuts;
+    std::vector<double> xf;
+    int64_t nfin = 0;
+    for (int64_t i = 0; i < n; ++i) nfin += std::isfinite(x[i]) ? 1 : 0;
+    if (nfin == 0) return cuts;
+    const int64_t step = std::max<int64_t>(1, nfin / (1 << 20));
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (std::isfinite(x[i])) {
+            if (k % step == 0) xf.push_back(x[i]);
+            ++k;
+        }
+    std::sort(xf.begin(), xf.end());
+    const double grid = 2.0 * std::fabs(eps);
+    const int64_t m = (int64_t)xf.size();
+    for (int r = 1; r < world; ++r) {
+        const double q = xf[std::min<int64_t>(m - 1, r * m / world)];
+        double c = (grid > 0 && std::isfinite(q / grid)) ? std::floor(q / grid) * grid : q;
+        if (!cuts.empty() && c < cuts.back()) c = cuts.back();
+        cuts.push_back(c);
+    }
+    return cuts;
+}
+
+struct Shard {
+    std::vector<int64_t> gid;  // slab points, increasing global visit index
+    std::vector<double> x, y;
+    std::vector<uint8_t> zone;
+    std::vector<int32_t> shared;  // slab indices of points in zones 0/1 of another shard too
+    std::vector<int32_t> root;    // slab fit output (-1: not core)
+    std::vector<int64_t> gs;      // global s(K) per local root
+    std::vector<int32_t> cluster;
+    std::vector<uint8_t> flag;
+    dbscan_handle* h = nullptr;
+    std::string err;
+    int32_t rc = DBSCAN_OK;
+};
+
+// node.py zones(): zone of x for shard r (0 owned, 1 inner halo, 2 outer halo, kOut) and
+// whether the point is shared (in zone 0/1 of an adjacent shard as well).
+uint8_t zone_of(double x, int r, int world, const std::vector<double>& cuts, double R,
+                bool* shared) {
+    const bool has_lo = r > 0, has_hi = r < world - 1;
+    const double lo = has_lo ? cuts[r - 1] : 0.0, hi = has_hi ? cuts[r] : 0.0;
+    bool own = (!has_lo || x >= lo) && (!has_hi || x < hi);
+    if (r == 0 && world > 1 && std::isnan(x)) own = true;
+    bool in1 = false, in2 = false, sh = false;
+    if (has_lo) {
+        const double m1 = margin1(lo, R), m2 = margin2(lo, R);
+        in1 = in1 || (x >= lo - m1 && x < lo);
+        in2 = in2 || (x >= lo - m2 && x < lo - m1);
+        sh = sh || (own && x <= lo + m1);
+    }
+    if (has_hi) {
+        const double m1 = margin1(hi, R), m2 = margin2(hi, R);
+        in1 = in1 || (x >= hi && x <= hi + m1);
+        in2 = in2 || (x > hi + m1 && x <= hi + m2);
+        sh = sh || (own && x >= hi - m1);
+    }
+    const uint8_t z = own ? 0 : (in1 ? 1 : (in2 ? 2 : kOut));
+    *shared = sh || z == 1;
+    return z;
+}
+
+// Phase 1 of one shard on its own handle/device: upload, slab fit, root back to the host.
+void shard_fit(Shard& s, int device, double eps, int32_t min_points) {
+    s.h = dbscan_create(device);
+    if (!s.h) {
+        s.rc = DBSCAN_EHIP;
+        s.err = dbscan_last_error();
+        return;
+    }
+    const int64_t m = (int64_t)s.gid.size();
+    s.root.assign(m, -1);
+    if (m == 0) return;
+    double *dx = nullptr, *dy = nullptr;
+    uint8_t *dz = nullptr, *dcore = nullptr;
+    int32_t* droot = nullptr;
+    auto fail = [&](hipError_t e, const char* what) {
+        s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
+        s.err = std::string(what) + ": " + hipGetErrorString(e);
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&dx, m * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&dy, m * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&dz, m);
+    if (e == hipSuccess) e = hipMalloc(&dcore, m);
+    if (e == hipSuccess) e = hipMalloc(&droot, m * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(dx, s.x.data(), m * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dy, s.y.data(), m * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dz, s.zone.data(), m, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        fail(e, "shard upload");
+    } else {
+        s.rc = dbscan_slab_fit_device(s.h, dx, dy, dz, m, eps, min_points, dcore, droot);
+        if (s.rc != DBSCAN_OK) {
+            s.err = dbscan_last_error();
+        } else {
+            e = hipMemcpy(s.root.data(), droot, m * sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) fail(e, "shard download");
+        }
+    }
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    (void)hipFree(dz);
+    (void)hipFree(dcore);
+    (void)hipFree(droot);
+}
+
+// Phase 2: labels of the shard's zone-0 points from the merged component ids.
+void shard_label(Shard& s, int device, const std::vector<int64_t>& all_roots, int32_t mode) {
+    const int64_t m = (int64_t)s.gid.size();
+    s.cluster.assign(m, 0);
+    s.flag.assign(m, DBSCAN_FLAG_NOT_FLAGGED);
+    if (m == 0) return;
+    uint8_t *dz = nullptr, *dfl = nullptr;
+    int64_t *dgid = nullptr, *dgs = nullptr, *droots = nullptr;
+    int32_t* dcl = nullptr;
+    const int64_t nr = (int64_t)all_roots.size();
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&dz, m);
+    if (e == hipSuccess) e = hipMalloc(&dfl, m);
+    if (e == hipSuccess) e = hipMalloc(&dgid, m * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMalloc(&dgs, m * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMalloc(&droots, std::max<int64_t>(1, nr) * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMalloc(&dcl, m * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(dz, s.zone.data(), m, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgid, s.gid.data(), m * sizeof(int64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dgs, s.gs.data(), m * sizeof(int64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nr > 0)
+        e = hipMemcpy(droots, all_roots.data(), nr * sizeof(int64_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dcl, s.cluster.data(), m * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dfl, s.flag.data(), m, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
+        s.err = std::string("shard label upload: ") + hipGetErrorString(e);
+    } else {
+        s.rc = dbscan_slab_label_device(s.h, dz, dgid, dgs, droots, nr, mode, dcl, dfl);
+        if (s.rc != DBSCAN_OK) {
+            s.err = dbscan_last_error();
+        } else {
+            e = hipMemcpy(s.cluster.data(), dcl, m * sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(s.flag.data(), dfl, m, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                s.rc = DBSCAN_EHIP;
+                s.err = std::string("shard label download: ") + hipGetErrorString(e);
+            }
+        }
+    }
+    for (void* p : {(void*)dz, (void*)dfl, (void*)dgid, (void*)dgs, (void*)droots, (void*)dcl})
+        (void)hipFree(p);
+}
+
+// Min-root union-find over global visit indices (host; the records are few).
+struct GidUnion {
+    std::unordered_map<int64_t, int64_t> up;
+    int64_t find(int64_t v) {
+        auto it = up.find(v);
+        if (it == up.end()) return v;
+        int64_t r = v;
+        while (true) {
+            auto jt = up.find(r);
+            if (jt == up.end() || jt->second == r) break;
+            r = jt->second;
+        }
+        while (v != r) {  // compress
+            int64_t& nx = up[v];
+            const int64_t t = nx;
+            nx = r;
+            v = t;
+        }
+        return r;
+    }
+    void unite(int64_t a, int64_t b) {
+        a = find(a);
+        b = find(b);
+        if (a == b) return;
+        if (a < b) std::swap(a, b);
+        up[a] = b;  // the larger index hangs under the smaller: a root is s(K)
+        up.emplace(b, b);
+    }
+};
+
+}  // namespace
+
+int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
+                   int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
+                   int64_t* n_clusters_out, std::string* err) {
+    const int ndev = dbscan_device_count();
+    if (ndev <= 0) {
+        *err = "no HIP device visible";
+        return DBSCAN_EHIP;
+    }
+    if (n_shards <= 0) n_shards = ndev;
+    const std::vector<double> cuts = make_cuts(x, n, n_shards, eps);
+    if (cuts.empty()) {  // one slab (or eps*eps not finite: all-pairs / no-pairs do not shard)
+        dbscan_handle* h = dbscan_create(0);
+        if (!h) {
+            *err = dbscan_last_error();
+            return DBSCAN_EHIP;
+        }
+        int32_t k = 0;
+        const int32_t rc = dbscan_fit_h(h, x, y, n, eps, min_points, mode, cluster_out, flag_out, &k);
+        if (rc != DBSCAN_OK) *err = dbscan_last_error();
+        dbscan_destroy(h);
+        *n_clusters_out = k;
+        return rc;
+    }
+    const int world = (int)cuts.size() + 1;
+    const double R = reach(eps);
+    std::vector<Shard> sh(world);
+    for (int64_t i = 0; i < n; ++i) {  // slab plan: points in increasing global visit order
+        // only the owner and shards whose halo can reach x need a look: scan neighbours of the
+        // owner until both directions fall out of reach
+        const int own = std::isnan(x[i])  // NaN x is owned by shard 0 (node.py zones)
+                            ? 0
+                            : (int)(std::upper_bound(cuts.begin(), cuts.end(), x[i]) -
+                                    cuts.begin());
+        for (int dir = -1; dir <= 1; dir += 2) {
+            for (int r = (dir < 0 ? own : own + 1); r >= 0 && r < world; r += dir) {
+                bool shared = false;
+                const uint8_t z = zone_of(x[i], r, world, cuts, R, &shared);
+                if (z == kOut) {
+                    if (r != own) break;
+                    continue;
+                }
+                Shard& s = sh[r];
+                if (shared) s.shared.push_back((int32_t)s.gid.size());
+                s.gid.push_back(i);
+                s.x.push_back(x[i]);
+                s.y.push_back(y[i]);
+                s.zone.push_back(z);
+            }
+        }
+    }
+    {
+        std::vector<std::thread> th;
+        for (int r = 0; r < world; ++r)
+            th.emplace_back(shard_fit, std::ref(sh[r]), r % ndev, eps, min_points);
+        for (auto& t : th) t.join();
+    }
+    int32_t rc = DBSCAN_OK;
+    for (auto& s : sh)
+        if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
+            rc = s.rc;
+            *err = s.err;
+        }
+    std::vector<int64_t> all_roots;
+    if (rc == DBSCAN_OK) {
+        GidUnion uf;  // records: shared core point -- its local root
+        for (auto& s : sh)
+            for (int32_t p : s.shared) {
+                const int32_t r = s.root[p];
+                if (r >= 0) uf.unite(s.gid[p], s.gid[r]);
+            }
+        for (auto& s : sh) {
+            const int64_t m = (int64_t)s.gid.size();
+            s.gs.assign(m, 0);
+            for (int64_t p = 0; p < m; ++p)
+                if (s.root[p] == (int32_t)p) {
+                    const int64_t g = s.gid[p], gs = uf.find(g);
+                    s.gs[p] = gs;
+                    if (s.zone[p] == 0 && gs == g) all_roots.push_back(g);
+                }
+        }
+        std::sort(all_roots.begin(), all_roots.end());
+        std::vector<std::thread> th;
+        for (int r = 0; r < world; ++r)
+            th.emplace_back(shard_label, std::ref(sh[r]), r % ndev, std::cref(all_roots), mode);
+        for (auto& t : th) t.join();
+        for (auto& s : sh)
+            if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
+                rc = s.rc;
+                *err = s.err;
+            }
+    }
+    if (rc == DBSCAN_OK) {
+        for (auto& s : sh)
+            for (size_t p = 0; p < s.gid.size(); ++p)
+                if (s.zone[p] == 0) {
+                    cluster_out[s.gid[p]] = s.cluster[p];
+                    flag_out[s.gid[p]] = s.flag[p];
+                }
+        *n_clusters_out = (int64_t)all_roots.size();
+    }
+    for (auto& s : sh)
+        if (s.h) dbscan_destroy(s.h);
+    return rc;
+}
+
+}  // namespace dbscan

@@ -6,4 +6,4 @@ in include/dbscan_hip.h); this package is the host-side mirror of the reference 
 """
 from ._lib import (DBSCANError, Handle, MODE_ARCHERY, MODE_NAIVE, LIB_PATH, load)  # noqa: F401
 from .local import (DBSCANLabeledPoint, DBSCANPoint, Flag, LocalDBSCANArchery,  # noqa: F401
-                    LocalDBSCANNaive, Unknown, fit_arrays)
+                    LocalDBSCANNaive, Unknown, fit_arrays, train_node)

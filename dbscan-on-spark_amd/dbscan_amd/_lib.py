@@ -36,6 +36,7 @@ SIGNATURES = [
     ("dbscan_profile_enable", _i32, [_vp, _i32]),
     ("dbscan_profile_reset", _i32, [_vp]),
     ("dbscan_profile_read", _i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
+    ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     ("dbscan_merge_union_device", _i32, [_vp, _vp, _i64, _vp, _vp]),

@@ -104,6 +104,26 @@ def fit_arrays(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
     return cl, fl, int(k.value)
 
 
+def train_node(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
+               n_shards: int = 0) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Whole-node fit of host arrays in one process (dbscan_train_node): n_shards x-slabs over
+    the visible GPUs (0: one per GPU), merged exactly -- the result equals one fit of all
+    points.  The DBSCAN.train(...).labeledPoints of DBSCAN.scala:91-283 for one node."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    if x.shape != y.shape or x.ndim != 1:
+        raise ValueError("x and y must be 1-D arrays of equal length")
+    n = x.size
+    cl = np.zeros(n, np.int32)
+    fl = np.zeros(n, np.uint8)
+    k = ctypes.c_int64(0)
+    _lib.check(_lib.load().dbscan_train_node(
+        x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p), n, float(eps),
+        int(min_points), int(mode), int(n_shards), cl.ctypes.data_as(ctypes.c_void_p),
+        fl.ctypes.data_as(ctypes.c_void_p), ctypes.byref(k)))
+    return cl, fl, int(k.value)
+
+
 class _LocalDBSCAN:
     _mode = _lib.MODE_NAIVE
 

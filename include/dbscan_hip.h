@@ -118,6 +118,18 @@ int32_t dbscan_profile_reset(dbscan_handle* h);
 int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, double* total_ms,
                             int64_t* launches, int32_t max);
 
+/* Whole-node entry: DBSCAN.train(points, eps, minPoints, ...).labeledPoints
+ * (DBSCAN.scala:91-283) for one node, from host arrays, in ONE process.  The points are cut
+ * into n_shards x-slabs at count quantiles snapped to the 2*eps grid (n_shards <= 0: one per
+ * visible GPU; shard s runs on device s % device_count, each with its own stream), every slab
+ * is fitted with its eps halos, and the slabs are merged exactly: the outputs equal one
+ * LocalDBSCANNaive / LocalDBSCANArchery fit of all n points in input order, global cluster ids
+ * 1..k (0 = Noise) -- not the reference merge's approximations.  The
+ * multi-process form of the same plan is dbscan_amd/node.py (one rank per GPU, RCCL). */
+int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double eps,
+                          int32_t min_points, int32_t mode, int32_t n_shards,
+                          int32_t* cluster_out, uint8_t* flag_out, int64_t* n_clusters_out);
+
 /* ---------------------------------------------------------------------------------------
  * Slab fits for the multi-GPU node path (dbscan_amd/node.py).  The caller
  * passes the points of one spatial slab grown by halos, in increasing global visit order, with

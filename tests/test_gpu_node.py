@@ -77,3 +77,44 @@ def test_gpu_merge_kernels_vs_double():
         ops.merge_reset(ta, tb, par)
         assert bool((par == -1).all())
     h.close()
+
+
+@pytest.mark.parametrize("shards,mode,noise,bad", [(2, 0, 0.2, 0), (3, 1, 0.1, 40), (4, 0, 0.0, 0),
+                                                    (7, 0, 0.3, 10)])
+def test_train_node_single_process(shards, mode, noise, bad):
+    """dbscan_train_node (one process, n_shards slabs on the visible GPUs -- here all on one):
+    the global labels equal one fit of the whole set, bit for bit, NaN/inf points included."""
+    import dbscan_amd
+
+    n = 300_000
+    x, y = gen_blobs(n, noise=noise, seed=shards * 7 + mode)
+    if bad:
+        rng = np.random.default_rng(bad)
+        idx = rng.choice(n, bad, replace=False)
+        x[idx[: bad // 2]] = np.nan
+        y[idx[bad // 2:]] = -np.inf
+    cl, fl, k = dbscan_amd.train_node(x, y, 2.55, 10, mode, shards)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, mode)
+    assert k == rk
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+
+
+def test_train_node_unshardable_and_labeled_csv(labeled_data):
+    """eps*eps = +inf (all pairs) falls back to one fit; the reference's csv through the node
+    entry equals the local fit (DBSCANSuite, maxPointsPerPartition small -> several slabs)."""
+    import dbscan_amd
+    from conftest import EPS_03F
+
+    x, y, _ = labeled_data
+    cl, fl, k = dbscan_amd.train_node(x, y, EPS_03F, 10, 0, 4)
+    rc, rf, rk = O.fit_sequential(x, y, EPS_03F, 10, 0)
+    assert k == rk == 3
+    np.testing.assert_array_equal(cl, rc)
+    np.testing.assert_array_equal(fl, rf)
+    xs, ys = gen_blobs(2000, seed=9)
+    cl, fl, k = dbscan_amd.train_node(xs, ys, 1e200, 5, 1, 3)
+    rc, rf, rk = O.fit_grid(xs, ys, 1e200, 5, 1)
+    assert k == rk
+    np.testing.assert_array_equal(cl, rc)
+    np.testing.assert_array_equal(fl, rf)
