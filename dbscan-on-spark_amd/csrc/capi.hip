@@ -401,6 +401,100 @@ int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double ep
     });
 }
 
+}  // extern "C"
+
+namespace {
+// Partitions to the caller's buffers: (x, y, x2, y2) quadruples + counts, at most max_parts;
+// returns the full count.
+int64_t emit_partitions(const std::vector<dbscan::Partition>& parts, double* rects_out,
+                        int64_t* counts_out, int64_t max_parts) {
+    const int64_t k = (int64_t)parts.size();
+    for (int64_t i = 0; i < k && i < max_parts; ++i) {
+        rects_out[4 * i + 0] = parts[i].x;
+        rects_out[4 * i + 1] = parts[i].y;
+        rects_out[4 * i + 2] = parts[i].x2;
+        rects_out[4 * i + 3] = parts[i].y2;
+        counts_out[i] = parts[i].count;
+    }
+    return k;
+}
+
+template <class F>
+int64_t guarded64(dbscan_handle* h, F&& f) {
+    int64_t r = 0;
+    const int32_t rc = guarded(h, [&]() -> int32_t {
+        r = f();
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? r : (int64_t)rc;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t dbscan_partition_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
+                                double eps, int64_t max_points_per_partition, double* rects_out,
+                                int64_t* counts_out, int64_t max_parts) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded64(h, [&]() -> int64_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
+        if (n < 0 || max_parts < 0 || (n > 0 && (!d_x || !d_y)) ||
+            (max_parts > 0 && (!rects_out || !counts_out)))
+            throw dbscan::ArgError{"bad partition arguments"};
+        std::vector<dbscan::Partition> parts;
+        dbscan::run_partition(h->stream, h->ws, d_x, d_y, n, eps, max_points_per_partition,
+                              &parts);
+        return emit_partitions(parts, rects_out, counts_out, max_parts);
+    });
+}
+
+int64_t dbscan_partition(dbscan_handle* h, const double* x, const double* y, int64_t n,
+                         double eps, int64_t max_points_per_partition, double* rects_out,
+                         int64_t* counts_out, int64_t max_parts) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded64(h, [&]() -> int64_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
+        if (n < 0 || max_parts < 0 || (n > 0 && (!x || !y)) ||
+            (max_parts > 0 && (!rects_out || !counts_out)))
+            throw dbscan::ArgError{"bad partition arguments"};
+        std::vector<dbscan::Partition> parts;
+        if (n > 0) {
+            double* dx = static_cast<double*>(h->hx.ensure(n * sizeof(double)));
+            double* dy = static_cast<double*>(h->hy.ensure(n * sizeof(double)));
+            DBSCAN_HIP_CHECK(
+                hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            DBSCAN_HIP_CHECK(
+                hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            dbscan::run_partition(h->stream, h->ws, dx, dy, n, eps, max_points_per_partition,
+                                  &parts);
+        }
+        return emit_partitions(parts, rects_out, counts_out, max_parts);
+    });
+}
+
+int64_t dbscan_partition_cells(const double* cell_x, const double* cell_y,
+                               const int64_t* cell_counts, int64_t ncells,
+                               int64_t max_points_per_partition, double min_rect_size,
+                               double* rects_out, int64_t* counts_out, int64_t max_parts) {
+    return guarded64(nullptr, [&]() -> int64_t {
+        if (ncells < 0 || max_parts < 0 || (ncells > 0 && (!cell_x || !cell_y || !cell_counts)) ||
+            (max_parts > 0 && (!rects_out || !counts_out)) || !(min_rect_size > 0))
+            throw dbscan::ArgError{"bad partition arguments"};
+        std::vector<dbscan::Partition> parts;
+        dbscan::partition_cells(cell_x, cell_y, cell_counts, ncells, max_points_per_partition,
+                                min_rect_size, &parts);
+        return emit_partitions(parts, rects_out, counts_out, max_parts);
+    });
+}
+
 int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
                                int32_t min_points, uint8_t* d_core, int32_t* d_root) {

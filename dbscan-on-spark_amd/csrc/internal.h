@@ -181,6 +181,22 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
                     const int64_t* all_roots, int64_t n_roots, int32_t mode, int32_t* cluster,
                     uint8_t* flag);
+// The reference's spatial partitioner (partition.hip): DBSCAN.scala:91-97 cell histogram on
+// the GPU, EvenSplitPartitioner.scala:44-209 splits on the host.
+constexpr double kMaxPartitionCells = 4e8;  // dense 2*eps cell window limit
+struct Partition {
+    double x, y, x2, y2;
+    int64_t count;
+};
+int64_t run_partition(hipStream_t s, Workspace& ws, const double* d_x, const double* d_y,
+                      int64_t n, double eps, int64_t max_points, std::vector<Partition>* out);
+int64_t partition_cells(const double* cell_x, const double* cell_y, const int64_t* counts,
+                        int64_t ncells, int64_t max_points, double mrs,
+                        std::vector<Partition>* out);
+int64_t split_partitions(double mrs, int64_t imin, int64_t jmin, int64_t W, int64_t H,
+                         const std::vector<uint32_t>& hist, int64_t max_points,
+                         std::vector<Partition>* out);
+
 // Whole-node fit in one process (node.hip): n_shards slabs over the visible GPUs.
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,

@@ -36,6 +36,9 @@ SIGNATURES = [
     ("dbscan_profile_enable", _i32, [_vp, _i32]),
     ("dbscan_profile_reset", _i32, [_vp]),
     ("dbscan_profile_read", _i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
+    ("dbscan_partition", _i64, [_vp, _vp, _vp, _i64, _d, _i64, _vp, _vp, _i64]),
+    ("dbscan_partition_device", _i64, [_vp, _vp, _vp, _i64, _d, _i64, _vp, _vp, _i64]),
+    ("dbscan_partition_cells", _i64, [_vp, _vp, _vp, _i64, _i64, _d, _vp, _vp, _i64]),
     ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),

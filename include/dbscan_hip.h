@@ -118,6 +118,31 @@ int32_t dbscan_profile_reset(dbscan_handle* h);
 int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, double* total_ms,
                             int64_t* launches, int32_t max);
 
+/* The reference's spatial partitioner: DBSCAN.scala:91-97 maps every point
+ * to its 2*eps cell (corner = (shiftIfNegative(p) / (2*eps)).intValue * 2*eps,
+ * DBSCAN.scala:345-356) and counts points per cell -- a histogram on the GPU here -- then
+ * EvenSplitPartitioner.partition(cells, maxPointsPerPartition, 2*eps)
+ * (EvenSplitPartitioner.scala:44-209) splits the bounding rectangle until every partition holds
+ * at most maxPointsPerPartition points or cannot be split (host, summed-area table).
+ * Partitions are written as (x, y, x2, y2) quadruples + point counts in the reference's list
+ * order, at most max_parts of them; the return value is the full partition count (call again
+ * with a larger buffer if it exceeds max_parts) or a negative error code.  Exact fp semantics
+ * of the reference, including its split-line/cell-corner defect; equal-cost
+ * splits are broken by candidate order (x splits, then y), where the reference iterates a
+ * Scala HashSet.  dbscan_partition_cells is EvenSplitPartitioner.partition over an explicit
+ * cell set (cells given by lower corners on the min_rect_size grid), as
+ * EvenSplitPartitionerSuite calls it. */
+int64_t dbscan_partition(dbscan_handle* h, const double* x, const double* y, int64_t n,
+                         double eps, int64_t max_points_per_partition, double* rects_out,
+                         int64_t* counts_out, int64_t max_parts);
+int64_t dbscan_partition_device(dbscan_handle* h, const double* d_x, const double* d_y, int64_t n,
+                                double eps, int64_t max_points_per_partition, double* rects_out,
+                                int64_t* counts_out, int64_t max_parts);
+int64_t dbscan_partition_cells(const double* cell_x, const double* cell_y,
+                               const int64_t* cell_counts, int64_t ncells,
+                               int64_t max_points_per_partition, double min_rect_size,
+                               double* rects_out, int64_t* counts_out, int64_t max_parts);
+
 /* Whole-node entry: DBSCAN.train(points, eps, minPoints, ...).labeledPoints
  * (DBSCAN.scala:91-283) for one node, from host arrays, in ONE process.  The points are cut
  * into n_shards x-slabs at count quantiles snapped to the 2*eps grid (n_shards <= 0: one per
