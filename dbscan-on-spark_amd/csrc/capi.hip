@@ -495,6 +495,31 @@ int64_t dbscan_partition_cells(const double* cell_x, const double* cell_y,
     });
 }
 
+int64_t dbscan_csv_read(const char* path, double* x_out, double* y_out, int64_t capacity) {
+    return guarded64(nullptr, [&]() -> int64_t {
+        if (!path || capacity < 0 || ((x_out == nullptr) != (y_out == nullptr)))
+            throw dbscan::ArgError{"bad csv arguments"};
+        return dbscan::csv_read(path, x_out, y_out, capacity);
+    });
+}
+
+int32_t dbscan_csv_write(const char* path, const double* x, const double* y,
+                         const int32_t* cluster, int64_t n) {
+    return guarded(nullptr, [&]() -> int32_t {
+        if (!path || n < 0 || (n > 0 && (!x || !y || !cluster)))
+            throw dbscan::ArgError{"bad csv arguments"};
+        dbscan::csv_write(path, x, y, cluster, n);
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_format_double(double v, char* buf) {
+    if (!buf) return DBSCAN_EARG;
+    const int k = dbscan::java_double_string_c(v, buf);
+    buf[k] = 0;
+    return k;
+}
+
 int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,
                                const uint8_t* d_zone, int64_t n, double eps,
                                int32_t min_points, uint8_t* d_core, int32_t* d_root) {

@@ -197,6 +197,12 @@ int64_t split_partitions(double mrs, int64_t imin, int64_t jmin, int64_t W, int6
                          const std::vector<uint32_t>& hist, int64_t max_points,
                          std::vector<Partition>* out);
 
+// Text I/O of the reference (csv.hip): DBSCANSuite/DBSCANSample input and output formats.
+int64_t csv_read(const char* path, double* x_out, double* y_out, int64_t capacity);
+void csv_write(const char* path, const double* x, const double* y, const int32_t* cluster,
+               int64_t n);
+int java_double_string_c(double d, char* buf);
+
 // Whole-node fit in one process (node.hip): n_shards slabs over the visible GPUs.
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,

@@ -39,6 +39,9 @@ SIGNATURES = [
     ("dbscan_partition", _i64, [_vp, _vp, _vp, _i64, _d, _i64, _vp, _vp, _i64]),
     ("dbscan_partition_device", _i64, [_vp, _vp, _vp, _i64, _d, _i64, _vp, _vp, _i64]),
     ("dbscan_partition_cells", _i64, [_vp, _vp, _vp, _i64, _i64, _d, _vp, _vp, _i64]),
+    ("dbscan_csv_read", _i64, [ctypes.c_char_p, _vp, _vp, _i64]),
+    ("dbscan_csv_write", _i32, [ctypes.c_char_p, _vp, _vp, _vp, _i64]),
+    ("dbscan_format_double", _i32, [_d, ctypes.c_char_p]),
     ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),

@@ -143,6 +143,22 @@ int64_t dbscan_partition_cells(const double* cell_x, const double* cell_y,
                                int64_t max_points_per_partition, double min_rect_size,
                                double* rects_out, int64_t* counts_out, int64_t max_parts);
 
+/* Text I/O of the reference, host code.
+ * dbscan_csv_read: the input of DBSCANSuite.scala:31-33 / DBSCANSample.scala:21,
+ *   sc.textFile(path).map(s => Vectors.dense(s.split(',').map(_.toDouble))): one point per
+ *   line, every field a java.lang.Double.parseDouble number (trailing empty fields dropped, as
+ *   String.split does), x = field 0, y = field 1 (DBSCANPoint reads only those two; a label
+ *   column is parsed and ignored).  With x_out == y_out == NULL returns the record count;
+ *   otherwise fills up to `capacity` records and returns the count; a malformed record is
+ *   DBSCAN_EARG naming its 1-based line.  Memory-mapped, parsed by host threads.
+ * dbscan_csv_write: the output of DBSCANSample.scala:35, "x,y,cluster" per point with x and y
+ *   in java.lang.Double.toString form (dbscan_format_double; buf >= 32 bytes, returns the
+ *   length): shortest round-trip digits, plain for 1e-3 <= |v| < 1e7, else d.dddE[-]n. */
+int64_t dbscan_csv_read(const char* path, double* x_out, double* y_out, int64_t capacity);
+int32_t dbscan_csv_write(const char* path, const double* x, const double* y,
+                         const int32_t* cluster, int64_t n);
+int32_t dbscan_format_double(double v, char* buf);
+
 /* Whole-node entry: DBSCAN.train(points, eps, minPoints, ...).labeledPoints
  * (DBSCAN.scala:91-283) for one node, from host arrays, in ONE process.  The points are cut
  * into n_shards x-slabs at count quantiles snapped to the 2*eps grid (n_shards <= 0: one per
