@@ -540,6 +540,27 @@ int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double
     });
 }
 
+int32_t dbscan_slab_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                     const uint8_t* d_zone, int64_t n, double eps,
+                                     int32_t min_points, uint8_t* d_core, int32_t* d_root) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, DBSCAN_MODE_NAIVE, d_x, d_y, d_core, d_root);
+        if (n > 0 && !d_zone) throw dbscan::ArgError{"NULL zone pointer"};
+        if (h->pending && h->prof.pending.size() > 4096) settle(h);
+        h->pending = false;
+        dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
+                          nullptr, d_core, d_root};
+        dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+        h->pending = true;
+        return DBSCAN_OK;
+    });
+}
+
 int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
                                        const int64_t* d_gid, const int32_t* d_root,
                                        const int32_t* d_parent, int64_t* d_gs_of_root,
@@ -560,17 +581,16 @@ int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_
     });
 }
 
-int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
-                                 const int64_t* d_gs_of_root, const int64_t* d_all_roots,
-                                 int64_t n_all_roots, int32_t mode, int32_t* d_cluster,
-                                 uint8_t* d_flag) {
+namespace {
+int32_t slab_label(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                   const int64_t* d_gs_of_root, const int64_t* d_all_roots, int64_t n_all_roots,
+                   int32_t mode, int32_t* d_cluster, uint8_t* d_flag, bool sync) {
     if (!h) {
         set_err("NULL handle");
         return DBSCAN_EARG;
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
-        settle(h);
         if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
             throw dbscan::ArgError{"bad mode"};
         if (n_all_roots < 0) throw dbscan::ArgError{"n_all_roots < 0"};
@@ -579,9 +599,30 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
             throw dbscan::ArgError{"NULL array pointer"};
         dbscan::run_slab_label(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gid, d_gs_of_root,
                                d_all_roots, n_all_roots, mode, d_cluster, d_flag);
-        h->prof.flush();
+        if (sync) {
+            DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+            settle(h);
+            h->prof.flush();
+        }
         return DBSCAN_OK;
     });
+}
+}  // namespace
+
+int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                                 const int64_t* d_gs_of_root, const int64_t* d_all_roots,
+                                 int64_t n_all_roots, int32_t mode, int32_t* d_cluster,
+                                 uint8_t* d_flag) {
+    return slab_label(h, d_zone, d_gid, d_gs_of_root, d_all_roots, n_all_roots, mode, d_cluster,
+                      d_flag, true);
+}
+
+int32_t dbscan_slab_label_device_async(dbscan_handle* h, const uint8_t* d_zone,
+                                       const int64_t* d_gid, const int64_t* d_gs_of_root,
+                                       const int64_t* d_all_roots, int64_t n_all_roots,
+                                       int32_t mode, int32_t* d_cluster, uint8_t* d_flag) {
+    return slab_label(h, d_zone, d_gid, d_gs_of_root, d_all_roots, n_all_roots, mode, d_cluster,
+                      d_flag, false);
 }
 
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {

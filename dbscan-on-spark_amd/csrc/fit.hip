@@ -1784,7 +1784,6 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     hipLaunchKernelGGL(permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace dbscan

@@ -159,17 +159,36 @@ class Comm:
 
 
 class HipSlabOps:
-    """The product slab fit and merge: libdbscan_hip.so through device tensors (the merge
-    kernels run on torch's current stream)."""
+    """The product slab fit and merge: libdbscan_hip.so through device tensors.  The slab fit
+    and label run asynchronously on the handle's stream, ordered against torch's current stream
+    by stream waits (no host synchronization); the merge kernels run on torch's stream.  A step
+    synchronizes the host only for the owned-root count and the all-gather sizes."""
 
     def __init__(self, handle: _lib.Handle):
         self.h = handle
+        self._hs = torch.cuda.ExternalStream(handle.stream,
+                                             device=torch.device("cuda", handle.device))
+        self._out = None
         self._bufs = None
 
-    def fit(self, x, y, zone, eps, min_points):
-        from . import device as D
+    def _to_handle(self):
+        self._hs.wait_stream(torch.cuda.current_stream())
 
-        return D.slab_fit(x, y, zone, eps, min_points, self.h)
+    def _from_handle(self):
+        torch.cuda.current_stream().wait_stream(self._hs)
+
+    def fit(self, x, y, zone, eps, min_points):
+        n = x.numel()
+        if self._out is None or self._out[0].numel() != n:
+            self._out = (torch.empty(n, dtype=torch.uint8, device=x.device),
+                         torch.empty(n, dtype=torch.int32, device=x.device))
+        core, root = self._out
+        self._to_handle()
+        _lib.check(_lib.load().dbscan_slab_fit_device_async(
+            self.h.ptr, _p(x), _p(y), _p(zone), n, float(eps), int(min_points), _p(core),
+            _p(root)))
+        self._from_handle()
+        return core, root
 
     @staticmethod
     def _stream():
@@ -184,18 +203,27 @@ class HipSlabOps:
                                                          self._stream()))
 
     def merge_roots(self, zone, gid, root, parent, gs_of_root):
-        from . import device as D
-
         n = zone.numel()
         if self._bufs is None or self._bufs.numel() < max(1, n):
             self._bufs = torch.empty(max(1, n), dtype=torch.int64, device=zone.device)
-        k = D.slab_merge_roots(zone, gid, root, parent, gs_of_root, self._bufs, self.h)
-        return self._bufs[:k]
+        k = ctypes.c_int64(0)
+        self._to_handle()
+        _lib.check(_lib.load().dbscan_slab_merge_roots_device(
+            self.h.ptr, n, _p(zone), _p(gid), _p(root), _p(parent), _p(gs_of_root),
+            _p(self._bufs), ctypes.byref(k)))  # synchronizes the handle stream (the count)
+        return self._bufs[:int(k.value)]
 
     def label(self, zone, gid, gs_of_root, all_roots, mode):
-        from . import device as D
-
-        return D.slab_label(zone, gid, gs_of_root, all_roots, mode, self.h)
+        n = zone.numel()
+        cluster = torch.zeros(n, dtype=torch.int32, device=zone.device)
+        flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
+        all_roots = all_roots.to(torch.int64).contiguous()
+        self._to_handle()
+        _lib.check(_lib.load().dbscan_slab_label_device_async(
+            self.h.ptr, _p(zone), _p(gid), _p(gs_of_root), _p(all_roots), all_roots.numel(),
+            int(mode), _p(cluster), _p(flag)))
+        self._from_handle()
+        return cluster, flag
 
 
 class NodeJob:

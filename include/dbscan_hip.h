@@ -197,6 +197,15 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
                                  const int64_t* d_gs_of_root, const int64_t* d_all_roots,
                                  int64_t n_all_roots, int32_t mode, int32_t* d_cluster,
                                  uint8_t* d_flag);
+/* The same two phases enqueued on the handle's stream without waiting (order the caller's own
+ * streams around dbscan_stream(h)); the fit's statistics settle at the next synchronizing call. */
+int32_t dbscan_slab_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                     const uint8_t* d_zone, int64_t n, double eps,
+                                     int32_t min_points, uint8_t* d_core, int32_t* d_root);
+int32_t dbscan_slab_label_device_async(dbscan_handle* h, const uint8_t* d_zone,
+                                       const int64_t* d_gid, const int64_t* d_gs_of_root,
+                                       const int64_t* d_all_roots, int64_t n_all_roots,
+                                       int32_t mode, int32_t* d_cluster, uint8_t* d_flag);
 
 /* Cross-slab merge of the node path (replaces DBSCAN.scala:158-222: band points,
  * findAdjacencies, DBSCANGraph components, global ids), enqueued on the CALLER's stream
