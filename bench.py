@@ -13,7 +13,9 @@ the host; the K steps are enqueued back to back and the timed region ends with o
 records + global union-find + relabel; per-GPU work is fixed (weak scaling).
 
 roofline: the dominant kernel of the timed region, timed with HIP events on the library's own
-stream; achieved = SURVEY §8d algorithmic bytes/point for that stage x points / avg duration.
+stream -- carried on the kernels' own dispatch packets (hipExtLaunchKernelGGL), so timing adds
+no idle gaps between kernels; achieved = algorithmic bytes per launch (SURVEY §8d per-point
+figure x points) / the kernel's average launch duration.
 cpu_baseline (rank 0, N = 1): the oracle's restatement of the reference path -- the
 EvenSplitPartitioner (maxPointsPerPartition = 8192) + LocalDBSCANNaive.fit O(m^2) per partition
 (oracle/reference_pipeline.c), on host threads, for a bounded time on the same points.
@@ -29,15 +31,17 @@ sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
 
 METRIC = "points clustered/sec (whole node) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# SURVEY.md §8d algorithmic bytes per point, by pipeline stage (each array crosses HBM once).
-# The §8d "union" (21 B) is split over the kernels that carry it: quarter_init
-# (core 1 + perm 4 + parent 4), union_tile (xy 16 + rep parent writes ~0), union_edge and
-# union_root (tile-edge strips and quarter reps only: ~0 per point).
+# Algorithmic bytes per point and launch, by kernel (SURVEY.md §8d's per-phase figures; each
+# array crosses HBM once): count 17 = sorted x,y 16 + core 1; the §8d union 21 is
+# carried by quarter_init (core 1 + perm 4 + parent 4) and tile_union (x,y 16; edge_union and
+# quarter_root touch tile-edge strips and quarter reps only); the §8d output 30 by final (13),
+# the rank scan and label_sorted/permute_out.  Radix passes: 4 launches per fit, each reading
+# key+perm 8 and writing 8.
 ALG_BYTES = {
-    "bbox": 16, "bin": 20, "sort_upsweep": 4, "sort_scan": 0, "sort_downsweep": 16,
-    "gather": 36, "cells": 8, "tables": 0, "segs": 0, "count": 17, "quarter_init": 9,
-    "union_tile": 16, "union_edge": 0, "union_root": 0, "union": 21, "final": 13, "rank": 5,
-    "output": 30,
+    "bbox_partial": 16, "bin": 20, "radix_upsweep": 4, "radix_downsweep": 16, "inverse": 8,
+    "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 17, "quarter_init": 9,
+    "tile_union": 16, "edge_union": 0, "quarter_root": 0, "final": 13, "label_sorted": 13,
+    "permute_out": 13,
 }
 PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
 
@@ -55,7 +59,9 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true", help="no per-stage events")
+    ap.add_argument("--no-profile", action="store_true", help="no kernel timing events")
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="untimed steps with every kernel timed (the breakdown)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--node", action="store_true", help="use the node path even at N = 1")
     return ap.parse_args()
@@ -144,8 +150,22 @@ def main():
     for _ in range(args.warmup):
         k = step()
     h.sync()
+    kernels, dom = {}, None
     if not args.no_profile:
-        h.profile(True)
+        # Per-kernel breakdown from a short profiled pass outside the timed region: events on
+        # every launch cost ~0.2 ms per fit of extra GPU time, so the timed region
+        # carries events on the dominant kernel's launches only.
+        h.profile(True, kernels=True)
+        h.profile_only(None)
+        h.profile_reset()
+        for _ in range(args.profile_steps):
+            step()
+        h.sync()
+        torch.cuda.synchronize()
+        kprof = h.profile_read()
+        kernels = {k2: v["ms"] / max(1, args.profile_steps) for k2, v in kprof.items()}
+        dom = max(kprof, key=lambda s: kprof[s]["ms"]) if kprof else None
+        h.profile_only(dom)
         h.profile_reset()
     if dist:
         dist.barrier()
@@ -171,14 +191,11 @@ def main():
 
     ms_per_step = el / args.steps * 1e3
     value = n_total * args.steps / el
-    stages = {k2: v["ms"] / max(1, args.steps) for k2, v in prof.items()}
     roof = None
-    if prof:
-        dom = max(prof, key=lambda s: prof[s]["ms"])
-        avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])
+    if prof and dom in prof:
+        avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])  # live, in the timed region
         pts = stats.get("n", args.points_per_gpu)
-        launches_per_step = prof[dom]["launches"] / max(1, args.steps)
-        alg = ALG_BYTES.get(dom, 0) * pts / max(1.0, launches_per_step)
+        alg = ALG_BYTES.get(dom, 0) * pts  # per launch
         achieved = alg / (avg_ms * 1e-3) / 1e9
         traffic = load_traffic(dom, pts) if (world == 1 and not args.node) else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -210,7 +227,11 @@ def main():
                 "occupied_cells": stats.get("cells"), "occupied_tiles": stats.get("tiles")},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "stages_ms_per_step": {k2: round(v, 4) for k2, v in stages.items()},
+            "kernels_ms_per_step": {k2: round(v, 4) for k2, v in
+                                    sorted(kernels.items(), key=lambda kv: -kv[1])},
+            "kernels_ms_note": (f"per-kernel event times from {args.profile_steps} untimed "
+                                "profiled steps; the timed steps carry events only on the "
+                                "roofline kernel"),
         }
         print(json.dumps(line), flush=True)
     if dist:

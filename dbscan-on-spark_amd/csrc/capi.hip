@@ -88,7 +88,7 @@ void Profiler::destroy() {
 }
 
 StageTimer::StageTimer(Profiler* p, hipStream_t st, const char* name) : prof(p), s(st) {
-    if (!prof || !prof->on) {
+    if (!prof || !prof->on || prof->mode != 1) {
         prof = nullptr;
         return;
     }
@@ -638,8 +638,15 @@ int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {
 }
 
 int32_t dbscan_profile_enable(dbscan_handle* h, int32_t on) {
-    if (!h) return DBSCAN_EARG;
+    if (!h || on < 0 || on > 2) return DBSCAN_EARG;
     h->prof.on = on != 0;
+    h->prof.mode = on;
+    return DBSCAN_OK;
+}
+
+int32_t dbscan_profile_only(dbscan_handle* h, const char* kernel) {
+    if (!h) return DBSCAN_EARG;
+    h->prof.only = kernel ? kernel : "";
     return DBSCAN_OK;
 }
 

@@ -1499,12 +1499,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "bbox");
             bbox_finite(s, a.x, a.y, n, misc, ws.scan_tmp);
-            hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
+            klaunch(prof, "grid", grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "bin");
-            hipLaunchKernelGGL(bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key,
+            klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key,
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
@@ -1513,9 +1513,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     } else {
         StageTimer t(prof, s, "bin");
         // all pairs: one cell holding every point, the predicate decides (incl. non-finite)
-        hipLaunchKernelGGL(grid_fixed_kernel, dim3(1), dim3(1), 0, s,
+        klaunch(prof, "grid_fixed", grid_fixed_kernel, dim3(1), dim3(1), 0, s,
                            mode == kGridAllPairs ? (int32_t)n : 0, gp, st);
-        hipLaunchKernelGGL(iota_key_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
+        klaunch(prof, "iota_key", iota_key_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
                            mode == kGridAllPairs ? 0u : kSentinelKey, key, perm);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
@@ -1550,9 +1550,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
 
     {
         StageTimer t(prof, s, "gather");
-        hipLaunchKernelGGL(inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, inv);
+        klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, inv);
         if (mode != kGridNoPairs)
-            hipLaunchKernelGGL(scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
+            klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
@@ -1563,30 +1563,30 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             int32_t* part =
                 static_cast<int32_t*>(ws.heads.ensure(6 * (size_t)nb * sizeof(int32_t)));
             int32_t* offs = part + 3 * nb;
-            hipLaunchKernelGGL(heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
+            klaunch(prof, "heads_reduce", heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                part);
             DBSCAN_HIP_CHECK(hipGetLastError());
             exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan_tmp);
             exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan_tmp);
             exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan_tmp);
-            hipLaunchKernelGGL(heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
+            klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "tables");
-            hipLaunchKernelGGL(tmap_clear_kernel, dim3(1024), dim3(kBlock), 0, s, gp, tmap);
+            klaunch(prof, "tmap_clear", tmap_clear_kernel, dim3(1024), dim3(kBlock), 0, s, gp, tmap);
             const unsigned tgrid = (unsigned)std::min<int64_t>(nblk(ntile_bound), 1024);
-            hipLaunchKernelGGL(tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
+            klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(tslot_kernel,
+            klaunch(prof, "tslot", tslot_kernel,
                                dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
                                dim3(kBlock),
                                0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
                                &st[kStCells], qidx, tmap, gp, tslot, tq, tnb);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            hipLaunchKernelGGL(tstage_kernel,
+            klaunch(prof, "tstage", tstage_kernel,
                                dim3((unsigned)std::min<int64_t>((ntile_bound + 1) / 2, kTileGrid)),
                                dim3(kBlock),
                                0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage);
@@ -1594,7 +1594,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         {
             StageTimer t(prof, s, "segs");
-            hipLaunchKernelGGL(segs_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, ckey, cstart,
+            klaunch(prof, "segs", segs_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, ckey, cstart,
                                &st[kStCells], tmap, tslot, gp, seg);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
@@ -1617,49 +1617,49 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 case 1024: kern = count_tile_kernel<1024>; break;
                 default: break;
             }
-            hipLaunchKernelGGL(kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
+            klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
                                tstage, &st[kStTiles], eps2, a.min_points, core,
                                parent, block_cores, nbr, nbr_k, count_ablate());
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
-        hipLaunchKernelGGL(count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
+        klaunch(prof, "count_rest", count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
                            a.min_points, core, parent, block_cores + tile_grid);
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = (int64_t)tile_grid + rest_grid;
         exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan_tmp);
         if (a.zone)  // (the core count above then includes zone-2 points: a statistic only)
-            hipLaunchKernelGGL(zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
+            klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
                                core);
     }
     if (mode == kGridEps) {  // quarter-cell unions (no-ops unless the grid made them cliques)
         {
             StageTimer t(prof, s, "quarter_init");
-            hipLaunchKernelGGL(quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
+            klaunch(prof, "quarter_init", quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
                                qkey, &st[kStQuarters], gp, perm, core, qinfo, qg, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_tile");
-            hipLaunchKernelGGL(tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
+            klaunch(prof, "tile_union", tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
                                &st[kStTiles], qinfo, qg, eps2, perm, core, parent, qcomp, gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_edge");
-            hipLaunchKernelGGL(edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
+            klaunch(prof, "edge_union", edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
                                &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent,
                                gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
-        hipLaunchKernelGGL(quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
+        klaunch(prof, "quarter_root", quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
                            &st[kStQuarters], gp, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
         StageTimer t(prof, s, "union");
-        hipLaunchKernelGGL(union_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
+        klaunch(prof, "union", union_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
                            eps2, perm, core, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
@@ -1669,7 +1669,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "final");
             DBSCAN_HIP_CHECK(hipMemsetAsync(is_root, 0, n, s));
-            hipLaunchKernelGGL(final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
+            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
                                parent, lab, is_root);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
@@ -1680,27 +1680,27 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "output");
             uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
-            hipLaunchKernelGGL(label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
+            klaunch(prof, "label_sorted", label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                                cell, seg, nbr, nbr_k, nf_p, n, eps2, a.mode, perm, core, lab,
                                rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
                                (const int64_t*)nullptr, (const int32_t*)nullptr, packed);
-            hipLaunchKernelGGL(permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
+            klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
                                packed, (const uint8_t*)nullptr, a.cluster, a.flag);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     } else {
         {
             StageTimer t(prof, s, "final");
-            hipLaunchKernelGGL(final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
+            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
                                parent, lab, (uint8_t*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "output");
             int32_t* packed = static_cast<int32_t*>(ws.packed.ensure(n * sizeof(int32_t)));
-            hipLaunchKernelGGL(slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, core, lab,
+            klaunch(prof, "slab_pack", slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, core, lab,
                                packed);
-            hipLaunchKernelGGL(slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
+            klaunch(prof, "slab_roots", slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
                                packed, a.core_out, a.root_out);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
@@ -1771,17 +1771,17 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     const uint8_t* core = static_cast<const uint8_t*>(ws.core.p);
     const int32_t* lab = static_cast<const int32_t*>(ws.lab.p);
     int32_t* label_of_root = static_cast<int32_t*>(ws.slab_lor.ensure(st.n * sizeof(int32_t)));
-    hipLaunchKernelGGL(slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n, perm,
+    klaunch(prof, "slab_root_labels", slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n, perm,
                        core, lab, gs_of_root, all_roots, n_roots, label_of_root);
     uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
-    hipLaunchKernelGGL(label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+    klaunch(prof, "label_sorted", label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
                        static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
                        reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) +
                            kStNf,
                        st.n, st.eps2, mode, perm, core, lab, (const int32_t*)nullptr, zone, gid,
                        gs_of_root, label_of_root, packed);
-    hipLaunchKernelGGL(permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
+    klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }

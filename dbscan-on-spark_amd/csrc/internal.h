@@ -24,6 +24,7 @@
 //   packed[n] u32 per sorted slot: (cluster << 1) | core, moved to input order through inv
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -81,9 +82,15 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
-// Stage timing with events on the fit stream.
+// Timing with events on the fit stream.  mode 1 (stages): an event pair brackets every pipeline
+// stage (each hipEventRecord between kernels costs ~10 us of idle GPU: 26 stage boundaries add
+// 0.24 ms to a 2.65 ms fit).  mode 2 (kernels): the events ride on the dispatch packets of the
+// kernels themselves (hipExtLaunchKernelGGL), one pair per kernel launch, with no extra packets
+// between kernels -- the form bench.py times with.
 struct Profiler {
     bool on = false;
+    int mode = 0;
+    std::string only;  // kernel mode: time only the launches of this kernel ("" = all)
     struct Stage {
         std::string name;
         double ms = 0;
@@ -102,7 +109,20 @@ struct Profiler {
     void destroy();
 };
 
-// RAII bracket around one stage's launches.
+// A kernel launch, timed by packet events in kernel-profiling mode.
+template <typename F, typename... Args>
+void klaunch(Profiler* prof, const char* name, F kernel, dim3 grid, dim3 block, uint32_t shmem,
+             hipStream_t s, Args... args) {
+    if (prof && prof->on && prof->mode == 2 && (prof->only.empty() || prof->only == name)) {
+        hipEvent_t a = prof->take(), b = prof->take();
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0, args...);
+        prof->pending.push_back({prof->stage_index(name), a, b});
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+    }
+}
+
+// RAII bracket around one stage's launches (stage-profiling mode only).
 struct StageTimer {
     Profiler* prof;
     hipStream_t s;

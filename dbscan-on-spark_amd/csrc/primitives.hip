@@ -392,8 +392,8 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
     for (int shift = 0; shift < max_bits; shift += 8) {
         {
             StageTimer st(prof, s, "sort_upsweep");
-            hipLaunchKernelGGL(radix_upsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, key,
-                               n, shift, bits_dev, nb, h);
+            klaunch(prof, "radix_upsweep", radix_upsweep_kernel, dim3((unsigned)nb), dim3(kBlock),
+                    0, s, key, n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -402,8 +402,8 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         }
         {
             StageTimer st(prof, s, "sort_downsweep");
-            hipLaunchKernelGGL(radix_downsweep_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s,
-                               key, val, key2, val2, n, shift, bits_dev, nb, h);
+            klaunch(prof, "radix_downsweep", radix_downsweep_kernel, dim3((unsigned)nb),
+                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         uint32_t* tk = key;

@@ -34,6 +34,7 @@ SIGNATURES = [
     ("dbscan_stream", _vp, [_vp]),
     ("dbscan_last_stats", _i32, [_vp, _vp, _i32]),
     ("dbscan_profile_enable", _i32, [_vp, _i32]),
+    ("dbscan_profile_only", _i32, [_vp, ctypes.c_char_p]),
     ("dbscan_profile_reset", _i32, [_vp]),
     ("dbscan_profile_read", _i32, [_vp, _vp, _i32, _vp, _vp, _i32]),
     ("dbscan_partition", _i64, [_vp, _vp, _vp, _i64, _d, _i64, _vp, _vp, _i64]),
@@ -138,8 +139,15 @@ class Handle:
                 "tiles", "clique"]
         return {keys[i]: int(buf[i]) for i in range(k)}
 
-    def profile(self, on: bool = True) -> None:
-        check(load().dbscan_profile_enable(self._h, 1 if on else 0))
+    def profile(self, on: bool = True, kernels: bool = False) -> None:
+        """Event timing on the handle's stream: per pipeline stage (event records between
+        stages, ~10 us of GPU idle each) or, with kernels=True, per kernel launch (events on
+        the dispatch packets: no added gaps)."""
+        check(load().dbscan_profile_enable(self._h, (2 if kernels else 1) if on else 0))
+
+    def profile_only(self, kernel=None) -> None:
+        """Kernel mode: time only `kernel`'s launches (None: every kernel)."""
+        check(load().dbscan_profile_only(self._h, kernel.encode() if kernel else None))
 
     def profile_reset(self) -> None:
         check(load().dbscan_profile_reset(self._h))

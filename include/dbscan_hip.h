@@ -110,10 +110,14 @@ void* dbscan_stream(dbscan_handle* h);
  * Returns the number of values written (<= max).                               */
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max);
 
-/* Per-kernel timing with HIP events on the handle's stream.  When enabled, every pipeline
- * stage of each fit is bracketed by events; read accumulates (name, total ms, launches).
+/* Timing with HIP events on the handle's stream.  dbscan_profile_enable(h, 1): every pipeline
+ * stage of each fit is bracketed by event records (each costs ~10 us of GPU idle); (h, 2): every
+ * kernel launch carries its own start/stop events on its dispatch packet (hipExtLaunchKernel; no
+ * added gaps); 0 turns timing off.  read accumulates (name, total ms, launches).
  * `names` receives NUL-separated stage names.  Returns the number of stages written. */
 int32_t dbscan_profile_enable(dbscan_handle* h, int32_t on);
+/* Kernel mode: time only the launches of the named kernel (its profile name; NULL = all). */
+int32_t dbscan_profile_only(dbscan_handle* h, const char* kernel);
 int32_t dbscan_profile_reset(dbscan_handle* h);
 int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, double* total_ms,
                             int64_t* launches, int32_t max);

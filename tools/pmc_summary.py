@@ -18,14 +18,14 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STAGE_OF = {  # kernel base name -> bench.py stage name
-    "tile_union_kernel": "union_tile", "edge_union_kernel": "union_edge",
-    "quarter_root_kernel": "union_root", "union_kernel": "union", "count_tile_kernel": "count",
-    "output_kernel": "output", "gather_kernel": "gather", "radix_downsweep_kernel":
-    "sort_downsweep", "radix_upsweep_kernel": "sort_upsweep", "final_kernel": "final",
-    "quarter_init_kernel": "quarter_init", "segs_kernel": "segs", "group_kernel": "cells",
-    "tslot_kernel": "tables", "bin_kernel": "bin", "bbox_partial_kernel": "bbox",
-}
+def stage_of(kernel):
+    """bench.py's per-kernel name (the klaunch names in csrc/fit.hip): the kernel's base name
+    without `_kernel`; count_tile_kernel is "count"."""
+    if kernel == "count_tile_kernel":
+        return "count"
+    return kernel[:-len("_kernel")] if kernel.endswith("_kernel") else None
+
+
 
 
 def base(name):
@@ -63,7 +63,7 @@ def main():
         fb = fetch.get(k, 0.0) * 2 * 1024
         wb = write.get(k, 0.0) * 1024
         rows.append((k, fetch.get(k, 0.0), write.get(k, 0.0), fb + wb, stats.get(k)))
-        st = STAGE_OF.get(k)
+        st = stage_of(k)
         if st:
             traffic[st] = {"kernel": k, "bytes_per_launch": round(fb + wb),
                            "fetch_kb": fetch.get(k), "write_kb": write.get(k),
