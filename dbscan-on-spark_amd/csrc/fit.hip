@@ -1493,6 +1493,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
 
     uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
     uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
+    int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
     int32_t* perm = static_cast<int32_t*>(ws.perm.ensure(n * sizeof(int32_t)));
     int32_t* perm2 = static_cast<int32_t*>(ws.perm2.ensure(n * sizeof(int32_t)));
     if (mode == kGridEps) {
@@ -1509,7 +1510,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         radix_sort_pairs(s, key, perm, key2, perm2, n, 32, &st[kStBits], ws.hist, ws.scan_tmp,
-                         prof);
+                         prof, inv);
     } else {
         StageTimer t(prof, s, "bin");
         // all pairs: one cell holding every point, the predicate decides (incl. non-finite)
@@ -1524,7 +1525,6 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
 
     // Sizes: every nf-sized table is allocated for n; the tile grid holds <= 2^23 tiles.
     const int64_t ntile_bound = std::min<int64_t>(n, kMaxGridTiles);
-    int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
     double2* xy = static_cast<double2*>(ws.xy.ensure(n * sizeof(double2)));
     int32_t* cell = static_cast<int32_t*>(ws.cell.ensure(n * sizeof(int32_t)));
     uint32_t* ckey = static_cast<uint32_t*>(ws.ckey.ensure(n * sizeof(uint32_t)));
@@ -1550,7 +1550,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
 
     {
         StageTimer t(prof, s, "gather");
-        klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, inv);
+        if (mode != kGridEps)  // (eps grids: the radix sort's final pass wrote inv)
+            klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
+                    inv);
         if (mode != kGridNoPairs)
             klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);

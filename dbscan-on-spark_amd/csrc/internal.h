@@ -247,9 +247,11 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 // (ping-pong through key2/val2).  Stable.
 // max_bits bounds the key width on the host (the pass count); bits_dev holds the actual width
 // on the device: passes at or beyond it copy instead of sorting.
+// inv (optional): the inverse permutation of the sorted vals (a permutation of 0..n-1),
+// inv[val] = sorted position, written by the final pass.
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof);
+                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof, int32_t* inv = nullptr);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

@@ -190,15 +190,21 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
     uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, int64_t n, int shift,
     const int32_t* __restrict__ bits_p, int64_t nblocks,
-    const int32_t* __restrict__ hist_scanned) {
+    const int32_t* __restrict__ hist_scanned, int32_t* __restrict__ inv) {
     __shared__ DownsweepSmem sm;
     const int t = threadIdx.x, w = t >> 6, lane = lane_id();
     const int64_t base = (int64_t)blockIdx.x * kTile;
     const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
-    if (shift >= *bits_p) {  // every key has this digit 0 (or all ones: the sentinel): copy
+    const int bits = *bits_p;
+    // the final order is known in the last sorting pass (or the first copy when none sorts):
+    // that pass also writes the inverse permutation inv[val] = position
+    const bool last = inv && ((shift < bits && shift + 8 >= bits) || (bits == 0 && shift == 0));
+    if (shift >= bits) {  // every key has this digit 0 (or all ones: the sentinel): copy
         for (int j = t; j < tile_n; j += kBlock) {
+            const int32_t v = val[base + j];
             key_out[base + j] = key[base + j];
-            val_out[base + j] = val[base + j];
+            val_out[base + j] = v;
+            if (last) inv[v] = (int32_t)(base + j);
         }
         return;
     }
@@ -268,8 +274,10 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         const uint32_t k = sm.keys[j];
         const uint32_t d = (k >> shift) & 255u;
         const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
+        const int32_t v = sm.vals[j];
         key_out[g] = k;
-        val_out[g] = sm.vals[j];
+        val_out[g] = v;
+        if (last) inv[v] = (int32_t)g;
     }
 }
 
@@ -385,7 +393,7 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof) {
+                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof, int32_t* inv) {
     if (n <= 0 || max_bits <= 0) return;
     const int64_t nb = (n + kTile - 1) / kTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
@@ -403,7 +411,7 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         {
             StageTimer st(prof, s, "sort_downsweep");
             klaunch(prof, "radix_downsweep", radix_downsweep_kernel, dim3((unsigned)nb),
-                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, h);
+                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, h, inv);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         uint32_t* tk = key;
