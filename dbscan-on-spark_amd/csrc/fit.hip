@@ -650,8 +650,13 @@ __device__ __forceinline__ bool count_point(const TileStage& st, const double2* 
 
 // Neighbour counts of one tile per loop trip.  Staged tiles are walked in LDS order (own rows
 // of the 10x10 extended grid), so a point's coordinates and cell come from LDS, not HBM.
-template <int CAP>
-__global__ __launch_bounds__(kBlock) void count_tile_kernel(
+// MINW: waves per SIMD the register allocation must allow.  The LDS capacity and MINW together
+// set the occupancy: CAP 1536 at 5 waves/SIMD (31.5 KB, 95 VGPRs) counted blobs in 0.46 ms and
+// 20%-noise data in 0.75 ms against 0.52 / 0.88 ms at CAP 2048 (39.7 KB, 125 VGPRs: 4 waves),
+// 1.91 vs 1.74 ms on dense data, whose tiles overflow to the global path more often
+// (tools/cap_sweep.sh, r05).
+template <int CAP, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
@@ -1442,10 +1447,9 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 // Host orchestration
 // ---------------------------------------------------------------------------------------
 
-// LDS staging capacity of the count pass (points of a tile + halo).  DBSCAN_COUNT_CAP
-// (3072/2048/1024) overrides it for measurements; results are identical for every choice
-// (tiles over capacity take the global-memory path).  2048 was fastest in the r02 sweep
-// (tools/tile_variants.sh): 40 KB of LDS leaves four workgroups per CU.
+// LDS staging capacity of the count pass (points of a tile + halo; tiles over it take the
+// global-memory path).  DBSCAN_COUNT_CAP = 2048 or 1024 overrides the 1536 default for
+// measurements; results are identical for every choice.
 // DBSCAN_COUNT_ABLATE (timing experiments only; results are wrong): 1 = staging only, no
 // neighbour scans; 2 = scans without neighbour lists.
 static int count_ablate() {
@@ -1613,10 +1617,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     {
         StageTimer t(prof, s, "count");
         if (mode != kGridNoPairs) {
-            auto kern = count_tile_kernel<2048>;
+            auto kern = count_tile_kernel<1536, 5>;
             switch (count_cap()) {
-                case 3072: kern = count_tile_kernel<3072>; break;
-                case 1024: kern = count_tile_kernel<1024>; break;
+                case 2048: kern = count_tile_kernel<2048, 1>; break;
+                case 1024: kern = count_tile_kernel<1024, 5>; break;
                 default: break;
             }
             klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
