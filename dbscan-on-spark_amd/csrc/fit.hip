@@ -1021,7 +1021,8 @@ constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
 // One tile per loop trip: quarter records and their quarter-grid neighbours in LDS, the
 // pair tests read the (L2-resident) coordinates directly -- staging them measured slower
 // (fewer resident workgroups; tools/tile_variants.sh, r02).
-__global__ __launch_bounds__(kBlock) void tile_union_kernel(
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ tq,
     const int32_t* __restrict__ ntiles_p, const int4* __restrict__ qinfo,
     const int4* __restrict__ qg, double eps2, const int32_t* __restrict__ perm,
@@ -1103,7 +1104,8 @@ __global__ __launch_bounds__(kBlock) void tile_union_kernel(
 // global union-find sees about one operation per component pair per tile side.
 constexpr int kEdgeNodes = 72;
 
-__global__ __launch_bounds__(kBlock) void edge_union_kernel(
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ ntiles_p,
     const int32_t* __restrict__ tq, const int4* __restrict__ tnb,
     const int4* __restrict__ qinfo, const int4* __restrict__ qg,
@@ -1459,6 +1461,16 @@ static int count_ablate() {
     }();
     return v;
 }
+// DBSCAN_UNION_W: register budget (waves/SIMD) of the tile/edge union kernels, 6 by default
+// (tile_union 88 -> 78 VGPRs, edge_union 100 -> 80): blobs 0.35 / 0.31 ms -> 0.31 / 0.23 ms;
+// 8 spills and is slower (tools/union_w_sweep.sh, r05).  5 and 7 for measurements.
+static int union_w() {
+    static const int v = [] {
+        const char* e = std::getenv("DBSCAN_UNION_W");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
 static int count_cap() {
     static const int v = [] {
         const char* e = std::getenv("DBSCAN_COUNT_CAP");
@@ -1647,15 +1659,20 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         {
             StageTimer t(prof, s, "union_tile");
-            klaunch(prof, "tile_union", tile_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
-                               &st[kStTiles], qinfo, qg, eps2, perm, core, parent, qcomp, gp);
+            auto tu = tile_union_kernel<6>;
+            if (union_w() == 5) tu = tile_union_kernel<5>;
+            if (union_w() == 7) tu = tile_union_kernel<7>;
+            klaunch(prof, "tile_union", tu, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
+                    &st[kStTiles], qinfo, qg, eps2, perm, core, parent, qcomp, gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "union_edge");
-            klaunch(prof, "edge_union", edge_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
-                               &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent,
-                               gp);
+            auto eu = edge_union_kernel<6>;
+            if (union_w() == 5) eu = edge_union_kernel<5>;
+            if (union_w() == 7) eu = edge_union_kernel<7>;
+            klaunch(prof, "edge_union", eu, dim3(tile_grid), dim3(kBlock), 0, s, xy,
+                    &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
