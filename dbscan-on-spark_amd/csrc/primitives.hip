@@ -17,7 +17,10 @@ namespace dbscan {
 
 namespace {
 
-constexpr int kItems = 16;                  // rounds per tile
+#ifndef RADIX_ITEMS
+#define RADIX_ITEMS 8
+#endif
+constexpr int kItems = 16;                  // rounds per scan tile
 constexpr int kTile = kBlock * kItems;      // 4096
 constexpr int kWaves = kBlock / 64;         // 4
 
@@ -146,6 +149,12 @@ size_t scan_tmp_elems(int64_t n) {
 
 // ------------------------------------ radix sort ------------------------------------------
 
+// Radix tiles: 2048 keys (8 rounds of 256).  Half the scan tiles' size keeps the downsweep at
+// 22 KB of LDS and ~70 VGPRs: 6+ workgroups per CU instead of 4 (measured in r05 against
+// 4096-key tiles: see DESIGN.md §3).
+constexpr int kRItems = RADIX_ITEMS;
+constexpr int kRTile = kBlock * kRItems;
+
 __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* __restrict__ key,
                                                                int64_t n, int shift,
                                                                const int32_t* __restrict__ bits_p,
@@ -156,9 +165,9 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
     const int w = threadIdx.x >> 6;
     for (int d = threadIdx.x; d < kWaves * 256; d += kBlock) (&h[0][0])[d] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int64_t base = (int64_t)blockIdx.x * kRTile;
 #pragma unroll 4
-    for (int r = 0; r < kItems; ++r) {
+    for (int r = 0; r < kRItems; ++r) {
         const int64_t i = base + r * kBlock + threadIdx.x;
         if (i < n) atomicAdd(&h[w][(key[i] >> shift) & 255u], 1u);
     }
@@ -179,8 +188,8 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
 // (tile sorted by digit), and each digit run is written coalesced to its global offset.
 struct DownsweepSmem {
     int32_t cnt[kWaves][256];  // per-wave digit counters -> wave offsets within a digit
-    uint32_t keys[kTile];
-    int32_t vals[kTile];
+    uint32_t keys[kRTile];
+    int32_t vals[kRTile];
     int32_t tile_start[257];
     int32_t gofs[256];
     int32_t wsum[kWaves];
@@ -193,8 +202,8 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     const int32_t* __restrict__ hist_scanned, int32_t* __restrict__ inv) {
     __shared__ DownsweepSmem sm;
     const int t = threadIdx.x, w = t >> 6, lane = lane_id();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+    const int64_t base = (int64_t)blockIdx.x * kRTile;
+    const int tile_n = (int)((n - base) < kRTile ? (n - base) : kRTile);
     const int bits = *bits_p;
     // the final order is known in the last sorting pass (or the first copy when none sorts):
     // that pass also writes the inverse permutation inv[val] = position
@@ -212,13 +221,13 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     for (int k = 0; k < kWaves; ++k) sm.cnt[k][t] = 0;
     __syncthreads();
 
-    uint32_t k_r[kItems];
-    int32_t v_r[kItems];
-    uint32_t dr[kItems];  // digit | (rank within the wave's digit run << 8); 0xFFFFFFFF invalid
+    uint32_t k_r[kRItems];
+    int32_t v_r[kRItems];
+    uint32_t dr[kRItems];  // digit | (rank within the wave's digit run << 8); 0xFFFFFFFF invalid
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int64_t wbase = base + (int64_t)w * (kTile / kWaves);
+    const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
 #pragma unroll
-    for (int r = 0; r < kItems; ++r) {
+    for (int r = 0; r < kRItems; ++r) {
         const int64_t i = wbase + r * 64 + lane;
         const bool valid = i < base + tile_n;
         const uint32_t k = valid ? key[i] : kSentinelKey;
@@ -261,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kItems; ++r) {
+    for (int r = 0; r < kRItems; ++r) {
         if (dr[r] != 0xFFFFFFFFu) {
             const uint32_t d = dr[r] & 255u;
             const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 8);
@@ -395,7 +404,7 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
                       int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
                       DevBuf& hist, DevBuf& scan_tmp, Profiler* prof, int32_t* inv) {
     if (n <= 0 || max_bits <= 0) return;
-    const int64_t nb = (n + kTile - 1) / kTile;
+    const int64_t nb = (n + kRTile - 1) / kRTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
     for (int shift = 0; shift < max_bits; shift += 8) {
         {
