@@ -1474,7 +1474,7 @@ static int union_w() {
 static int count_cap() {
     static const int v = [] {
         const char* e = std::getenv("DBSCAN_COUNT_CAP");
-        return e ? std::atoi(e) : 2048;
+        return e ? std::atoi(e) : 0;
     }();
     return v;
 }
