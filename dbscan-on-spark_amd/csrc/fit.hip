@@ -35,9 +35,10 @@
 //                over the facing strips, then one global union per joined pair of tile
 //                components (lock-free, hooking the root with the larger visit index under the
 //                smaller, so a root IS s(K)); quarter reps then point at their roots
-//   final        root of every core -> lab = s(K); roots flagged in input order
-//   [scan of root flags in input order -> rank = cluster id - 1]
-//   output       cores rank[lab]+1; non-cores min lab over core neighbours + Naive/Archery
+//   final        root of every core -> lab = s(K); roots set in a bit array in input order
+//   [scan of the bit words' popcounts -> cluster id of root o = 1 + roots before o]
+//   output       cores cluster_of_root(lab); non-cores min lab over core neighbours +
+//                Naive/Archery
 //                rule; written in input order
 #include "internal.h"
 
@@ -1225,7 +1226,7 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
                                                        const uint8_t* __restrict__ core,
                                                        const int32_t* __restrict__ parent,
                                                        int32_t* __restrict__ lab,
-                                                       uint8_t* __restrict__ is_root) {
+                                                       unsigned long long* __restrict__ root_bits) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     if (!core[p]) {
@@ -1234,8 +1235,19 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
     }
     int r = (int)p;
     for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
-    lab[p] = perm[r];
-    if (r == (int)p && is_root) is_root[perm[p]] = 1;
+    const int32_t o = perm[r];
+    lab[p] = o;
+    if (r == (int)p && root_bits) atomicOr(root_bits + (o >> 6), 1ull << (o & 63));
+}
+
+// Cluster id of the component whose root (s(K)) is input point o: 1 + number of roots before o
+// in input order, from the root bit words and their scanned popcounts (L2-resident: n/8 +
+// n/16 bytes, where a per-point rank array would be 4n bytes of scattered reads).
+__device__ __forceinline__ uint32_t cluster_of_root(const uint64_t* __restrict__ root_bits,
+                                                    const int32_t* __restrict__ word_rank,
+                                                    int32_t o) {
+    const uint64_t below = root_bits[o >> 6] & ((1ull << (o & 63)) - 1ull);
+    return (uint32_t)(word_rank[o >> 6] + __popcll(below)) + 1u;
 }
 
 // Labels, one thread per sorted slot: cores rank[lab]+1 (or the merged label for slab fits);
@@ -1252,7 +1264,8 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const Seg* __restrict__ seg, const int32_t* __restrict__ nbr, int nbr_k,
     const int32_t* __restrict__ nf_p, int64_t n, double eps2, int32_t mode, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
-    const int32_t* __restrict__ rank, const uint8_t* __restrict__ zone,
+    const uint64_t* __restrict__ root_bits, const int32_t* __restrict__ word_rank,
+    const uint8_t* __restrict__ zone,
     const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
     const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1260,7 +1273,8 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const int64_t nf = *nf_p;
     uint32_t v = 0;  // Noise
     if (core[p]) {
-        const uint32_t cl = SLAB ? (uint32_t)label_of_root[lab[p]] : (uint32_t)rank[lab[p]] + 1u;
+        const uint32_t cl = SLAB ? (uint32_t)label_of_root[lab[p]]
+                                 : cluster_of_root(root_bits, word_rank, lab[p]);
         v = (cl << 1) | 1u;
     } else if (p < nf) {
         const int32_t o = perm[p];
@@ -1297,7 +1311,8 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
         }
         const int64_t self = SLAB ? gid[o] : (int64_t)o;
         if (mr >= 0 && (mode != 0 || m < self)) {
-            const uint32_t cl = SLAB ? (uint32_t)label_of_root[mr] : (uint32_t)rank[mr] + 1u;
+            const uint32_t cl = SLAB ? (uint32_t)label_of_root[mr]
+                                     : cluster_of_root(root_bits, word_rank, mr);
             v = cl << 1;  // Border
         }
     }
@@ -1525,7 +1540,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        radix_sort_pairs(s, key, perm, key2, perm2, n, 32, &st[kStBits], ws.hist, ws.scan_tmp,
+        radix_sort_pairs(s, key, perm, key2, perm2, n, 32, &st[kStBits], ws.hist, ws.scan,
                          prof, inv);
     } else {
         StageTimer t(prof, s, "bin");
@@ -1584,9 +1599,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "heads_reduce", heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                part);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan_tmp);
-            exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan_tmp);
-            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan_tmp);
+            exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan);
+            exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan);
+            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
@@ -1645,7 +1660,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                            a.min_points, core, parent, block_cores + tile_grid);
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = (int64_t)tile_grid + rest_grid;
-        exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan_tmp);
+        exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan);
         if (a.zone)  // (the core count above then includes zone-2 points: a statistic only)
             klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
                                core);
@@ -1687,25 +1702,26 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     if (!a.zone) {
-        uint8_t* is_root = static_cast<uint8_t*>(ws.is_root.ensure(n));
-        int32_t* rank = static_cast<int32_t*>(ws.rank.ensure(n * sizeof(int32_t)));
+        const int64_t nw = (n + 63) / 64;
+        uint64_t* root_bits = static_cast<uint64_t*>(ws.is_root.ensure(nw * sizeof(uint64_t)));
+        int32_t* word_rank = static_cast<int32_t*>(ws.rank.ensure(nw * sizeof(int32_t)));
         {
             StageTimer t(prof, s, "final");
-            DBSCAN_HIP_CHECK(hipMemsetAsync(is_root, 0, n, s));
+            DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
-                               parent, lab, is_root);
+                               parent, lab, reinterpret_cast<unsigned long long*>(root_bits));
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "rank");
-            exclusive_scan(s, 1, is_root, rank, n, &st[kStClusters], ws.scan_tmp);
+            exclusive_scan(s, 2, root_bits, word_rank, nw, &st[kStClusters], ws.scan);
         }
         {
             StageTimer t(prof, s, "output");
             uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
             klaunch(prof, "label_sorted", label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                                cell, seg, nbr, nbr_k, nf_p, n, eps2, a.mode, perm, core, lab,
-                               rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
+                               root_bits, word_rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
                                (const int64_t*)nullptr, (const int32_t*)nullptr, packed);
             klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
                                packed, (const uint8_t*)nullptr, a.cluster, a.flag);
@@ -1715,7 +1731,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "final");
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
-                               parent, lab, (uint8_t*)nullptr);
+                               parent, lab, (unsigned long long*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -1802,7 +1818,8 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                        static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
                        reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) +
                            kStNf,
-                       st.n, st.eps2, mode, perm, core, lab, (const int32_t*)nullptr, zone, gid,
+                       st.n, st.eps2, mode, perm, core, lab, (const uint64_t*)nullptr,
+                       (const int32_t*)nullptr, zone, gid,
                        gs_of_root, label_of_root, packed);
     klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);

@@ -19,7 +19,8 @@
 //            quarter-grid coordinates
 //   nbr[nf][minPoints-1]  slots of each non-core's neighbours (-1 terminated), minPoints <= 12
 //   core[n]  u8, parent[n] i32 (union-find over slots, hooked by visit index), lab[n] i32
-//   is_root[n] u8 and rank[n] i32 over INPUT order (cluster numbering scan)
+//   is_root[ceil(n/64)] u64 root bits over INPUT order and rank[ceil(n/64)] i32 their per-word
+//   exclusive popcount prefix: rank(o) = rank[o>>6] + popc(is_root[o>>6] below bit o&63)
 //   inv[n]   i32 sorted slot of each input index (inverse of perm)
 //   packed[n] u32 per sorted slot: (cluster << 1) | core, moved to input order through inv
 #pragma once
@@ -132,15 +133,26 @@ struct StageTimer {
     ~StageTimer();
 };
 
+// Look-back state of the single-pass scan: state[0] a watchdog flag, then one status word per
+// tile; the epoch distinguishes successive scans so the words need clearing only on fresh
+// memory or when the 30-bit epoch wraps.
+struct ScanState {
+    DevBuf buf;
+    uint32_t epoch = 0;
+    uint64_t* prepare(hipStream_t s, int64_t ntiles);  // also advances the epoch
+};
+
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag;
+    ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
+        scan.buf.release();
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
@@ -236,12 +248,12 @@ int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:
 //   0: in = const int32_t* values
-//   1: in = const uint8_t* flags (0/1)
-//   2: head flags of a sorted u32 key array: v[i] = (i == 0 || key[i] != key[i-1])
-//   3: head flags of key >> 2 (the eps cell of a quarter-cell key)
-// Writes out[0..n) and, if total_dev != nullptr, the total at *total_dev.
+//   1: in = const uint8_t* flags (nonzero counts 1)
+//   2: in = const uint64_t* bit words (each counts its popcount)
+// Writes out[0..n) (out may equal in) and, if total_dev != nullptr, the total at *total_dev.
+// One launch; successive scans on one ScanState must be stream-ordered.
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
-                    int32_t* total_dev, DevBuf& tmp);
+                    int32_t* total_dev, ScanState& ss);
 
 // LSD radix sort of (key, val) pairs on the low bits; results end in key/val
 // (ping-pong through key2/val2).  Stable.
@@ -251,7 +263,7 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 // inv[val] = sorted position, written by the final pass.
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof, int32_t* inv = nullptr);
+                      DevBuf& hist, ScanState& scan, Profiler* prof, int32_t* inv = nullptr);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

@@ -161,7 +161,7 @@ int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint
     hipLaunchKernelGGL(roots_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, n, zone, gid,
                        root, parent, gs_of_root, cnt);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    exclusive_scan(s, 0, cnt, off, nb, off + nb, ws.scan_tmp);
+    exclusive_scan(s, 0, cnt, off, nb, off + nb, ws.scan);
     hipLaunchKernelGGL(roots_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, n, zone, gid,
                        root, parent, off, own_roots);
     DBSCAN_HIP_CHECK(hipGetLastError());

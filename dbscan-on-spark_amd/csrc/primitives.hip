@@ -1,7 +1,7 @@
 // primitives.hip -- hand-written device-wide primitives for the fit pipeline (gfx950).
 //
-//   exclusive_scan     reduce-then-scan over 4096-element tiles (256 threads x 16 rounds),
-//                      wave64 shuffle scans, recursive over the tile sums
+//   exclusive_scan     one launch: 4096-element tiles held in registers (LDS transpose to
+//                      16 consecutive elements per thread), tiles chained by decoupled look-back
 //   radix_sort_pairs   stable LSD radix sort, 8-bit digits, 4096-key tiles:
 //                      upsweep (per-wave LDS histograms) -> scan -> downsweep that ranks keys
 //                      with 64-bit wave ballots (match-any over the 8 digit bits) against
@@ -42,6 +42,8 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
+// Scan inputs: MODE 0 int32 values, MODE 1 uint8 flags (nonzero -> 1), MODE 2 the popcounts of
+// uint64 bit words.
 template <int MODE>
 __device__ __forceinline__ int scan_value(const void* in, int64_t i, int64_t n) {
     if (i >= n) return 0;
@@ -49,102 +51,129 @@ __device__ __forceinline__ int scan_value(const void* in, int64_t i, int64_t n) 
         return static_cast<const int32_t*>(in)[i];
     } else if constexpr (MODE == 1) {
         return static_cast<const uint8_t*>(in)[i] ? 1 : 0;
-    } else if constexpr (MODE == 2) {
-        const uint32_t* k = static_cast<const uint32_t*>(in);
-        return (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
-    } else {  // head flags of key >> 2 (cell of a quarter-cell key)
-        const uint32_t* k = static_cast<const uint32_t*>(in);
-        return (i == 0 || (k[i] >> 2) != (k[i - 1] >> 2)) ? 1 : 0;
+    } else {
+        return __popcll(static_cast<const uint64_t*>(in)[i]);
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const void* in, int64_t n,
-                                                             int32_t* partial) {
-    __shared__ int ws[kWaves];
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    int acc = 0;
-#pragma unroll 4
-    for (int r = 0; r < kItems; ++r) acc += scan_value<MODE>(in, base + r * kBlock + threadIdx.x, n);
-    acc = wave_sum(acc);
-    if (lane_id() == 0) ws[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int s = 0;
-        for (int w = 0; w < kWaves; ++w) s += ws[w];
-        partial[blockIdx.x] = s;
-    }
+// Single-pass exclusive scan: one 4096-element tile per block, chained by decoupled look-back.
+// Tile = blockIdx.x: workgroups are dispatched in index order (per XCD), so the lowest
+// unfinished tile only ever waits on finished ones and the chain always drains.  (A tile
+// counter taken with a device-scope atomic would guarantee that on any dispatcher, but it
+// serialises at ~20 ns a block across the XCDs: 50 us for 2442 tiles.)  A bounded spin keeps
+// the kernel finite even if that assumption broke: it then flags state[0] and the results
+// are wrong, never hung.  A block loads its tile with 16 coalesced rounds issued back to back,
+// transposes it through LDS so each thread owns 16 consecutive elements (one 17-word padded
+// row: conflict-free), scans in registers, publishes the tile aggregate, sums its predecessors'
+// published values 64 tiles at a time -- aggregates until the nearest inclusive prefix --
+// publishes its own inclusive prefix and stores the tile back through LDS, coalesced.  A status
+// word packs (epoch, flag, value) in 64 bits, stored and polled with agent-scope atomics; the
+// epoch (one per scan call) makes words of earlier scans unreadable, so the status array is
+// never cleared.  In place (out == in) is fine: a block reads its whole tile before writing.
+constexpr uint64_t kStAgg = 1, kStIncl = 2;
+constexpr int kSpinLimit = 1 << 22;
+constexpr int kRow = kItems + 1;  // padded LDS row per thread
+
+__device__ __forceinline__ uint64_t scan_status(uint32_t epoch, uint64_t flag, int32_t v) {
+    return ((uint64_t)epoch << 34) | (flag << 32) | (uint32_t)v;
 }
 
-// Exclusive scan of one tile per block, offset by the scanned tile sums (or 0).
+__device__ __forceinline__ int lds_slot(int e) { return e + (e >> 4); }  // e = r*256 + tid
+
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void scan_down_kernel(const void* in, int64_t n,
-                                                           const int32_t* tile_offset,
-                                                           int32_t* out, int32_t* total) {
-    __shared__ int ws[2][kWaves];
-    const int64_t base = (int64_t)blockIdx.x * kTile;
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    int carry = tile_offset ? tile_offset[blockIdx.x] : 0;
-    for (int r = 0; r < kItems; ++r) {
-        const int64_t i = base + r * kBlock + threadIdx.x;
-        const int v = scan_value<MODE>(in, i, n);
-        const int incl = wave_incl_scan(v);
-        if (lane == 63) ws[r & 1][w] = incl;
-        __syncthreads();
-        int woff = 0, btot = 0;
+__global__ __launch_bounds__(kBlock) void scan_kernel(const void* in, int64_t n, int32_t* out,
+                                                      int32_t* total, uint64_t* state,
+                                                      uint32_t epoch, int64_t ntiles) {
+    __shared__ int wtot[kWaves], wstop[kWaves], wsum[kWaves];
+    __shared__ int buf[kBlock * kRow];
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const int t = blockIdx.x;
+    const int64_t base = (int64_t)t * kTile;
+    int v[kItems];
 #pragma unroll
-        for (int k = 0; k < kWaves; ++k) {
-            const int t = ws[r & 1][k];
-            woff += (k < w) ? t : 0;
-            btot += t;
-        }
-        if (i < n) out[i] = carry + woff + incl - v;
-        carry += btot;
+    for (int r = 0; r < kItems; ++r) v[r] = scan_value<MODE>(in, base + r * kBlock + tid, n);
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) buf[lds_slot(r * kBlock + tid)] = v[r];
+    __syncthreads();
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {  // thread-local exclusive scan of its 16 elements
+        const int x = buf[tid * kRow + k];
+        v[k] = sum;
+        sum += x;
     }
-    if (total && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = carry;
-}
-
-template <int MODE>
-__global__ void scan_total_kernel(const void* in, const int32_t* out, int64_t n, int32_t* tot) {
-    *tot = out[n - 1] + scan_value<MODE>(in, n - 1, n);
+    const int incl = wave_incl_scan(sum);
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    int agg = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) agg += wtot[k];
+    int prefix = 0;
+    if (ntiles > 1) {
+        uint64_t* status = state + 1;
+        if (tid == 0) {
+            __hip_atomic_store(status + t, scan_status(epoch, t == 0 ? kStIncl : kStAgg, agg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // all 256 threads look back, one predecessor each per round: when every block is
+        // resident at once the inclusive prefixes advance a whole window per L2 round trip
+        for (int j = t - 1; j >= 0; j -= kBlock) {
+            const int idx = j - tid;
+            uint64_t st = 0;
+            if (idx >= 0) {
+                for (int spin = 0;; ++spin) {
+                    st = __hip_atomic_load(status + idx, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)(st >> 34) == epoch && ((st >> 32) & 3u) != 0) break;
+                    if (spin == kSpinLimit) {  // watchdog: never reached with in-order dispatch
+                        __hip_atomic_fetch_or(state, 1ull, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+                        st = scan_status(epoch, kStIncl, 0);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            const uint64_t inc = __ballot(idx >= 0 && ((st >> 32) & 3u) == kStIncl);
+            if (lane == 0) wstop[w] = inc ? __builtin_ctzll(inc) : 64;
+            __syncthreads();
+            int first = kWaves;  // nearest wave holding an inclusive prefix
+#pragma unroll
+            for (int k = kWaves - 1; k >= 0; --k) first = wstop[k] < 64 ? k : first;
+            const bool take = idx >= 0 && (w < first || (w == first && lane <= wstop[first]));
+            const int part = wave_sum(take ? (int32_t)(uint32_t)st : 0);
+            if (lane == 0) wsum[w] = part;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kWaves; ++k) prefix += wsum[k];
+            if (first < kWaves) break;
+        }
+        if (tid == 0 && t > 0)
+            __hip_atomic_store(status + t, scan_status(epoch, kStIncl, prefix + agg),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0 && t == ntiles - 1 && total) *total = prefix + agg;
+    int off = prefix + incl - sum;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) off += (k < w) ? wtot[k] : 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) buf[tid * kRow + k] = off + v[k];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const int64_t i = base + r * kBlock + tid;
+        if (i < n) out[i] = buf[lds_slot(r * kBlock + tid)];
+    }
 }
 
 template <int MODE>
 void scan_impl(hipStream_t s, const void* in, int32_t* out, int64_t n, int32_t* total_dev,
-               int32_t* tmp, size_t tmp_elems) {
+               ScanState& ss) {
     const int64_t nb = (n + kTile - 1) / kTile;
-    if (nb <= 1) {
-        hipLaunchKernelGGL(scan_down_kernel<MODE>, dim3(1), dim3(kBlock), 0, s, in, n, nullptr,
-                           out, total_dev);
-        DBSCAN_HIP_CHECK(hipGetLastError());
-        return;
-    }
-    if ((size_t)nb > tmp_elems) throw ArgError{"scan workspace too small"};
-    int32_t* partial = tmp;
-    hipLaunchKernelGGL(scan_reduce_kernel<MODE>, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n,
-                       partial);
+    uint64_t* state = nb > 1 ? ss.prepare(s, nb) : nullptr;
+    hipLaunchKernelGGL(scan_kernel<MODE>, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n, out,
+                       total_dev, state, ss.epoch, nb);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    // exclusive scan of the tile sums in place (recursion on a smaller problem)
-    scan_impl<0>(s, partial, partial, nb, nullptr, tmp + nb, tmp_elems - (size_t)nb);
-    hipLaunchKernelGGL(scan_down_kernel<MODE>, dim3((unsigned)nb), dim3(kBlock), 0, s, in, n,
-                       partial, out, nullptr);
-    DBSCAN_HIP_CHECK(hipGetLastError());
-    if (total_dev) {
-        // total = last exclusive value + last input value
-        hipLaunchKernelGGL(scan_total_kernel<MODE>, dim3(1), dim3(1), 0, s, in, out, n,
-                           total_dev);
-        DBSCAN_HIP_CHECK(hipGetLastError());
-    }
-}
-
-size_t scan_tmp_elems(int64_t n) {
-    size_t need = 0;
-    int64_t m = n;
-    while (m > kTile) {
-        m = (m + kTile - 1) / kTile;
-        need += (size_t)m;
-    }
-    return need + 16;
 }
 
 // ------------------------------------ radix sort ------------------------------------------
@@ -384,25 +413,34 @@ __global__ __launch_bounds__(kBlock) void bbox_final_kernel(const double* partia
 
 }  // namespace
 
+uint64_t* ScanState::prepare(hipStream_t s, int64_t ntiles) {
+    void* old = buf.p;
+    uint64_t* p = static_cast<uint64_t*>(buf.ensure((size_t)(ntiles + 1) * sizeof(uint64_t)));
+    if (p != old || epoch == 0x3FFFFFFFu) {  // fresh memory or epoch wrap: clear, restart at 1
+        DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, buf.bytes, s));
+        epoch = 0;
+    }
+    ++epoch;
+    return p;
+}
+
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
-                    int32_t* total_dev, DevBuf& tmp) {
+                    int32_t* total_dev, ScanState& ss) {
     if (n <= 0) {
         if (total_dev) DBSCAN_HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(int32_t), s));
         return;
     }
-    const size_t need = scan_tmp_elems(n);
-    int32_t* t = static_cast<int32_t*>(tmp.ensure(need * sizeof(int32_t)));
-    switch (mode) {
-        case 0: scan_impl<0>(s, in, out, n, total_dev, t, need); break;
-        case 1: scan_impl<1>(s, in, out, n, total_dev, t, need); break;
-        case 2: scan_impl<2>(s, in, out, n, total_dev, t, need); break;
-        default: scan_impl<3>(s, in, out, n, total_dev, t, need); break;
-    }
+    if (mode == 0)
+        scan_impl<0>(s, in, out, n, total_dev, ss);
+    else if (mode == 1)
+        scan_impl<1>(s, in, out, n, total_dev, ss);
+    else
+        scan_impl<2>(s, in, out, n, total_dev, ss);
 }
 
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, DevBuf& scan_tmp, Profiler* prof, int32_t* inv) {
+                      DevBuf& hist, ScanState& scan, Profiler* prof, int32_t* inv) {
     if (n <= 0 || max_bits <= 0) return;
     const int64_t nb = (n + kRTile - 1) / kRTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
@@ -415,7 +453,7 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         }
         {
             StageTimer st(prof, s, "sort_scan");
-            exclusive_scan(s, 0, h, h, nb * 256, nullptr, scan_tmp);
+            exclusive_scan(s, 0, h, h, nb * 256, nullptr, scan);
         }
         {
             StageTimer st(prof, s, "sort_downsweep");
