@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict
 // known on the device); every loop trip ends in a barrier before the stage is overwritten.
 // ---------------------------------------------------------------------------------------
 struct TileStage {
-    int ok, total, ts, te, t;
+    int ok, total, ts, te, t, q0, nq;
     int cb[100];   // global slot begin of each extended cell
     int off[101];  // LDS offset of each extended cell
     int cn[100];
@@ -441,13 +441,15 @@ __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restri
     }
 }
 
-struct StageMeta {  // one tile's staging table, held in registers (lanes < 100; lane 0: range)
-    int b = 0, cnt = 0, ts = 0, te = 0;
+struct StageMeta {  // one tile's staging table, held in registers (lanes < 100; lane 0: range
+                    // and, with tq, the tile's quarter range)
+    int b = 0, cnt = 0, ts = 0, te = 0, q0 = 0, q1 = 0;
 };
 
 __device__ __forceinline__ StageMeta stage_meta(int t, int ntiles,
                                                 const int2* __restrict__ tstage,
-                                                const int32_t* __restrict__ tstart) {
+                                                const int32_t* __restrict__ tstart,
+                                                const int32_t* __restrict__ tq = nullptr) {
     StageMeta m;
     if (t >= ntiles) return m;
     const int tid = threadIdx.x;
@@ -459,6 +461,10 @@ __device__ __forceinline__ StageMeta stage_meta(int t, int ntiles,
     if (tid == 0) {
         m.ts = tstart[t];
         m.te = tstart[t + 1];
+        if (tq) {
+            m.q0 = tq[(int64_t)t * kTslot];
+            m.q1 = tq[(int64_t)t * kTslot + 64];
+        }
     }
     return m;
 }
@@ -474,6 +480,8 @@ __device__ bool stage_build(const StageMeta& m, const double2* __restrict__ xy, 
     if (tid == 0) {
         st.ts = m.ts;
         st.te = m.te;
+        st.q0 = m.q0;
+        st.nq = m.q1 - m.q0;
     }
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the 100 counts by wave 0 (2 chunks)
@@ -649,32 +657,334 @@ __device__ __forceinline__ bool count_point(const TileStage& st, const double2* 
     }
 }
 
-// Neighbour counts of one tile per loop trip.  Staged tiles are walked in LDS order (own rows
-// of the 10x10 extended grid), so a point's coordinates and cell come from LDS, not HBM.
-// MINW: waves per SIMD the register allocation must allow.  The LDS capacity and MINW together
-// set the occupancy: CAP 1536 at 5 waves/SIMD (31.5 KB, 95 VGPRs) counted blobs in 0.46 ms and
-// 20%-noise data in 0.75 ms against 0.52 / 0.88 ms at CAP 2048 (39.7 KB, 125 VGPRs: 4 waves),
-// 1.91 vs 1.74 ms on dense data, whose tiles overflow to the global path more often
-// (tools/cap_sweep.sh, r05).
-template <int CAP, int MINW>
+// Does any core of quarter A (points in registers: px/py, n) lie within eps of a core of B?
+// core(j): is slot (or LDS index) j a core point.
+template <class Src, class CoreF>
+__device__ __forceinline__ bool pair_found(const double* px, const double* py, int na,
+                                           const Src* __restrict__ src, int b0, int b1,
+                                           uint32_t bmask, CoreF core, int boff, double eps2) {
+    if (b1 - b0 <= 32) {
+        uint32_t m = bmask;
+        while (m) {
+            const int j = __ffs(m) - 1;
+            m &= m - 1;
+            const double2 pb = src[b0 - boff + j];
+            bool f = false;
+#pragma unroll
+            for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
+            if (f) return true;
+        }
+        return false;
+    }
+    for (int j = b0; j < b1; ++j) {
+        if (!core(j)) continue;
+        const double2 pb = src[j - boff];
+        bool f = false;
+#pragma unroll
+        for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
+        if (f) return true;
+    }
+    return false;
+}
+
+// own quarter's cores into registers; returns the count, or -1 if > kQReg (generic path)
+template <class Src>
+__device__ __forceinline__ int load_own(const Src* __restrict__ src, int4 me, int off,
+                                        double* px, double* py) {
+#pragma unroll
+    for (int k = 0; k < kQReg; ++k) {
+        px[k] = 0.0;
+        py[k] = 0.0;
+    }
+    if (me.y - me.x > 32) return -1;
+    uint32_t m = (uint32_t)me.w;
+    int na = 0;
+#pragma unroll
+    for (int k = 0; k < kQReg; ++k) {
+        if (m) {
+            const int j = __ffs(m) - 1;
+            m &= m - 1;
+            const double2 v = src[me.x - off + j];
+            px[k] = v.x;
+            py[k] = v.y;
+            na = k + 1;
+        }
+    }
+    return m ? -1 : na;
+}
+
+// generic pair test when a quarter holds more than kQReg cores (dense data)
+template <class Src, class CoreF>
+__device__ bool pair_found_generic(const Src* __restrict__ src, int off, int4 a, int4 b,
+                                   CoreF core, double eps2) {
+    for (int i = a.x; i < a.y; ++i) {
+        if (!core(i)) continue;
+        const double2 pa = src[i - off];
+        for (int j = b.x; j < b.y; ++j) {
+            if (!core(j)) continue;
+            const double2 pb = src[j - off];
+            if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) return true;
+        }
+    }
+    return false;
+}
+
+// Orders one wave's LDS accesses across its lanes (a wave executes in lockstep; this keeps the
+// compiler from reordering LDS reads above another lane's earlier writes).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS union-find over the tile's quarter cells (local indices; hook larger under smaller).
+__device__ __forceinline__ int lfind(int* lp, int x) {
+    while (true) {
+        const int p = lp[x];
+        if (p == x) return x;
+        const int gp = lp[p];
+        if (gp != p) lp[x] = gp;
+        x = gp;
+    }
+}
+__device__ __forceinline__ void lunite(int* lp, int a, int b) {
+    for (;;) {
+        a = lfind(lp, a);
+        b = lfind(lp, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(&lp[a], a, b) == a) return;
+    }
+}
+
+constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
+
+// ---------------------------------------------------------------------------------------
+// Tile-local quarter union fused into the count (plain fits with clique quarters): once a
+// tile's core flags are known the block that counted it builds the quarter records
+// (quarter_init's job) and unions the tile's quarters (tile_union's job) against the
+// coordinates it still holds in LDS, instead of two later kernels re-reading them from memory.
+// Every core of the tile then points straight at its tile component's rep.
+// ---------------------------------------------------------------------------------------
+struct FuseArgs {
+    const int32_t* tq;       // per tile: first quarter of each local cell (+ end)
+    const int32_t* qstart;   // quarter slot ranges
+    const uint32_t* qkey;    // quarter keys
+    const int32_t* perm;     // visit index per slot
+    const GridParams* gp;
+    int4* qinfo;             // out: (begin, end, rep, core mask) per quarter
+    int4* qg;                // out: (quarter-grid x, y, min visit index of its cores, 0)
+    int32_t* qcomp;          // out: tile component rep per quarter (-1: no cores)
+};
+
+struct UnionLds {  // aliases the count's neighbour-list staging (the two never overlap in time)
+    int lp[kMaxTileQ];           // LDS union-find over the tile's quarters
+    uint32_t lrange[kMaxTileQ];  // staged: LDS begin | length << 11; local quarter-grid cell
+                                 // (16 y + x) << 22; bit 31: holds cores
+    uint32_t lmask[kMaxTileQ];   // cores among the first 32 points
+    uint16_t qmap[kMaxTileQ];    // 16x16 local quarter grid -> local quarter (0xFFFF: none)
+    unsigned long long cmin[kMaxTileQ];  // per component: min (visit index << 32 | rep)
+};
+static_assert(sizeof(UnionLds) <= kMaxNbr * kBlock * sizeof(uint16_t), "UnionLds must fit");
+
+// Quarter-grid offsets to test from each quarter: one of each opposite pair (dy < 0, or dy == 0
+// and dx < 0), so every unordered quarter pair within the 5x5 stencil is one item -- the 4
+// adjacent offsets first, then the 8 at distance 2.
+__constant__ int8_t kRingDx[12] = {-1, 0, 1, -1, -2, -1, 0, 1, 2, -2, 2, -2};
+__constant__ int8_t kRingDy[12] = {-1, -1, -1, 0, -2, -2, -2, -2, -2, -1, -1, 0};
+
+// Is there an eps pair between a core of quarter A and a core of quarter B?  Ranges are LDS
+// indices (staged) or slots; masks hold the cores among each quarter's first 32 points.
+template <class CoreF>
+__device__ __forceinline__ bool quarters_touch(const double2* __restrict__ src, int ab, int ae,
+                                               uint32_t am, int bb, int be, uint32_t bm,
+                                               CoreF is_core, double eps2) {
+    if (ae - ab <= 32 && be - bb <= 32) {
+        for (uint32_t m1 = am; m1; m1 &= m1 - 1) {
+            const double2 pa = src[ab + __ffs(m1) - 1];
+            for (uint32_t m2 = bm; m2; m2 &= m2 - 1) {
+                const double2 pb = src[bb + __ffs(m2) - 1];
+                if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) return true;
+            }
+        }
+        return false;
+    }
+    for (int i = ab; i < ae; ++i) {
+        if (!is_core(i)) continue;
+        const double2 pa = src[i];
+        for (int j = bb; j < be; ++j)
+            if (is_core(j) && within_eps(pa.x, pa.y, src[j].x, src[j].y, eps2)) return true;
+    }
+    return false;
+}
+
+// A workgroup barrier that orders LDS only: unlike __syncthreads it does not wait for this
+// wave's outstanding global loads (a perm load stays in flight across the pair tests).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// b, e, key: this thread's quarter (threadIdx.x < nq), loaded before the count.
+template <bool STAGED>
+__device__ void fused_tile_union(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
+                                 const GridParams& g, const TileStage& st,
+                                 const double2* __restrict__ buf,
+                                 const uint32_t* __restrict__ lcore,
+                                 const double2* __restrict__ xy, const uint8_t* __restrict__ core,
+                                 double eps2, int32_t* __restrict__ parent, UnionLds& u,
+                                 int ablate) {
+    const int i = threadIdx.x;
+    const auto is_core = [&](int j) {  // j: LDS index (staged) or slot
+        if constexpr (STAGED) return ((lcore[j >> 5] >> (j & 31)) & 1u) != 0;
+        else return core[j] != 0;
+    };
+    u.qmap[i] = 0xFFFF;
+    u.cmin[i] = ~0ull;
+    lds_barrier();
+    // quarter records: quarter_init's rep and core mask.  The radix sort is stable and the
+    // visit index is the input index, so a quarter's slots are in visit order and its rep (the
+    // core with the smallest visit index) is simply its first core: one perm load, whose
+    // latency the pair tests below hide.
+    int rep = -1, best = 0x7FFFFFFF, gx = 0, gy = 0;
+    if (i < nq) {
+        uint32_t cx, cy;
+        cell_xy(key >> 2, g.ntx, cx, cy);
+        gx = (int)(2 * cx + (key & 1u));
+        gy = (int)(2 * cy + ((key >> 1) & 1u));
+        const int lq = (gy & 15) * 16 + (gx & 15);
+        const int len = e - b;
+        int jb = b;
+        if constexpr (STAGED) {
+            const int l = (int)((key >> 2) & 63u);
+            const int k = ((l >> 3) + 1) * 10 + (l & 7) + 1;
+            jb = st.off[k] + (b - st.cb[k]);
+        }
+        uint32_t mask = 0;
+        int first = -1;
+        if (STAGED && len <= 32) {  // the quarter's core bits straight from the bitmap
+            const int w = jb >> 5, o = jb & 31;
+            const uint64_t v = (uint64_t)lcore[w] | ((uint64_t)lcore[w + 1] << 32);
+            mask = (uint32_t)(v >> o) & (len == 32 ? ~0u : ((1u << len) - 1u));
+            first = mask ? __ffs(mask) - 1 : -1;
+        } else {
+            for (int j = 0; j < len && (j < 32 || first < 0); ++j)
+                if (is_core(jb + j)) {
+                    if (j < 32) mask |= 1u << j;
+                    if (first < 0) first = j;
+                }
+        }
+        if (first >= 0) {
+            rep = b + first;
+            best = fa.perm[rep];
+        }
+        fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
+        u.lp[i] = i;
+        u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) |
+                      (STAGED ? (uint32_t)jb | ((uint32_t)len << 11) : 0u);
+        u.lmask[i] = mask;
+        u.qmap[lq] = (uint16_t)i;
+    }
+    lds_barrier();
+    // tile_union's pair tests, one (quarter, offset) item per thread, adjacent quarters first so
+    // that most distance-2 pairs are found joined and skipped
+    if (ablate != 3) {  // (ablate 3: time without the pair tests)
+        for (int sweep = 0; sweep < (ablate == 5 ? 1 : 2); ++sweep) {
+            const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
+            for (int k = i; k < nq * nofs; k += kBlock) {
+                const int o = k / nq, qi = k - o * nq;
+                const uint32_t ri = u.lrange[qi];
+                if (!(ri >> 31)) continue;
+                const int lq = (int)((ri >> 22) & 255u);
+                const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+                if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+                const int j = u.qmap[uy * 16 + ux];
+                if (j == 0xFFFF) continue;
+                const uint32_t rj = u.lrange[j];
+                if (!(rj >> 31)) continue;
+                // (adjacent items run all at once: a find before each would rarely prune)
+                if (sweep && ablate != 6 && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                int ab, ae, bb, be;
+                if constexpr (STAGED) {
+                    ab = (int)(ri & 2047u);
+                    ae = ab + (int)((ri >> 11) & 2047u);
+                    bb = (int)(rj & 2047u);
+                    be = bb + (int)((rj >> 11) & 2047u);
+                } else {
+                    ab = fa.qstart[q0 + qi];
+                    ae = fa.qstart[q0 + qi + 1];
+                    bb = fa.qstart[q0 + j];
+                    be = fa.qstart[q0 + j + 1];
+                }
+                if (quarters_touch(STAGED ? buf : xy, ab, ae, u.lmask[qi], bb, be, u.lmask[j],
+                                   is_core, eps2))
+                    lunite(u.lp, qi, j);
+            }
+            lds_barrier();
+        }
+    }
+    // tile components: rep = the quarter rep with the smallest visit index
+    int r = -1;
+    if (i < nq && rep >= 0) {
+        r = lfind(u.lp, i);
+        atomicMin(&u.cmin[r], ((unsigned long long)(uint32_t)best << 32) | (uint32_t)rep);
+    }
+    lds_barrier();
+    if (i < nq) {
+        const int crep = r >= 0 ? (int)(uint32_t)(u.cmin[r] & 0xFFFFFFFFull) : -1;
+        fa.qg[q0 + i] = make_int4(gx, gy, best, 0);
+        fa.qcomp[q0 + i] = crep;
+        if (rep >= 0) parent[rep] = crep;  // cores reach it through their quarter's rep
+    }
+}
+
+// FUSE: also the tile-local quarter union (fused_tile_union) when the grid's quarter cells are
+// cliques; the parents are then written there, once.
+template <int CAP, int MINW, bool FUSE>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
     int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate) {
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate,
+    FuseArgs fa) {
     __shared__ TileStage st;
     __shared__ double2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
     __shared__ int rowoff[9];
-    __shared__ uint16_t lsts[kMaxNbr * kBlock];
+    __shared__ __attribute__((aligned(16))) uint16_t lsts[kMaxNbr * kBlock];
+    __shared__ uint32_t lcore[FUSE ? (CAP + 31) / 32 + 1 : 1];  // core bits per LDS index
+    static_assert(!FUSE || CAP < 2048, "fused union packs LDS ranges in 11 bits");
     uint16_t* lst = lsts + threadIdx.x;
     const int ntiles = *ntiles_p;
     int mine = 0;
-    StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart);
+    bool fuse = false;
+    GridParams g{};
+    if constexpr (FUSE) {
+        g = *fa.gp;
+        fuse = g.clique != 0 && ablate != 4;  // (ablate 4: time the count alone)
+    }
+    const int32_t* tq = fuse ? fa.tq : nullptr;
+    StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart, tq);
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (FUSE && threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
         const bool staged = stage_build<CAP>(meta, xy, st, buf);
-        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart);  // in flight during the scans
+        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart, tq);  // in flight during the scans
+        // this thread's quarter record, in flight during the count (fused union)
+        int qb = 0, qe = 0, q0 = 0, nq = 0;
+        uint32_t qk = 0;
+        if (fuse) {
+            q0 = st.q0;
+            nq = st.nq;
+            if ((int)threadIdx.x < nq) {
+                qb = fa.qstart[q0 + threadIdx.x];
+                qe = fa.qstart[q0 + threadIdx.x + 1];
+                qk = fa.qkey[q0 + threadIdx.x];
+            }
+        }
         if (staged) {
             if (threadIdx.x == 0) {  // own points per row of the tile: prefix over rows
                 int acc = 0;
@@ -708,9 +1018,15 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
                                                 min_points, lst, ablate == 2 ? nullptr : nbr,
                                                 nbr_k);
                 }
-                parent[p] = p;
+                if (!fuse) parent[p] = p;
+                if (FUSE && is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
+            }
+            if (fuse) {
+                __syncthreads();
+                fused_tile_union<true>(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, core, eps2,
+                                       parent, *reinterpret_cast<UnionLds*>(lsts), ablate);
             }
         } else {
             for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
@@ -721,9 +1037,14 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
                     is_core = count_point<false>(st, buf, xy, cell, seg, 0, 0, p, eps2,
                                                  min_points, lst, nbr, nbr_k);
                 }
-                parent[p] = p;
+                if (!fuse) parent[p] = p;
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
+            }
+            if (fuse) {
+                __syncthreads();  // (workgroup scope: this block's core[] writes are visible)
+                fused_tile_union<false>(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, core, eps2,
+                                        parent, *reinterpret_cast<UnionLds*>(lsts), ablate);
             }
         }
         __syncthreads();
@@ -913,112 +1234,6 @@ __global__ __launch_bounds__(kBlock) void quarter_init_kernel(
         if (core[j]) parent[j] = rep;
 }
 
-// Does any core of quarter A (points in registers: px/py, n) lie within eps of a core of B?
-template <class Src>
-__device__ __forceinline__ bool pair_found(const double* px, const double* py, int na,
-                                           const Src* __restrict__ src, int b0, int b1,
-                                           uint32_t bmask, const uint8_t* __restrict__ core,
-                                           int boff, double eps2) {
-    if (b1 - b0 <= 32) {
-        uint32_t m = bmask;
-        while (m) {
-            const int j = __ffs(m) - 1;
-            m &= m - 1;
-            const double2 pb = src[b0 - boff + j];
-            bool f = false;
-#pragma unroll
-            for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
-            if (f) return true;
-        }
-        return false;
-    }
-    for (int j = b0; j < b1; ++j) {
-        if (!core[j]) continue;
-        const double2 pb = src[j - boff];
-        bool f = false;
-#pragma unroll
-        for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
-        if (f) return true;
-    }
-    return false;
-}
-
-// own quarter's cores into registers; returns the count, or -1 if > kQReg (generic path)
-template <class Src>
-__device__ __forceinline__ int load_own(const Src* __restrict__ src, int4 me, int off,
-                                        double* px, double* py) {
-#pragma unroll
-    for (int k = 0; k < kQReg; ++k) {
-        px[k] = 0.0;
-        py[k] = 0.0;
-    }
-    if (me.y - me.x > 32) return -1;
-    uint32_t m = (uint32_t)me.w;
-    int na = 0;
-#pragma unroll
-    for (int k = 0; k < kQReg; ++k) {
-        if (m) {
-            const int j = __ffs(m) - 1;
-            m &= m - 1;
-            const double2 v = src[me.x - off + j];
-            px[k] = v.x;
-            py[k] = v.y;
-            na = k + 1;
-        }
-    }
-    return m ? -1 : na;
-}
-
-// generic pair test when a quarter holds more than kQReg cores (dense data)
-template <class Src>
-__device__ bool pair_found_generic(const Src* __restrict__ src, int off, int4 a, int4 b,
-                                   const uint8_t* __restrict__ core, double eps2) {
-    for (int i = a.x; i < a.y; ++i) {
-        if (!core[i]) continue;
-        const double2 pa = src[i - off];
-        for (int j = b.x; j < b.y; ++j) {
-            if (!core[j]) continue;
-            const double2 pb = src[j - off];
-            if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) return true;
-        }
-    }
-    return false;
-}
-
-// Orders one wave's LDS accesses across its lanes (a wave executes in lockstep; this keeps the
-// compiler from reordering LDS reads above another lane's earlier writes).
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// LDS union-find over the tile's quarter cells (local indices; hook larger under smaller).
-__device__ __forceinline__ int lfind(int* lp, int x) {
-    while (true) {
-        const int p = lp[x];
-        if (p == x) return x;
-        const int gp = lp[p];
-        if (gp != p) lp[x] = gp;
-        x = gp;
-    }
-}
-__device__ __forceinline__ void lunite(int* lp, int a, int b) {
-    for (;;) {
-        a = lfind(lp, a);
-        b = lfind(lp, b);
-        if (a == b) return;
-        if (a < b) {
-            const int t = a;
-            a = b;
-            b = t;
-        }
-        if (atomicCAS(&lp[a], a, b) == a) return;
-    }
-}
-
-constexpr int kMaxTileQ = 256;  // 64 cells x 4 quarters
-
 // One tile per loop trip: quarter records and their quarter-grid neighbours in LDS, the
 // pair tests read the (L2-resident) coordinates directly -- staging them measured slower
 // (fewer resident workgroups; tools/tile_variants.sh, r02).
@@ -1037,6 +1252,7 @@ __global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
     __shared__ int crep[kMaxTileQ];
     const int ntiles = *ntiles_p;
     const int i = threadIdx.x;
+    const auto gcore = [core](int j) { return core[j] != 0; };
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int q0 = tq[(int64_t)t * kTslot], nq = tq[(int64_t)t * kTslot + 64] - q0;
         qmap[i] = -1;
@@ -1072,8 +1288,8 @@ __global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
                         if (o.z < 0) continue;
                         if (lfind(lp, i) == lfind(lp, j)) continue;
                         const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
-                                                            (uint32_t)o.w, core, 0, eps2)
-                                               : pair_found_generic(xy, 0, me, o, core, eps2);
+                                                            (uint32_t)o.w, gcore, 0, eps2)
+                                               : pair_found_generic(xy, 0, me, o, gcore, eps2);
                         if (f) lunite(lp, i, j);
                     }
         }
@@ -1121,6 +1337,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
+    const auto gcore = [core](int j) { return core[j] != 0; };
     // one (tile, side) per wave and loop trip: waves never wait for each other
     for (int tw = blockIdx.x * (kBlock / 64) + w; tw < 2 * ntiles;
          tw += gridDim.x * (kBlock / 64)) {
@@ -1191,8 +1408,8 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                         if (o.z < 0) continue;
                         if (lfind(lp, a) == lfind(lp, b)) continue;
                         const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
-                                                            (uint32_t)o.w, core, 0, eps2)
-                                               : pair_found_generic(xy, 0, me, o, core, eps2);
+                                                            (uint32_t)o.w, gcore, 0, eps2)
+                                               : pair_found_generic(xy, 0, me, o, gcore, eps2);
                         if (!f) continue;
                         lunite(lp, a, b);
                         const int ra = uf_find(parent, ncomp[w][a]);
@@ -1221,10 +1438,15 @@ __global__ __launch_bounds__(kBlock) void quarter_root_kernel(const int4* __rest
     parent[rep] = r;
 }
 
-__global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
+// qidx/qinfo (fused union: core parents were never written): a grid core's walk starts at its
+// quarter's rep (slots >= nf are outside the grid and their own parents).
+__global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t* __restrict__ nf_p,
+                                                       const GridParams* __restrict__ gp,
                                                        const int32_t* __restrict__ perm,
                                                        const uint8_t* __restrict__ core,
                                                        const int32_t* __restrict__ parent,
+                                                       const int32_t* __restrict__ qidx,
+                                                       const int4* __restrict__ qinfo,
                                                        int32_t* __restrict__ lab,
                                                        unsigned long long* __restrict__ root_bits) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1234,6 +1456,14 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n,
         return;
     }
     int r = (int)p;
+    const int64_t nf = *nf_p;
+    if (qidx && gp->clique && nf > 0) {
+        // Branch-free on purpose: the divergent form `p < nf ? qinfo[qidx[p]].z : p` was
+        // miscompiled (ROCm 7.2 clang, gfx950: the else value was never moved into place for
+        // the lanes with p >= nf).  Clamp the index, load, select.
+        const int rq = qinfo[qidx[p < nf ? p : nf - 1]].z;
+        r = p < nf ? rq : r;
+    }
     for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
     const int32_t o = perm[r];
     lab[p] = o;
@@ -1493,6 +1723,14 @@ static int count_cap() {
     }();
     return v;
 }
+// DBSCAN_FUSE=0: run quarter_init and tile_union as their own kernels (A/B measurements)
+static bool fuse_union() {
+    static const bool v = [] {
+        const char* e = std::getenv("DBSCAN_FUSE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 
 // Enqueues one whole fit on stream s and never waits on the device: the grid, the finite count
 // nf and every table size live in device memory (ws.misc), so launch sizes derive from n alone
@@ -1578,6 +1816,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* qstart = static_cast<int32_t*>(ws.qstart.ensure((n + 1) * sizeof(int32_t)));
     int4* qinfo = static_cast<int4*>(ws.qrep.ensure(n * sizeof(int4)));
     int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
+    // plain fits: the tile-local quarter union runs inside the count kernel (slab fits clear
+    // zone-2 core flags after the count, so their unions must come later)
+    const bool fuse = mode == kGridEps && !a.zone && fuse_union() && count_cap() == 0;
 
     {
         StageTimer t(prof, s, "gather");
@@ -1644,15 +1885,16 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     {
         StageTimer t(prof, s, "count");
         if (mode != kGridNoPairs) {
-            auto kern = count_tile_kernel<1536, 5>;
+            auto kern = fuse ? count_tile_kernel<1536, 5, true> : count_tile_kernel<1536, 5, false>;
             switch (count_cap()) {
-                case 2048: kern = count_tile_kernel<2048, 1>; break;
-                case 1024: kern = count_tile_kernel<1024, 5>; break;
+                case 2048: kern = count_tile_kernel<2048, 1, false>; break;
+                case 1024: kern = count_tile_kernel<1024, 5, false>; break;
                 default: break;
             }
+            const FuseArgs fa{tq, qstart, qkey, perm, gp, qinfo, qg, qcomp};
             klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
                                tstage, &st[kStTiles], eps2, a.min_points, core,
-                               parent, block_cores, nbr, nbr_k, count_ablate());
+                               parent, block_cores, nbr, nbr_k, count_ablate(), fa);
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
@@ -1666,13 +1908,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                core);
     }
     if (mode == kGridEps) {  // quarter-cell unions (no-ops unless the grid made them cliques)
-        {
+        if (!fuse) {
             StageTimer t(prof, s, "quarter_init");
             klaunch(prof, "quarter_init", quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
                                qkey, &st[kStQuarters], gp, perm, core, qinfo, qg, parent);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        {
+        if (!fuse) {
             StageTimer t(prof, s, "union_tile");
             auto tu = tile_union_kernel<6>;
             if (union_w() == 5) tu = tile_union_kernel<5>;
@@ -1708,8 +1950,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "final");
             DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
-            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
-                               parent, lab, reinterpret_cast<unsigned long long*>(root_bits));
+            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
+                               parent, fuse ? qidx : nullptr, qinfo, lab,
+                               reinterpret_cast<unsigned long long*>(root_bits));
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -1730,8 +1973,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     } else {
         {
             StageTimer t(prof, s, "final");
-            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm, core,
-                               parent, lab, (unsigned long long*)nullptr);
+            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
+                               parent, (const int32_t*)nullptr, qinfo, lab,
+                               (unsigned long long*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
