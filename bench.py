@@ -32,16 +32,16 @@ sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
 METRIC = "points clustered/sec (whole node) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Algorithmic bytes per point and launch, by kernel (SURVEY.md §8d's per-phase figures; each
-# array crosses HBM once): count 17 = sorted x,y 16 + core 1; the §8d union 21 is
-# carried by quarter_init (core 1 + perm 4 + parent 4) and tile_union (x,y 16; edge_union and
-# quarter_root touch tile-edge strips and quarter reps only); the §8d output 30 by final (13),
-# the rank scan and label_sorted/permute_out.  Radix passes: 4 launches per fit, each reading
-# key+perm 8 and writing 8.
+# array crosses HBM once).  count = 21: the count kernel also builds the quarter
+# records and the tile-local quarter union (fused), so it carries §8d's count (sorted x,y 16 +
+# core 1) and union (parent 4; the union's x,y read is the count's, already in LDS).
+# edge_union and quarter_root touch tile-edge strips and quarter reps only.  The §8d output 30
+# is carried by final (13), the rank scan and label_sorted/permute_out.  Radix passes: 4
+# launches per fit, each reading key+perm 8 and writing 8.
 ALG_BYTES = {
     "bbox_partial": 16, "bin": 20, "radix_upsweep": 4, "radix_downsweep": 16, "inverse": 8,
-    "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 17, "quarter_init": 9,
-    "tile_union": 16, "edge_union": 0, "quarter_root": 0, "final": 13, "label_sorted": 13,
-    "permute_out": 13,
+    "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 21, "edge_union": 0,
+    "quarter_root": 0, "final": 13, "label_sorted": 13, "permute_out": 13,
 }
 PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
 
