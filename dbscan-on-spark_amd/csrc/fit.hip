@@ -441,6 +441,71 @@ __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restri
     }
 }
 
+// Clique grids: tiles by the size of their tile + halo stage (the tstage counts), listed for
+// the three count paths: small (<= kSmallCap points: count_wave_kernel, one wave per tile),
+// medium (<= CAP: count_tile32_kernel, one workgroup per tile) and big (over CAP:
+// big_count_kernel + big_union_kernel, global memory).  64 tiles per workgroup; one atomic
+// per class and workgroup.
+enum TileClass { kTileSmall = 0, kTileMedium = 1, kTileBig = 2, kTileNone = 3 };
+constexpr int kSmallCap = 192;
+
+struct TileLists {
+    int32_t* n;      // [3] list lengths (device)
+    int32_t* small;  // occupied tile indices per class
+    int32_t* medium;
+    int32_t* big;
+};
+
+template <int CAP>
+__global__ __launch_bounds__(kBlock) void tile_class_kernel(const int2* __restrict__ tstage,
+                                                            const int32_t* __restrict__ ntiles_p,
+                                                            const GridParams* __restrict__ gp,
+                                                            TileLists tl) {
+    if (!gp->clique) return;
+    __shared__ uint8_t cls[64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ntiles = *ntiles_p;
+    for (int base = blockIdx.x * 64; base < ntiles; base += gridDim.x * 64) {
+        int c[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {  // 16 tiles per wave, all loads in flight together
+            const int t = base + w * 16 + r;
+            c[r] = 0;
+            if (t < ntiles) {
+                c[r] = tstage[(int64_t)t * 100 + lane].y;
+                if (lane < 36) c[r] += tstage[(int64_t)t * 100 + 64 + lane].y;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c[r] += __shfl_xor(c[r], o, 64);
+            if (lane == 0) {
+                const int t = base + w * 16 + r;
+                cls[w * 16 + r] = t >= ntiles ? kTileNone
+                                               : (c[r] <= kSmallCap ? kTileSmall
+                                                                     : (c[r] <= CAP ? kTileMedium
+                                                                                    : kTileBig));
+            }
+        }
+        __syncthreads();
+        if (w == 0) {
+            const int v = cls[lane];
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint64_t m = __ballot(v == k);
+                int at = 0;
+                if (lane == 0 && m) at = atomicAdd(&tl.n[k], __popcll(m));
+                at = __shfl(at, 0, 64);
+                int32_t* list = k == 0 ? tl.small : (k == 1 ? tl.medium : tl.big);
+                if (v == k) list[at + __popcll(m & lt)] = base + lane;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 struct StageMeta {  // one tile's staging table, held in registers (lanes < 100; lane 0: range
                     // and, with tq, the tile's quarter range)
     int b = 0, cnt = 0, ts = 0, te = 0, q0 = 0, q1 = 0;
@@ -775,7 +840,10 @@ struct FuseArgs {
     const int32_t* qstart;   // quarter slot ranges
     const uint32_t* qkey;    // quarter keys
     const int32_t* perm;     // visit index per slot
+    const uint32_t* tkey;    // occupied tile ids
     const GridParams* gp;
+    int f32;                 // clique grids are counted by count_tile32_kernel
+    TileLists tl;            // f32: clique-grid tiles by stage size (tile_class_kernel)
     int4* qinfo;             // out: (begin, end, rep, core mask) per quarter
     int4* qg;                // out: (quarter-grid x, y, min visit index of its cores, 0)
     int32_t* qcomp;          // out: tile component rep per quarter (-1: no cores)
@@ -965,6 +1033,10 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     GridParams g{};
     if constexpr (FUSE) {
         g = *fa.gp;
+        if (fa.f32 && g.clique && ablate != 4) {  // count_tile32_kernel + big_count_kernel's
+            if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
+            return;
+        }
         fuse = g.clique != 0 && ablate != 4;  // (ablate 4: time the count alone)
     }
     const int32_t* tq = fuse ? fa.tq : nullptr;
@@ -1057,6 +1129,731 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
         int tot = 0;
         for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
         block_cores[blockIdx.x] = tot;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// The clique-grid count with fp32 tile coordinates (count_tile32_kernel).  A tile's staged
+// points are held in LDS as float2 offsets from the tile's halo corner in CELL units,
+//   r = fl32((v*0.5 - vmin*0.5) * inv - (8*tile - 1)),   |r| < 10 (+ grid rounding),
+// the same cell coordinate the bin kernel floors, so F = fl32(dx*dx + dy*dy) approximates the
+// exact squared distance over h^2 to within 1.6e-5 (fp32 rounding of |r| <= 16: 4.8e-7 per
+// coordinate, |dx| <= 3 inside the 3x3 stencil; the fp64 cell coordinates are off by < 3e-8).
+// With e2 = eps*eps / h^2 (the clique grid has hx = hy = h) and M = 2^-14:
+//   F <= lo = rd(e2 - M)  =>  the reference's fp64 dx*dx + dy*dy <= eps*eps   (a neighbour)
+//   F >  hi = ru(e2 + M)  =>  it is not
+//   otherwise             =>  the fp64 predicate itself on the two points' coordinates
+// so counts, flags and pair tests stay bit-exact, while the hot loop runs fp32 math on 8-byte
+// LDS records (half the LDS and registers of the fp64 staging; one ambiguous candidate in
+// ~10^5 takes the exact path).
+// ---------------------------------------------------------------------------------------
+struct F32Cut {
+    float lo, hi;
+};
+
+__device__ __forceinline__ F32Cut f32_cut(const GridParams& g, double eps2) {
+    const double s = 0.5 * g.invx;  // 1 / h
+    const double e2 = eps2 * s * s;
+    return {__double2float_rd(e2 - 0x1p-14), __double2float_ru(e2 + 0x1p-14)};
+}
+
+// LDS index -> global slot of a staged tile (largest extended cell k with off[k] <= q)
+__device__ __forceinline__ int stage_slot(const TileStage& st, int q) {
+    int k = 0;
+#pragma unroll
+    for (int s = 64; s > 0; s >>= 1)
+        if (k + s < 100 && st.off[k + s] <= q) k += s;
+    return st.cb[k] + (q - st.off[k]);
+}
+
+__device__ __forceinline__ float f32_d2(float2 a, float2 b) {
+    const float dx = b.x - a.x, dy = b.y - a.y;
+    return __builtin_fmaf(dx, dx, dy * dy);
+}
+
+// stage_build with the float2 cell-unit records (origin ox, oy: the tile's halo corner)
+template <int CAP>
+__device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy, TileStage& st,
+                              float2* buf, const GridParams& g, double ox, double oy) {
+    const int tid = threadIdx.x;
+    if (tid < 100) {
+        st.cb[tid] = m.b;
+        st.cn[tid] = m.cnt;
+    }
+    if (tid == 0) {
+        st.ts = m.ts;
+        st.te = m.te;
+        st.q0 = m.q0;
+        st.nq = m.q1 - m.q0;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        int carry = 0;
+        for (int base = 0; base < 100; base += 64) {
+            const int i = base + tid;
+            const int v = i < 100 ? st.cn[i] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(incl, o, 64);
+                if (tid >= o) incl += u;
+            }
+            if (i < 100) st.off[i] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (tid == 0) {
+            st.off[100] = carry;
+            st.total = carry;
+            st.ok = carry <= CAP;
+        }
+    }
+    __syncthreads();
+    if (st.ok) {
+        constexpr int kPer = (CAP + kBlock - 1) / kBlock;
+        const int total = st.total;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = tid + u * kBlock;
+            if (i < total) {
+                int lo = 0;
+#pragma unroll
+                for (int s = 64; s > 0; s >>= 1)
+                    if (lo + s < 100 && st.off[lo + s] <= i) lo += s;
+                const double2 v = xy[st.cb[lo] + (i - st.off[lo])];
+                buf[i] = make_float2((float)((v.x * 0.5 - g.xmin2) * g.invx - ox),
+                                     (float)((v.y * 0.5 - g.ymin2) * g.invy - oy));
+            }
+        }
+    }
+    __syncthreads();
+    return st.ok;
+}
+
+// One LDS range of candidates in batches of 8 (the last batch masked).  Sure hits by F <= lo,
+// ambiguous ones by the exact fp64 predicate (exact(q) for LDS index q).  REC: each batch with
+// hits is noted as ONE record (first LDS index | range tag << 11 | hit bits << 16) in the
+// thread's column of lst while fewer than nbr_k records exist; a point that ends below
+// minPoints has at most minPoints - 1 hits, so its records are complete.
+template <bool REC, int STRIDE = kBlock, class ExactF>
+__device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
+                                             float2 me, F32Cut cut, int min_points, int& cnt,
+                                             uint32_t* lst, int& nrec, int nbr_k, int tag,
+                                             ExactF exact) {
+    for (int j = b; j < e; j += 8) {
+        const int nin = e - j;
+        float2 qq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) qq[u] = buf[u < nin ? j + u : j];
+        uint32_t hm = 0, am = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float F = f32_d2(me, qq[u]);
+            hm |= (u < nin && F <= cut.lo) ? (1u << u) : 0u;
+            am |= (u < nin && F <= cut.hi) ? (1u << u) : 0u;
+        }
+        am ^= hm;
+        if (__builtin_expect(am != 0, 0)) {
+            for (uint32_t m = am; m; m &= m - 1) {
+                const int u = __ffs(m) - 1;
+                if (exact(j + u)) hm |= 1u << u;
+            }
+        }
+        if (REC && hm && nrec < nbr_k) {
+            lst[nrec * STRIDE] = (uint32_t)j | ((uint32_t)tag << 11) | (hm << 16);
+            ++nrec;
+        }
+        cnt += __popc(hm);
+        if (cnt >= min_points) return true;
+    }
+    return cnt >= min_points;
+}
+
+// Is there an eps pair between a core of quarter A and a core of quarter B (LDS ranges)?
+template <class CoreF, class ExactF>
+__device__ __forceinline__ bool quarters_touch32(const float2* __restrict__ buf, int ab, int ae,
+                                                 uint32_t am, int bb, int be, uint32_t bm,
+                                                 CoreF is_core, F32Cut cut, ExactF exact) {
+    if (ae - ab <= 32 && be - bb <= 32) {
+        for (uint32_t m1 = am; m1; m1 &= m1 - 1) {
+            const int ia = ab + __ffs(m1) - 1;
+            const float2 pa = buf[ia];
+            for (uint32_t m2 = bm; m2; m2 &= m2 - 1) {
+                const int ib = bb + __ffs(m2) - 1;
+                const float F = f32_d2(pa, buf[ib]);
+                if (F <= cut.lo) return true;
+                if (F <= cut.hi && exact(ia, ib)) return true;
+            }
+        }
+        return false;
+    }
+    for (int i = ab; i < ae; ++i) {
+        if (!is_core(i)) continue;
+        const float2 pa = buf[i];
+        for (int j = bb; j < be; ++j) {
+            if (!is_core(j)) continue;
+            const float F = f32_d2(pa, buf[j]);
+            if (F <= cut.lo) return true;
+            if (F <= cut.hi && exact(i, j)) return true;
+        }
+    }
+    return false;
+}
+
+// fused_tile_union over the float2 stage (see fused_tile_union for the structure)
+__device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
+                                   const GridParams& g, const TileStage& st,
+                                   const float2* __restrict__ buf,
+                                   const uint32_t* __restrict__ lcore,
+                                   const double2* __restrict__ xy, double eps2, F32Cut cut,
+                                   int32_t* __restrict__ parent, UnionLds& u, int ablate) {
+    const int i = threadIdx.x;
+    const auto is_core = [&](int j) { return ((lcore[j >> 5] >> (j & 31)) & 1u) != 0; };
+    const auto exact = [&](int qa, int qb) {
+        const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
+        return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
+    };
+    u.qmap[i] = 0xFFFF;
+    u.cmin[i] = ~0ull;
+    lds_barrier();
+    int rep = -1, best = 0x7FFFFFFF, gx = 0, gy = 0;
+    if (i < nq) {
+        uint32_t cx, cy;
+        cell_xy(key >> 2, g.ntx, cx, cy);
+        gx = (int)(2 * cx + (key & 1u));
+        gy = (int)(2 * cy + ((key >> 1) & 1u));
+        const int lq = (gy & 15) * 16 + (gx & 15);
+        const int len = e - b;
+        const int l = (int)((key >> 2) & 63u);
+        const int k = ((l >> 3) + 1) * 10 + (l & 7) + 1;
+        const int jb = st.off[k] + (b - st.cb[k]);
+        uint32_t mask = 0;
+        int first = -1;
+        if (len <= 32) {
+            const int w = jb >> 5, o = jb & 31;
+            const uint64_t v = (uint64_t)lcore[w] | ((uint64_t)lcore[w + 1] << 32);
+            mask = (uint32_t)(v >> o) & (len == 32 ? ~0u : ((1u << len) - 1u));
+            first = mask ? __ffs(mask) - 1 : -1;
+        } else {
+            for (int j = 0; j < len && (j < 32 || first < 0); ++j)
+                if (is_core(jb + j)) {
+                    if (j < 32) mask |= 1u << j;
+                    if (first < 0) first = j;
+                }
+        }
+        if (first >= 0) {
+            rep = b + first;
+            best = fa.perm[rep];
+        }
+        fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
+        u.lp[i] = i;
+        u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) | (uint32_t)jb |
+                      ((uint32_t)len << 11);
+        u.lmask[i] = mask;
+        u.qmap[lq] = (uint16_t)i;
+    }
+    lds_barrier();
+    if (ablate != 3) {
+        for (int sweep = 0; sweep < 2; ++sweep) {
+            const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
+            for (int k = i; k < nq * nofs; k += kBlock) {
+                const int o = k / nq, qi = k - o * nq;
+                const uint32_t ri = u.lrange[qi];
+                if (!(ri >> 31)) continue;
+                const int lq = (int)((ri >> 22) & 255u);
+                const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+                if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+                const int j = u.qmap[uy * 16 + ux];
+                if (j == 0xFFFF) continue;
+                const uint32_t rj = u.lrange[j];
+                if (!(rj >> 31)) continue;
+                if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
+                const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
+                if (quarters_touch32(buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, cut,
+                                     exact))
+                    lunite(u.lp, qi, j);
+            }
+            lds_barrier();
+        }
+    }
+    int r = -1;
+    if (i < nq && rep >= 0) {
+        r = lfind(u.lp, i);
+        atomicMin(&u.cmin[r], ((unsigned long long)(uint32_t)best << 32) | (uint32_t)rep);
+    }
+    lds_barrier();
+    if (i < nq) {
+        const int crep = r >= 0 ? (int)(uint32_t)(u.cmin[r] & 0xFFFFFFFFull) : -1;
+        fa.qg[q0 + i] = make_int4(gx, gy, best, 0);
+        fa.qcomp[q0 + i] = crep;
+        if (rep >= 0) parent[rep] = crep;
+    }
+}
+
+// Count + fused tile union on clique grids with the fp32 tile records above (the fp64
+// count_tile_kernel<.., true> runs the other grids; each exits at once on the other's).
+template <int CAP, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
+    const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
+    int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate,
+    FuseArgs fa) {
+    const GridParams g = *fa.gp;
+    if (!g.clique || ablate == 4) {  // count_tile_kernel counts this grid
+        if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
+        return;
+    }
+    __shared__ TileStage st;
+    __shared__ float2 buf[CAP];
+    __shared__ int wcores[kBlock / 64];
+    __shared__ int rowoff[9];
+    __shared__ __attribute__((aligned(16))) uint32_t lsts[kMaxNbr * kBlock];
+    __shared__ uint32_t lcore[(CAP + 31) / 32 + 1];
+    static_assert(CAP < 2048, "LDS ranges are packed in 11 bits");
+    static_assert(sizeof(UnionLds) <= sizeof(lsts), "UnionLds must fit");
+    uint32_t* lst = lsts + threadIdx.x;
+    const int ntiles = *ntiles_p;
+    const F32Cut cut = f32_cut(g, eps2);
+    int mine = 0;
+    // the medium tiles (tile_class_kernel): each fits the staging capacity
+    const int nt = fa.tl.n[kTileMedium];
+    const auto tile_at = [&](int k) { return k < nt ? fa.tl.medium[k] : ntiles; };
+    StageMeta meta = stage_meta(tile_at(blockIdx.x), ntiles, tstage, tstart, fa.tq);
+    for (int k = blockIdx.x; k < nt; k += gridDim.x) {
+        const int t = tile_at(k);
+        if (threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
+        const uint32_t tk = fa.tkey[t];
+        const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
+        const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
+        stage_build32<CAP>(meta, xy, st, buf, g, ox, oy);
+        meta = stage_meta(tile_at(k + gridDim.x), ntiles, tstage, tstart, fa.tq);
+        const int q0 = st.q0, nq = st.nq;
+        int qb = 0, qe = 0;
+        uint32_t qk = 0;
+        if ((int)threadIdx.x < nq) {
+            qb = fa.qstart[q0 + threadIdx.x];
+            qe = fa.qstart[q0 + threadIdx.x + 1];
+            qk = fa.qkey[q0 + threadIdx.x];
+        }
+        {
+            if (threadIdx.x == 0) {
+                int acc = 0;
+                for (int r = 0; r < 8; ++r) {
+                    rowoff[r] = acc;
+                    acc += st.off[(r + 1) * 10 + 9] - st.off[(r + 1) * 10 + 1];
+                }
+                rowoff[8] = acc;
+            }
+            __syncthreads();
+            const int own = rowoff[8];
+            for (int i = (int)threadIdx.x; i < own; i += kBlock) {
+                int r = 0;
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (r + s < 8 && rowoff[r + s] <= i) r += s;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - rowoff[r]);
+                int ex = 0;
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
+                const int p = st.cb[base + ex] + (j - st.off[base + ex]);
+                bool is_core = true;
+                if (min_points > 0 && ablate != 1) {
+                    const int l = r * 8 + ex;
+                    const float2 me = buf[j];
+                    const LdsRanges rg = lds_ranges(st, l);
+                    const auto exact = [&](int q) {
+                        const double2 a = xy[p], o = xy[stage_slot(st, q)];
+                        return within_eps(a.x, a.y, o.x, o.y, eps2);
+                    };
+                    int cnt = 0, nrec = 0;
+                    const int k_rec = ablate == 2 ? 0 : nbr_k;
+                    bool done = scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points, cnt,
+                                                   lst, nrec, k_rec, 0, exact);
+#pragma unroll
+                    for (int k = 0; k < 3 && !done; ++k) {
+                        const int lo = rg.b[k], hi = rg.e[k];
+                        if (lo <= rg.cs && rg.ce <= hi) {
+                            done = scan_count32<true>(buf, lo, rg.cs, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact) ||
+                                   scan_count32<true>(buf, rg.ce, hi, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact);
+                        } else {
+                            done = scan_count32<true>(buf, lo, hi, me, cut, min_points, cnt, lst,
+                                                      nrec, k_rec, k, exact);
+                        }
+                    }
+                    is_core = cnt >= min_points;
+                    if (!is_core && k_rec > 0) {
+                        // the non-core's neighbours (self excluded), -1 terminated
+                        int32_t* out = nbr + (int64_t)p * nbr_k;
+                        int w = 0;
+                        for (int rr = 0; rr < nrec; ++rr) {
+                            const uint32_t v = lst[rr * kBlock];
+                            const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
+                            const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
+                            for (uint32_t m = v >> 16; m; m &= m - 1) {
+                                const int qq = q + __ffs(m) - 1;
+                                const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
+                                              (qq >= st.off[k0 + 2] ? 1 : 0);
+                                const int sq = st.cb[c] + (qq - st.off[c]);
+                                if (sq != p) out[w++] = sq;
+                            }
+                        }
+                        if (w < nbr_k) out[w] = -1;
+                    }
+                }
+                if (is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
+            }
+            __syncthreads();
+            fused_tile_union32(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
+                               *reinterpret_cast<UnionLds*>(lsts), ablate);
+        }
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        block_cores[blockIdx.x] = tot;
+    }
+}
+
+// Small clique-grid tiles (tile + halo <= kSmallCap points; most tiles of a clustered set are
+// sparse ones at cluster edges): ONE WAVE per tile, the same stage / count / quarter union as
+// count_tile32_kernel with wave syncs instead of workgroup barriers, so the four waves of a
+// workgroup work on four tiles independently and a tile's latency chain (stage loads, scans,
+// union) never waits for a slower tile.
+constexpr int kWaveQ = kSmallCap;  // quarters of a small tile (each holds >= 1 own point)
+
+struct WaveUnion {  // per wave, aliases the count's neighbour records
+    int lp[kWaveQ];
+    uint32_t lrange[kWaveQ];
+    uint32_t lmask[kWaveQ];
+    unsigned long long cmin[kWaveQ];
+    uint16_t qmap[kMaxTileQ];
+};
+
+struct WaveTile {
+    TileStage st;
+    int rowoff[9];
+    uint32_t lcore[kSmallCap / 32 + 1];
+    float2 buf[kSmallCap];
+    union {
+        uint32_t rec[kMaxNbr * 64];
+        WaveUnion u;
+    };
+};
+
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
+    const int2* __restrict__ tstage, double eps2, int32_t min_points,
+    uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, FuseArgs fa) {
+    __shared__ WaveTile wt[kBlock / 64];
+    __shared__ int wcores[kBlock / 64];
+    const GridParams g = *fa.gp;
+    const int lane = __lane_id(), w = threadIdx.x >> 6;
+    WaveTile& T = wt[w];
+    TileStage& st = T.st;
+    WaveUnion& u = T.u;
+    int mine = 0;
+    if (g.clique) {
+        const F32Cut cut = f32_cut(g, eps2);
+        const int nt = fa.tl.n[kTileSmall];
+        for (int k = blockIdx.x * (kBlock / 64) + w; k < nt; k += gridDim.x * (kBlock / 64)) {
+            const int t = fa.tl.small[k];
+            // stage table: extended cells lane and lane + 64, scanned across the wave
+            const int2 m0 = tstage[(int64_t)t * 100 + lane];
+            const int2 m1 = lane < 36 ? tstage[(int64_t)t * 100 + 64 + lane] : make_int2(0, 0);
+            const uint32_t tk = fa.tkey[t];
+            const int q0 = fa.tq[(int64_t)t * kTslot], nq = fa.tq[(int64_t)t * kTslot + 64] - q0;
+            int i0 = m0.y, i1 = m1.y;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v0 = __shfl_up(i0, o, 64), v1 = __shfl_up(i1, o, 64);
+                if (lane >= o) {
+                    i0 += v0;
+                    i1 += v1;
+                }
+            }
+            const int tot0 = __shfl(i0, 63, 64), total = tot0 + __shfl(i1, 63, 64);
+            st.cb[lane] = m0.x;
+            st.off[lane] = i0 - m0.y;
+            if (lane < 36) {
+                st.cb[64 + lane] = m1.x;
+                st.off[64 + lane] = tot0 + i1 - m1.y;
+            }
+            if (lane == 0) st.off[100] = total;
+            if (lane < kSmallCap / 32 + 1) T.lcore[lane] = 0u;
+            wave_sync();
+            {
+                const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
+                const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
+#pragma unroll
+                for (int uu = 0; uu < kSmallCap / 64; ++uu) {
+                    const int e = lane + uu * 64;
+                    if (e < total) {
+                        int c = 0;
+#pragma unroll
+                        for (int sh = 64; sh > 0; sh >>= 1)
+                            if (c + sh < 100 && st.off[c + sh] <= e) c += sh;
+                        const double2 v = xy[st.cb[c] + (e - st.off[c])];
+                        T.buf[e] = make_float2((float)((v.x * 0.5 - g.xmin2) * g.invx - ox),
+                                               (float)((v.y * 0.5 - g.ymin2) * g.invy - oy));
+                    }
+                }
+            }
+            if (lane < 8) {  // own points per tile row, prefix over the rows
+                const int rs = st.off[(lane + 1) * 10 + 9] - st.off[(lane + 1) * 10 + 1];
+                int incl = rs;
+#pragma unroll
+                for (int o = 1; o < 8; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                T.rowoff[lane] = incl - rs;
+                if (lane == 7) T.rowoff[8] = incl;
+            }
+            wave_sync();
+            const int own = T.rowoff[8];
+            for (int i = lane; i < own; i += 64) {
+                int r = 0;
+#pragma unroll
+                for (int sh = 4; sh > 0; sh >>= 1)
+                    if (r + sh < 8 && T.rowoff[r + sh] <= i) r += sh;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - T.rowoff[r]);
+                int ex = 0;
+#pragma unroll
+                for (int sh = 4; sh > 0; sh >>= 1)
+                    if (ex + sh < 8 && st.off[base + ex + sh] <= j) ex += sh;
+                const int p = st.cb[base + ex] + (j - st.off[base + ex]);
+                bool is_core = true;
+                if (min_points > 0) {
+                    const float2 me = T.buf[j];
+                    const LdsRanges rg = lds_ranges(st, r * 8 + ex);
+                    const auto exact = [&](int q) {
+                        const double2 a = xy[p], o = xy[stage_slot(st, q)];
+                        return within_eps(a.x, a.y, o.x, o.y, eps2);
+                    };
+                    uint32_t* lst = T.rec + lane;
+                    int cnt = 0, nrec = 0;
+                    bool done = scan_count32<true, 64>(T.buf, rg.cs, rg.ce, me, cut, min_points,
+                                                       cnt, lst, nrec, nbr_k, 0, exact);
+#pragma unroll
+                    for (int kk = 0; kk < 3 && !done; ++kk) {
+                        const int lo = rg.b[kk], hi = rg.e[kk];
+                        if (lo <= rg.cs && rg.ce <= hi) {
+                            done = scan_count32<true, 64>(T.buf, lo, rg.cs, me, cut, min_points,
+                                                          cnt, lst, nrec, nbr_k, kk, exact) ||
+                                   scan_count32<true, 64>(T.buf, rg.ce, hi, me, cut, min_points,
+                                                          cnt, lst, nrec, nbr_k, kk, exact);
+                        } else {
+                            done = scan_count32<true, 64>(T.buf, lo, hi, me, cut, min_points, cnt,
+                                                          lst, nrec, nbr_k, kk, exact);
+                        }
+                    }
+                    is_core = cnt >= min_points;
+                    if (!is_core && nbr_k > 0) {
+                        int32_t* out = nbr + (int64_t)p * nbr_k;
+                        int wn = 0;
+                        for (int rr = 0; rr < nrec; ++rr) {
+                            const uint32_t v = lst[rr * 64];
+                            const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
+                            const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
+                            for (uint32_t m = v >> 16; m; m &= m - 1) {
+                                const int qq = q + __ffs(m) - 1;
+                                const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
+                                              (qq >= st.off[k0 + 2] ? 1 : 0);
+                                const int sq = st.cb[c] + (qq - st.off[c]);
+                                if (sq != p) out[wn++] = sq;
+                            }
+                        }
+                        if (wn < nbr_k) out[wn] = -1;
+                    }
+                }
+                if (is_core) atomicOr(&T.lcore[j >> 5], 1u << (j & 31));
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
+            }
+            wave_sync();
+            // quarter records + union over the tile's quarters (fused_tile_union32, per wave)
+            for (int idx = lane; idx < kMaxTileQ; idx += 64) u.qmap[idx] = 0xFFFF;
+            for (int idx = lane; idx < kWaveQ; idx += 64) u.cmin[idx] = ~0ull;
+            wave_sync();
+            int rep[kWaveQ / 64], best[kWaveQ / 64];
+#pragma unroll
+            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
+                const int qi = lane + pp * 64;
+                rep[pp] = -1;
+                best[pp] = 0x7FFFFFFF;
+                if (qi < nq) {
+                    const int b = fa.qstart[q0 + qi], e = fa.qstart[q0 + qi + 1];
+                    const uint32_t key = fa.qkey[q0 + qi];
+                    uint32_t cx, cy;
+                    cell_xy(key >> 2, g.ntx, cx, cy);
+                    const int gx = (int)(2 * cx + (key & 1u)), gy = (int)(2 * cy + ((key >> 1) & 1u));
+                    const int lq = (gy & 15) * 16 + (gx & 15);
+                    const int len = e - b;
+                    const int l = (int)((key >> 2) & 63u);
+                    const int kc = ((l >> 3) + 1) * 10 + (l & 7) + 1;
+                    const int jb = st.off[kc] + (b - st.cb[kc]);
+                    // len <= 32: a small tile's quarter rarely holds more; else scan the bits
+                    uint32_t mask = 0;
+                    int first = -1;
+                    for (int jj = 0; jj < len && (jj < 32 || first < 0); ++jj)
+                        if ((T.lcore[(jb + jj) >> 5] >> ((jb + jj) & 31)) & 1u) {
+                            if (jj < 32) mask |= 1u << jj;
+                            if (first < 0) first = jj;
+                        }
+                    if (first >= 0) {
+                        rep[pp] = b + first;
+                        best[pp] = fa.perm[rep[pp]];
+                    }
+                    fa.qinfo[q0 + qi] = make_int4(b, e, rep[pp], (int)mask);
+                    fa.qg[q0 + qi] = make_int4(gx, gy, best[pp], 0);
+                    u.lp[qi] = qi;
+                    u.lrange[qi] = (rep[pp] >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) |
+                                   (uint32_t)jb | ((uint32_t)len << 11);
+                    u.lmask[qi] = mask;
+                    u.qmap[lq] = (uint16_t)qi;
+                }
+            }
+            wave_sync();
+            const auto is_core_l = [&](int j) { return ((T.lcore[j >> 5] >> (j & 31)) & 1u) != 0; };
+            const auto exact2 = [&](int qa, int qb) {
+                const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
+                return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
+            };
+            for (int sweep = 0; sweep < 2; ++sweep) {
+                const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
+                for (int it = lane; it < nq * nofs; it += 64) {
+                    const int o = it / nq, qi = it - o * nq;
+                    const uint32_t ri = u.lrange[qi];
+                    if (!(ri >> 31)) continue;
+                    const int lq = (int)((ri >> 22) & 255u);
+                    const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+                    if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+                    const int j = u.qmap[uy * 16 + ux];
+                    if (j == 0xFFFF) continue;
+                    const uint32_t rj = u.lrange[j];
+                    if (!(rj >> 31)) continue;
+                    if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                    const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
+                    const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
+                    if (quarters_touch32(T.buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j],
+                                         is_core_l, cut, exact2))
+                        lunite(u.lp, qi, j);
+                }
+                wave_sync();
+            }
+            int rr[kWaveQ / 64];
+#pragma unroll
+            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
+                const int qi = lane + pp * 64;
+                rr[pp] = -1;
+                if (qi < nq && rep[pp] >= 0) {
+                    rr[pp] = lfind(u.lp, qi);
+                    atomicMin(&u.cmin[rr[pp]],
+                              ((unsigned long long)(uint32_t)best[pp] << 32) | (uint32_t)rep[pp]);
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
+                const int qi = lane + pp * 64;
+                if (qi < nq) {
+                    const int crep =
+                        rr[pp] >= 0 ? (int)(uint32_t)(u.cmin[rr[pp]] & 0xFFFFFFFFull) : -1;
+                    fa.qcomp[q0 + qi] = crep;
+                    if (rep[pp] >= 0) parent[rep[pp]] = crep;
+                }
+            }
+            wave_sync();
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (lane == 0) wcores[w] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int v = 0; v < kBlock / 64; ++v) tot += wcores[v];
+        block_cores[blockIdx.x] = tot;
+    }
+}
+
+// Clique-grid tiles over the fp32 staging capacity (big_tiles_kernel's list): their points'
+// counts from global memory, spread over kBigChunks workgroups per tile (such tiles are the
+// dense cores of clusters: thousands of points each), then each tile's quarter union.
+constexpr int kBigChunks = 8;
+
+template <int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart, double eps2,
+    int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ block_cores,
+    int32_t* __restrict__ nbr, int nbr_k, FuseArgs fa) {
+    __shared__ int wcores[kBlock / 64];
+    __shared__ TileStage st;  // (unused by the global-memory count)
+    int mine = 0;
+    if (fa.gp->clique) {
+        const int nb = fa.tl.n[kTileBig];
+        for (int k = blockIdx.x; k < nb * kBigChunks; k += gridDim.x) {
+            const int t = fa.tl.big[k / kBigChunks], c = k % kBigChunks;
+            const int te = tstart[t + 1];
+            for (int p = tstart[t] + c * kBlock + (int)threadIdx.x; p < te;
+                 p += kBigChunks * kBlock) {
+                const bool is_core =
+                    min_points <= 0 ||
+                    count_point<false>(st, nullptr, xy, cell,
+                                       seg, 0, 0, p, eps2, min_points, nullptr, nbr, nbr_k);
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        block_cores[blockIdx.x] = tot;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void big_union_kernel(const double2* __restrict__ xy,
+                                                           const uint8_t* __restrict__ core,
+                                                           double eps2,
+                                                           int32_t* __restrict__ parent,
+                                                           FuseArgs fa, int ablate) {
+    const GridParams g = *fa.gp;
+    if (!g.clique) return;
+    __shared__ UnionLds u;
+    __shared__ TileStage st;  // (unused by the global-memory union)
+    const int nb = fa.tl.n[kTileBig];
+    for (int k = blockIdx.x; k < nb; k += gridDim.x) {
+        const int t = fa.tl.big[k];
+        const int q0 = fa.tq[(int64_t)t * kTslot], nq = fa.tq[(int64_t)t * kTslot + 64] - q0;
+        int qb = 0, qe = 0;
+        uint32_t qk = 0;
+        if ((int)threadIdx.x < nq) {
+            qb = fa.qstart[q0 + threadIdx.x];
+            qe = fa.qstart[q0 + threadIdx.x + 1];
+            qk = fa.qkey[q0 + threadIdx.x];
+        }
+        fused_tile_union<false>(q0, nq, qb, qe, qk, fa, g, st, nullptr, nullptr, xy, core, eps2,
+                                parent, u, ablate);
+        __syncthreads();
     }
 }
 
@@ -1723,6 +2520,14 @@ static int count_cap() {
     }();
     return v;
 }
+// DBSCAN_F32=0: count clique grids with the fp64 staging (A/B measurements)
+static bool f32_count() {
+    static const bool v = [] {
+        const char* e = std::getenv("DBSCAN_F32");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 // DBSCAN_FUSE=0: run quarter_init and tile_union as their own kernels (A/B measurements)
 static bool fuse_union() {
     static const bool v = [] {
@@ -1876,8 +2681,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     // per-tile kernels: grid stride over occupied tiles (their count stays on the device)
     const unsigned tile_grid = (unsigned)std::min<int64_t>(ntile_bound, kTileGrid);
     const unsigned rest_grid = std::min(nblk(n), 1024u);  // slots [nf, n): outside the grid
+    // clique grids: the fp32-record count (count_tile32_kernel); DBSCAN_F32=0 keeps the fp64
+    // one for A/B measurements
+    const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
+    // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
+    // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
-        ws.blockcnt.ensure(2 * ((size_t)tile_grid + rest_grid + 1) * sizeof(int32_t)));
+        ws.blockcnt.ensure(2 * ((size_t)4 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
     const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
@@ -1891,17 +2701,50 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 case 1024: kern = count_tile_kernel<1024, 5, false>; break;
                 default: break;
             }
-            const FuseArgs fa{tq, qstart, qkey, perm, gp, qinfo, qg, qcomp};
-            klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg, tstart,
-                               tstage, &st[kStTiles], eps2, a.min_points, core,
-                               parent, block_cores, nbr, nbr_k, count_ablate(), fa);
+            TileLists tl{};
+            if (f32) {
+                int32_t* lists =
+                    static_cast<int32_t*>(ws.bigt.ensure(3 * ntile_bound * sizeof(int32_t)));
+                tl = TileLists{&st[kStTileLists], lists, lists + ntile_bound,
+                               lists + 2 * ntile_bound};
+            }
+            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, qinfo, qg, qcomp};
+            if (f32) {
+                // clique grids by tile stage size: small tiles one wave each (count_wave),
+                // medium one workgroup each (count32), big from global memory (big_count +
+                // big_union); other grids: count (fp64)
+                klaunch(prof, "tile_class", tile_class_kernel<1536>,
+                        dim3((unsigned)std::min<int64_t>((ntile_bound + 63) / 64, 2048)),
+                        dim3(kBlock), 0, s, tstage, &st[kStTiles], gp, tl);
+                klaunch(prof, "count_wave", count_wave_kernel<5>, dim3(tile_grid), dim3(kBlock),
+                        0, s, xy, tstart, tstage, eps2, a.min_points, core, parent,
+                        block_cores + 3 * tile_grid, nbr, nbr_k, fa);
+                auto k32 =
+                    union_w() == 5 ? count_tile32_kernel<1536, 5> : count_tile32_kernel<1536, 6>;
+                klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
+                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
+                        block_cores, nbr, nbr_k, count_ablate(), fa);
+                klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,
+                        s, xy, cell, seg, tstart, eps2, a.min_points, core,
+                        block_cores + tile_grid, nbr, nbr_k, fa);
+                klaunch(prof, "big_union", big_union_kernel, dim3(2048), dim3(kBlock), 0, s, xy,
+                        (const uint8_t*)core, eps2, parent, fa, count_ablate());
+                klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
+                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
+                        block_cores + 2 * tile_grid, nbr, nbr_k, count_ablate(), fa);
+            } else {
+                klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
+                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
+                        block_cores, nbr, nbr_k, count_ablate(), fa);
+            }
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
+        const int64_t nmain = (f32 ? 4 : 1) * (int64_t)tile_grid;
         klaunch(prof, "count_rest", count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
-                           a.min_points, core, parent, block_cores + tile_grid);
+                           a.min_points, core, parent, block_cores + nmain);
         DBSCAN_HIP_CHECK(hipGetLastError());
-        const int64_t nb = (int64_t)tile_grid + rest_grid;
+        const int64_t nb = nmain + rest_grid;
         exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan);
         if (a.zone)  // (the core count above then includes zone-2 points: a statistic only)
             klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,

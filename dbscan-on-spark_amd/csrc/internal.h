@@ -49,6 +49,7 @@ enum FitState {
     kStNf = 6,        // points inside the grid (finite coordinates)
     kStBits = 7,      // radix key width
     kStError = 8,     // the eps grid could not be sized
+    kStTileLists = 9,  // [3] clique-grid tiles per count path: small, medium, big
     kStCount = 16
 };
 
@@ -145,7 +146,7 @@ struct ScanState {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag;
+        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -157,7 +158,7 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag})
+                          &own_flag, &bigt})
             b->release();
     }
 };
