@@ -167,6 +167,17 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
     if (p < *nf_p) xy[p] = make_double2(x[i], y[i]);
 }
 
+// Slab fits: the zone-2 points (count candidates, never core) marked in sorted order (zs,
+// zeroed before), so the fused count kernels know them before their tile unions.  Zone 2 is a
+// thin band: a coalesced zone read per point, a scattered write per zone-2 point only.
+__global__ __launch_bounds__(kBlock) void zone_mark_kernel(int64_t n,
+                                                           const uint8_t* __restrict__ zone,
+                                                           const int32_t* __restrict__ inv,
+                                                           uint8_t* __restrict__ zs) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && zone[i] == 2) zs[inv[i]] = 2;
+}
+
 // Occupied tiles, eps cells and quarter cells in one pass over the sorted keys (they are
 // nested prefixes of the key: tile = key >> 8, cell = key >> 2, quarter = key).  A head flag
 // marks the first slot of each group; groups are numbered by an exclusive scan of the flags:
@@ -844,6 +855,7 @@ struct FuseArgs {
     const GridParams* gp;
     int f32;                 // clique grids are counted by count_tile32_kernel
     TileLists tl;            // f32: clique-grid tiles by stage size (tile_class_kernel)
+    const uint8_t* zs;       // slab fits: zone per sorted slot (2: candidate only, never core)
     int4* qinfo;             // out: (begin, end, rep, core mask) per quarter
     int4* qg;                // out: (quarter-grid x, y, min visit index of its cores, 0)
     int32_t* qcomp;          // out: tile component rep per quarter (-1: no cores)
@@ -1487,7 +1499,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                         }
                     }
                     is_core = cnt >= min_points;
-                    if (!is_core && k_rec > 0) {
+                    if (!is_core && k_rec > 0) {  // (a complete list: cnt < minPoints)
                         // the non-core's neighbours (self excluded), -1 terminated
                         int32_t* out = nbr + (int64_t)p * nbr_k;
                         int w = 0;
@@ -1506,6 +1518,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                         if (w < nbr_k) out[w] = -1;
                     }
                 }
+                if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
                 if (is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
@@ -1681,6 +1694,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                         if (wn < nbr_k) out[wn] = -1;
                     }
                 }
+                if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
                 if (is_core) atomicOr(&T.lcore[j >> 5], 1u << (j & 31));
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
@@ -1813,9 +1827,10 @@ __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
             for (int p = tstart[t] + c * kBlock + (int)threadIdx.x; p < te;
                  p += kBigChunks * kBlock) {
                 const bool is_core =
-                    min_points <= 0 ||
-                    count_point<false>(st, nullptr, xy, cell,
-                                       seg, 0, 0, p, eps2, min_points, nullptr, nbr, nbr_k);
+                    (min_points <= 0 ||
+                     count_point<false>(st, nullptr, xy, cell, seg, 0, 0, p, eps2, min_points,
+                                        nullptr, nbr, nbr_k)) &&
+                    !(fa.zs && fa.zs[p] == 2);  // slab halo: candidate only
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
             }
@@ -2621,9 +2636,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* qstart = static_cast<int32_t*>(ws.qstart.ensure((n + 1) * sizeof(int32_t)));
     int4* qinfo = static_cast<int4*>(ws.qrep.ensure(n * sizeof(int4)));
     int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
-    // plain fits: the tile-local quarter union runs inside the count kernel (slab fits clear
-    // zone-2 core flags after the count, so their unions must come later)
-    const bool fuse = mode == kGridEps && !a.zone && fuse_union() && count_cap() == 0;
+    // the tile-local quarter union runs inside the count kernels (slab fits: the fp32 count
+    // kernels, which read the sorted zones; the fp64 fused kernel would union zone-2 points)
+    const bool fuse =
+        mode == kGridEps && fuse_union() && count_cap() == 0 && (!a.zone || f32_count());
+    uint8_t* zs = (a.zone && fuse) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
 
     {
         StageTimer t(prof, s, "gather");
@@ -2633,6 +2650,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         if (mode != kGridNoPairs)
             klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);
+        if (zs) {
+            DBSCAN_HIP_CHECK(hipMemsetAsync(zs, 0, n, s));
+            klaunch(prof, "zone_mark", zone_mark_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
+                    a.zone, inv, zs);
+        }
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     if (mode != kGridNoPairs) {
@@ -2708,12 +2730,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 tl = TileLists{&st[kStTileLists], lists, lists + ntile_bound,
                                lists + 2 * ntile_bound};
             }
-            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, qinfo, qg, qcomp};
+            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp};
             if (f32) {
                 // clique grids by tile stage size: small tiles one wave each (count_wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
                 // big_union); other grids: count (fp64)
-                klaunch(prof, "tile_class", tile_class_kernel<1536>,
+                const bool cap2k = union_w() == 2047;  // (A/B: count32 capacity 2047)
+                klaunch(prof, "tile_class", cap2k ? tile_class_kernel<2047> : tile_class_kernel<1536>,
                         dim3((unsigned)std::min<int64_t>((ntile_bound + 63) / 64, 2048)),
                         dim3(kBlock), 0, s, tstage, &st[kStTiles], gp, tl);
                 klaunch(prof, "count_wave", count_wave_kernel<5>, dim3(tile_grid), dim3(kBlock),
@@ -2721,6 +2744,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         block_cores + 3 * tile_grid, nbr, nbr_k, fa);
                 auto k32 =
                     union_w() == 5 ? count_tile32_kernel<1536, 5> : count_tile32_kernel<1536, 6>;
+                if (cap2k) k32 = count_tile32_kernel<2047, 5>;
                 klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
                         tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
                         block_cores, nbr, nbr_k, count_ablate(), fa);
@@ -2817,7 +2841,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "final");
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
-                               parent, (const int32_t*)nullptr, qinfo, lab,
+                               parent, fuse ? qidx : nullptr, qinfo, lab,
                                (unsigned long long*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
