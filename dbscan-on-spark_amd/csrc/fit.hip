@@ -2146,6 +2146,9 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
     __shared__ int ncomp[kBlock / 64][kEdgeNodes];
     __shared__ int nlp[kBlock / 64][kEdgeNodes];
+    // facing nodes by position along the strip: facing cell f (0..7; the corner cell is f = 8
+    // on side 0, f = -1 on side 1) holds nodes [fnb[f + 1], fne[f + 1])
+    __shared__ int fnb[kBlock / 64][10], fne[kBlock / 64][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
@@ -2183,6 +2186,16 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             }
             nA = __shfl(incl, 7, 64);
             ntot = __shfl(incl, 16, 64);
+            if (lane < 10) {
+                fnb[w][lane] = 0;
+                fne[w][lane] = 0;
+            }
+            wave_sync();
+            if (lane >= 8 && lane <= 16) {
+                const int f = lane < 16 ? k : (side ? -1 : 8);
+                fnb[w][f + 1] = incl - cnt;
+                fne[w][f + 1] = incl;
+            }
             for (int j = 0; j < cnt; ++j) {
                 const int idx = incl - cnt + j;
                 nqi[w][idx] = qinfo[q0 + j];
@@ -2211,9 +2224,13 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             if (me.z >= 0) {
                 double px[kQReg], py[kQReg];
                 const int na = load_own(xy, me, 0, px, py);
+                // only facing cells within quarter distance 2 along the strip
+                const int ua = (side ? mg.x : mg.y) & 15;
+                const int flo = (ua - 2) >> 1, fhi = (ua + 2) >> 1;
 #pragma unroll
                 for (int sweep = 1; sweep <= 2; ++sweep)
-                    for (int b = nA + half; b < ntot; b += 2) {
+                    for (int f = flo; f <= fhi; ++f)
+                    for (int b = fnb[w][f + 1] + half; b < fne[w][f + 1]; b += 2) {
                         const int2 og = ngq[w][b];
                         if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
                         const int4 o = nqi[w][b];
