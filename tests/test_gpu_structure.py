@@ -114,3 +114,26 @@ def test_single_tile_and_single_row(dm, handle):
     x = rng.uniform(0, 500, 20000)
     y = rng.uniform(0, 0.1, 20000)
     _check(dm, handle, x, y, 0.3, 5)  # one row of cells, many tiles along x
+
+
+@pytest.mark.parametrize("div,mp", [(1, 5), (1, 3), (3, 29), (3, 10), (5, 40)])
+def test_lattice_pairs_at_exactly_eps(dm, handle, div, mp):
+    """Lattices of spacing eps/div: every point has lattice neighbours at distance eps exactly
+    (up to the fp64 rounding of the coordinates), so the fp32 cell-unit pre-filter of the
+    clique-grid count and pair tests (count_wave / count32) finds them ambiguous and the exact
+    fp64 predicate decides -- core flags hinge on those pairs when minPoints equals the lattice
+    disc count.  div 1: small tiles (one wave each); div 3 / 5: medium and big tiles.  Offsets
+    of 1e3 and a few one-ulp nudges make the fp64 differences round both ways."""
+    eps = 0.3
+    rng = np.random.default_rng(div * 100 + mp)
+    side = {1: 120, 3: 150, 5: 160}[div]
+    i, j = np.meshgrid(np.arange(side), np.arange(side), indexing="ij")
+    x = 1e3 + i.ravel() * (eps / div)
+    y = -2e3 + j.ravel() * (eps / div)
+    k = rng.choice(x.size, x.size // 10, replace=False)
+    x[k] = np.nextafter(x[k], np.where(rng.random(k.size) < 0.5, -np.inf, np.inf))
+    k = rng.choice(y.size, y.size // 10, replace=False)
+    y[k] = np.nextafter(y[k], np.where(rng.random(k.size) < 0.5, -np.inf, np.inf))
+    p = rng.permutation(x.size)
+    _check(dm, handle, x[p].copy(), y[p].copy(), eps, mp)
+    assert handle.stats()["clique"] == 1
