@@ -365,10 +365,13 @@ __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict
                                                       const int32_t* __restrict__ tmap,
                                                       const int32_t* __restrict__ tslot,
                                                       const GridParams* __restrict__ gp,
-                                                      Seg* __restrict__ seg) {
+                                                      Seg* __restrict__ seg,
+                                                      const uint8_t* __restrict__ tclass) {
     const int c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= *ncells_p) return;
     const GridParams g = *gp;
+    // tclass (clique grids, neighbour lists kept): only the big tiles' cells read their pieces
+    if (tclass && g.clique && tclass[tmap[ckey[c] >> 6]] != 2) return;
     uint32_t cx, cy;
     cell_xy(ckey[c], g.ntx, cx, cy);
     const uint32_t lox = cx > 0 ? cx - 1 : cx, hix = cx + 1 < g.nx ? cx + 1 : cx;
@@ -424,39 +427,56 @@ struct TileStage {
 };
 
 // tstage[t][k] = (first slot, point count) of extended cell k of tile t: the staging table of
-// the per-tile kernels, so that staging a tile is one coalesced load per extended cell.
+// the per-tile kernels, so that staging a tile is one coalesced load per extended cell.  One
+// wave per tile (cells lane and lane + 64); tsz[t] = the stage's point count.
+__device__ __forceinline__ int2 tstage_entry(const GridParams& g, const int32_t* __restrict__ tmap,
+                                             const int32_t* __restrict__ tslot, int tx0,
+                                             int ty0, int k) {
+    const int ey = k / 10 - 1, ex = k % 10 - 1;
+    const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
+    const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
+    const int occ = tile_occ(tmap, g, tx, ty);
+    int b = 0, cnt = 0;
+    if (occ >= 0) {
+        const int l = (ey & 7) * 8 + (ex & 7);
+        b = tslot[(int64_t)occ * kTslot + l];
+        cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
+    }
+    return make_int2(b, cnt);
+}
+
 __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restrict__ tkey,
                                                         const int32_t* __restrict__ ntiles_p,
                                                         const int32_t* __restrict__ tmap,
                                                         const int32_t* __restrict__ tslot,
                                                         const GridParams* __restrict__ gp,
-                                                        int2* __restrict__ tstage) {
-    const int k = threadIdx.x & 127;
-    if (k >= 100) return;
+                                                        int2* __restrict__ tstage,
+                                                        int32_t* __restrict__ tsz) {
+    const int lane = threadIdx.x & 63;
     const GridParams g = *gp;
     const int ntiles = *ntiles_p;
-    for (int t = blockIdx.x * 2 + (threadIdx.x >> 7); t < ntiles; t += gridDim.x * 2) {
+    for (int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < ntiles;
+         t += gridDim.x * (kBlock / 64)) {
         const uint32_t tk = tkey[t];
         const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
-        const int ey = k / 10 - 1, ex = k % 10 - 1;
-        const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
-        const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
-        const int occ = tile_occ(tmap, g, tx, ty);
-        int b = 0, cnt = 0;
-        if (occ >= 0) {
-            const int l = (ey & 7) * 8 + (ex & 7);
-            b = tslot[(int64_t)occ * kTslot + l];
-            cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
-        }
-        tstage[(int64_t)t * 100 + k] = make_int2(b, cnt);
+        const int2 e0 = tstage_entry(g, tmap, tslot, tx0, ty0, lane);
+        const int2 e1 = lane < 36 ? tstage_entry(g, tmap, tslot, tx0, ty0, 64 + lane)
+                                  : make_int2(0, 0);
+        tstage[(int64_t)t * 100 + lane] = e0;
+        if (lane < 36) tstage[(int64_t)t * 100 + 64 + lane] = e1;
+        int c = e0.y + e1.y;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) tsz[t] = c;
     }
 }
 
 // Clique grids: tiles by the size of their tile + halo stage (the tstage counts), listed for
 // the three count paths: small (<= kSmallCap points: count_wave_kernel, one wave per tile),
 // medium (<= CAP: count_tile32_kernel, one workgroup per tile) and big (over CAP:
-// big_count_kernel + big_union_kernel, global memory).  64 tiles per workgroup; one atomic
-// per class and workgroup.
+// big_count_kernel + big_union_kernel, global memory).  One tile per lane; one atomic per
+// class and workgroup of 1024 tiles.  tclass[t] keeps the class (segs_kernel builds stencil pieces for the big
+// tiles only).
 enum TileClass { kTileSmall = 0, kTileMedium = 1, kTileBig = 2, kTileNone = 3 };
 constexpr int kSmallCap = 192;
 
@@ -467,50 +487,54 @@ struct TileLists {
     int32_t* big;
 };
 
+constexpr int kClassRounds = 4;  // tile_class_kernel: 64 tiles per lane round, 1024 per block
+
 template <int CAP>
-__global__ __launch_bounds__(kBlock) void tile_class_kernel(const int2* __restrict__ tstage,
+__global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __restrict__ tsz,
                                                             const int32_t* __restrict__ ntiles_p,
                                                             const GridParams* __restrict__ gp,
-                                                            TileLists tl) {
+                                                            TileLists tl,
+                                                            uint8_t* __restrict__ tclass) {
     if (!gp->clique) return;
-    __shared__ uint8_t cls[64];
+    __shared__ int wcnt[3][kBlock / 64];
+    __shared__ int bbase[3];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ntiles = *ntiles_p;
-    for (int base = blockIdx.x * 64; base < ntiles; base += gridDim.x * 64) {
-        int c[16];
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int base = blockIdx.x * kBlock * kClassRounds; base < ntiles;
+         base += gridDim.x * kBlock * kClassRounds) {  // block-uniform loop
+        int v[kClassRounds];
+        int cnt[3] = {0, 0, 0};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {  // 16 tiles per wave, all loads in flight together
-            const int t = base + w * 16 + r;
-            c[r] = 0;
+        for (int r = 0; r < kClassRounds; ++r) {  // tile = base + (r * 4 + w) * 64 + lane
+            const int t = base + (r * (kBlock / 64) + w) * 64 + lane;
+            v[r] = kTileNone;
             if (t < ntiles) {
-                c[r] = tstage[(int64_t)t * 100 + lane].y;
-                if (lane < 36) c[r] += tstage[(int64_t)t * 100 + 64 + lane].y;
+                const int c = tsz[t];
+                v[r] = c <= kSmallCap ? kTileSmall : (c <= CAP ? kTileMedium : kTileBig);
+                tclass[t] = (uint8_t)v[r];
             }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cnt[k] += __popcll(__ballot(v[r] == k));
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) c[r] += __shfl_xor(c[r], o, 64);
-            if (lane == 0) {
-                const int t = base + w * 16 + r;
-                cls[w * 16 + r] = t >= ntiles ? kTileNone
-                                               : (c[r] <= kSmallCap ? kTileSmall
-                                                                     : (c[r] <= CAP ? kTileMedium
-                                                                                    : kTileBig));
-            }
+        if (lane < 3) wcnt[lane][w] = lane == 0 ? cnt[0] : (lane == 1 ? cnt[1] : cnt[2]);
+        __syncthreads();
+        if (threadIdx.x < 3) {  // one atomic per class and workgroup
+            const int k = threadIdx.x;
+            const int tot = wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
+            bbase[k] = tot ? atomicAdd(&tl.n[k], tot) : 0;
         }
         __syncthreads();
-        if (w == 0) {
-            const int v = cls[lane];
-            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const uint64_t m = __ballot(v == k);
-                int at = 0;
-                if (lane == 0 && m) at = atomicAdd(&tl.n[k], __popcll(m));
-                at = __shfl(at, 0, 64);
-                int32_t* list = k == 0 ? tl.small : (k == 1 ? tl.medium : tl.big);
-                if (v == k) list[at + __popcll(m & lt)] = base + lane;
+        for (int k = 0; k < 3; ++k) {
+            int at = bbase[k];
+            for (int q = 0; q < w; ++q) at += wcnt[k][q];
+            int32_t* list = k == 0 ? tl.small : (k == 1 ? tl.medium : tl.big);
+#pragma unroll
+            for (int r = 0; r < kClassRounds; ++r) {
+                const uint64_t m = __ballot(v[r] == k);
+                if (v[r] == k) list[at + __popcll(m & lt)] = base + (r * (kBlock / 64) + w) * 64 + lane;
+                at += __popcll(m);
             }
         }
         __syncthreads();
@@ -1990,21 +2014,24 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
                                                        const int32_t* __restrict__ perm,
                                                        const uint8_t* __restrict__ core,
                                                        int32_t* __restrict__ parent) {
-    if (gp->clique) return;  // quarter-cell unions instead
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= *nf_p || !core[p]) return;
-    const double2 me = xy[p];
-    const Seg s = load_seg(seg, cell[p]);
-    int rp = uf_find(parent, (int)p);
-    for_candidates(s, [&](int j) {
-        if (j >= (int)p) return true;
-        const double2 q = xy[j];
-        if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
-            const int rj = uf_find(parent, j);
-            if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
-        }
-        return true;
-    });
+    if (gp->clique) return;  // quarter-cell unions instead (a small grid: exits at once)
+    const int64_t nf = *nf_p;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
+         p += (int64_t)gridDim.x * kBlock) {
+        if (!core[p]) continue;
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int rp = uf_find(parent, (int)p);
+        for_candidates(s, [&](int j) {
+            if (j >= (int)p) return true;
+            const double2 q = xy[j];
+            if (within_eps(me.x, me.y, q.x, q.y, eps2) && core[j]) {
+                const int rj = uf_find(parent, j);
+                if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
+            }
+            return true;
+        });
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2658,6 +2685,18 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     const bool fuse =
         mode == kGridEps && fuse_union() && count_cap() == 0 && (!a.zone || f32_count());
     uint8_t* zs = (a.zone && fuse) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
+    // clique grids: the fp32-record count kernels by tile class (tile_class_kernel);
+    // DBSCAN_F32=0 keeps the fp64 count_tile_kernel for A/B measurements
+    const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
+    const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
+    TileLists tl{};
+    uint8_t* tclass = nullptr;
+    if (f32) {
+        int32_t* lists = static_cast<int32_t*>(ws.bigt.ensure(3 * ntile_bound * sizeof(int32_t)));
+        tl = TileLists{&st[kStTileLists], lists, lists + ntile_bound, lists + 2 * ntile_bound};
+        tclass = static_cast<uint8_t*>(ws.tclass.ensure(ntile_bound));
+    }
+    int32_t* tsz = static_cast<int32_t*>(ws.tsz.ensure(ntile_bound * sizeof(int32_t)));
 
     {
         StageTimer t(prof, s, "gather");
@@ -2705,29 +2744,32 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                &st[kStCells], qidx, tmap, gp, tslot, tq, tnb);
             DBSCAN_HIP_CHECK(hipGetLastError());
             klaunch(prof, "tstage", tstage_kernel,
-                               dim3((unsigned)std::min<int64_t>((ntile_bound + 1) / 2, kTileGrid)),
+                               dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
                                dim3(kBlock),
-                               0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage);
+                               0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz);
             DBSCAN_HIP_CHECK(hipGetLastError());
+            if (f32)  // clique grids: small / medium / big tile lists
+                klaunch(prof, "tile_class", tile_class_kernel<1536>,
+                        dim3((unsigned)std::min<int64_t>(
+                            (ntile_bound + kBlock * kClassRounds - 1) / (kBlock * kClassRounds),
+                            1024)),
+                        dim3(kBlock), 0, s, tsz, &st[kStTiles], gp, tl, tclass);
         }
         {
             StageTimer t(prof, s, "segs");
             klaunch(prof, "segs", segs_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, ckey, cstart,
-                               &st[kStCells], tmap, tslot, gp, seg);
+                               &st[kStCells], tmap, tslot, gp, seg,
+                               (f32 && nbr_k > 0) ? (const uint8_t*)tclass : nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     }
     // per-tile kernels: grid stride over occupied tiles (their count stays on the device)
     const unsigned tile_grid = (unsigned)std::min<int64_t>(ntile_bound, kTileGrid);
     const unsigned rest_grid = std::min(nblk(n), 1024u);  // slots [nf, n): outside the grid
-    // clique grids: the fp32-record count (count_tile32_kernel); DBSCAN_F32=0 keeps the fp64
-    // one for A/B measurements
-    const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
     // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
     // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
         ws.blockcnt.ensure(2 * ((size_t)4 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
-    const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
@@ -2740,28 +2782,16 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 case 1024: kern = count_tile_kernel<1024, 5, false>; break;
                 default: break;
             }
-            TileLists tl{};
-            if (f32) {
-                int32_t* lists =
-                    static_cast<int32_t*>(ws.bigt.ensure(3 * ntile_bound * sizeof(int32_t)));
-                tl = TileLists{&st[kStTileLists], lists, lists + ntile_bound,
-                               lists + 2 * ntile_bound};
-            }
             const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp};
             if (f32) {
                 // clique grids by tile stage size: small tiles one wave each (count_wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
                 // big_union); other grids: count (fp64)
-                const bool cap2k = union_w() == 2047;  // (A/B: count32 capacity 2047)
-                klaunch(prof, "tile_class", cap2k ? tile_class_kernel<2047> : tile_class_kernel<1536>,
-                        dim3((unsigned)std::min<int64_t>((ntile_bound + 63) / 64, 2048)),
-                        dim3(kBlock), 0, s, tstage, &st[kStTiles], gp, tl);
                 klaunch(prof, "count_wave", count_wave_kernel<5>, dim3(tile_grid), dim3(kBlock),
                         0, s, xy, tstart, tstage, eps2, a.min_points, core, parent,
                         block_cores + 3 * tile_grid, nbr, nbr_k, fa);
                 auto k32 =
                     union_w() == 5 ? count_tile32_kernel<1536, 5> : count_tile32_kernel<1536, 6>;
-                if (cap2k) k32 = count_tile32_kernel<2047, 5>;
                 klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
                         tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
                         block_cores, nbr, nbr_k, count_ablate(), fa);
@@ -2823,7 +2853,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
         StageTimer t(prof, s, "union");
-        klaunch(prof, "union", union_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
+        klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 4096u)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
                            eps2, perm, core, parent);
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
