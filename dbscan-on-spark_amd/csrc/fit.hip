@@ -54,7 +54,7 @@ enum GridMode { kGridEps = 0, kGridAllPairs = 1, kGridNoPairs = 2 };
 namespace {
 
 constexpr int kTslot = 65;        // per-tile cell-start table stride (64 cells + end)
-constexpr int kQReg = 8;          // own-quarter core points kept in registers for pair tests
+constexpr int kQReg = 4;          // own-quarter core points kept in registers for pair tests
 constexpr int64_t kTileGrid = 8192;  // workgroups of the per-tile kernels (grid stride)
 constexpr int kMaxNbr = 11;  // neighbour lists of non-cores kept while minPoints - 1 <= this
 
