@@ -11,7 +11,8 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libdbscan_hip.so")
+# DBSCAN_LIB_PATH: an alternative build of the same library (A/B measurements of build options)
+LIB_PATH = os.environ.get("DBSCAN_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libdbscan_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "dbscan_hip.h")
 
 DBSCAN_OK, DBSCAN_EARG, DBSCAN_EHIP, DBSCAN_EOOM = 0, -1, -2, -3
