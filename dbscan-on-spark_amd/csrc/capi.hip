@@ -561,6 +561,34 @@ int32_t dbscan_slab_fit_device_async(dbscan_handle* h, const double* d_x, const 
     });
 }
 
+int32_t dbscan_slab_fit_shared_device_async(dbscan_handle* h, const double* d_x,
+                                            const double* d_y, const uint8_t* d_zone, int64_t n,
+                                            double eps, int32_t min_points,
+                                            const int64_t* d_shared, int64_t n_shared,
+                                            uint8_t* d_core, int32_t* d_root) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        check_fit_args(n, eps, DBSCAN_MODE_NAIVE, d_x, d_y, d_core, d_root);
+        if (n > 0 && !d_zone) throw dbscan::ArgError{"NULL zone pointer"};
+        if (n_shared < 0 || n_shared > n || (n_shared > 0 && !d_shared))
+            throw dbscan::ArgError{"bad shared point list"};
+        if (h->pending && h->prof.pending.size() > 4096) settle(h);
+        h->pending = false;
+        dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
+                          nullptr, d_core, d_root};
+        static const int64_t kNone = 0;
+        a.shared_idx = n_shared > 0 ? d_shared : &kNone;  // non-null: the lean output
+        a.n_shared = n_shared;
+        dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+        h->pending = true;
+        return DBSCAN_OK;
+    });
+}
+
 int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
                                        const int64_t* d_gid, const int32_t* d_root,
                                        const int32_t* d_parent, int64_t* d_gs_of_root,

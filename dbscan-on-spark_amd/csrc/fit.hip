@@ -2304,7 +2304,8 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t*
                                                        const int32_t* __restrict__ qidx,
                                                        const int4* __restrict__ qinfo,
                                                        int32_t* __restrict__ lab,
-                                                       unsigned long long* __restrict__ root_bits) {
+                                                       unsigned long long* __restrict__ root_bits,
+                                                       int32_t* __restrict__ root_out) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     if (!core[p]) {
@@ -2324,6 +2325,24 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t*
     const int32_t o = perm[r];
     lab[p] = o;
     if (r == (int)p && root_bits) atomicOr(root_bits + (o >> 6), 1ull << (o & 63));
+    if (r == (int)p && root_out) root_out[o] = o;  // lean slab output: the local roots
+}
+
+// Lean slab output for the listed (shared) slab points: core flag and local root.
+__global__ __launch_bounds__(kBlock) void slab_shared_kernel(int64_t m,
+                                                             const int64_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ inv,
+                                                             const uint8_t* __restrict__ core,
+                                                             const int32_t* __restrict__ lab,
+                                                             uint8_t* __restrict__ core_out,
+                                                             int32_t* __restrict__ root_out) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    const int64_t i = idx[k];
+    const int32_t p = inv[i];
+    const bool c = core[p] != 0;
+    core_out[i] = c ? 1 : 0;
+    root_out[i] = c ? lab[p] : -1;
 }
 
 // Cluster id of the component whose root (s(K)) is input point o: 1 + number of roots before o
@@ -2866,7 +2885,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
-                               reinterpret_cast<unsigned long long*>(root_bits));
+                               reinterpret_cast<unsigned long long*>(root_bits), (int32_t*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -2887,18 +2906,27 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     } else {
         {
             StageTimer t(prof, s, "final");
+            const bool lean = a.shared_idx != nullptr;
+            if (lean) DBSCAN_HIP_CHECK(hipMemsetAsync(a.root_out, 0xFF, n * sizeof(int32_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
-                               (unsigned long long*)nullptr);
+                               (unsigned long long*)nullptr, lean ? a.root_out : (int32_t*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer t(prof, s, "output");
-            int32_t* packed = static_cast<int32_t*>(ws.packed.ensure(n * sizeof(int32_t)));
-            klaunch(prof, "slab_pack", slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, core, lab,
-                               packed);
-            klaunch(prof, "slab_roots", slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
-                               packed, a.core_out, a.root_out);
+            if (a.shared_idx) {
+                if (a.n_shared > 0)
+                    klaunch(prof, "slab_shared", slab_shared_kernel, dim3(nblk(a.n_shared)),
+                            dim3(kBlock), 0, s, a.n_shared, a.shared_idx, inv, core, lab,
+                            a.core_out, a.root_out);
+            } else {
+                int32_t* packed = static_cast<int32_t*>(ws.packed.ensure(n * sizeof(int32_t)));
+                klaunch(prof, "slab_pack", slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
+                        core, lab, packed);
+                klaunch(prof, "slab_roots", slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
+                        n, inv, packed, a.core_out, a.root_out);
+            }
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     }

@@ -190,6 +190,11 @@ struct FitArgs {
     uint8_t* flag;
     uint8_t* core_out;
     int32_t* root_out;
+    // slab fits with shared_idx: only what the merge reads -- root_out[r] = r for every local
+    // root r, root/core of the n_shared listed points, -1 / undefined elsewhere (no full
+    // permutation of the per-point roots to slab order)
+    const int64_t* shared_idx = nullptr;
+    int64_t n_shared = 0;
 };
 
 // What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).

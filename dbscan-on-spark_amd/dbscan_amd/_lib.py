@@ -48,6 +48,8 @@ SIGNATURES = [
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     ("dbscan_slab_fit_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
+    ("dbscan_slab_fit_shared_device_async", _i32,
+     [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _i64, _vp, _vp]),
     ("dbscan_slab_label_device_async", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     ("dbscan_merge_union_device", _i32, [_vp, _vp, _i64, _vp, _vp]),
     ("dbscan_merge_reset_device", _i32, [_vp, _vp, _i64, _vp, _vp]),

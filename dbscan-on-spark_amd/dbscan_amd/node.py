@@ -177,16 +177,24 @@ class HipSlabOps:
     def _from_handle(self):
         torch.cuda.current_stream().wait_stream(self._hs)
 
-    def fit(self, x, y, zone, eps, min_points):
+    def fit(self, x, y, zone, eps, min_points, shared=None):
+        """Slab fit.  shared (int64 slab indices): the lean form -- core/root valid only at
+        those indices, root[r] == r marking every local root, -1 elsewhere (all the merge
+        reads)."""
         n = x.numel()
         if self._out is None or self._out[0].numel() != n:
             self._out = (torch.empty(n, dtype=torch.uint8, device=x.device),
                          torch.empty(n, dtype=torch.int32, device=x.device))
         core, root = self._out
         self._to_handle()
-        _lib.check(_lib.load().dbscan_slab_fit_device_async(
-            self.h.ptr, _p(x), _p(y), _p(zone), n, float(eps), int(min_points), _p(core),
-            _p(root)))
+        if shared is None:
+            _lib.check(_lib.load().dbscan_slab_fit_device_async(
+                self.h.ptr, _p(x), _p(y), _p(zone), n, float(eps), int(min_points), _p(core),
+                _p(root)))
+        else:
+            _lib.check(_lib.load().dbscan_slab_fit_shared_device_async(
+                self.h.ptr, _p(x), _p(y), _p(zone), n, float(eps), int(min_points), _p(shared),
+                shared.numel(), _p(core), _p(root)))
         self._from_handle()
         return core, root
 
@@ -286,7 +294,8 @@ class NodeJob:
         """One step.  tick(name), if given, is called after each phase (tools/node_breakdown.py
         synchronizes and times there)."""
         tick = tick or (lambda name: None)
-        core, root = self.ops.fit(self.x, self.y, self.zone, self.eps, self.min_points)
+        core, root = self.ops.fit(self.x, self.y, self.zone, self.eps, self.min_points,
+                                  shared=self.sh_idx)
         tick("slab_fit")
         # records: (gid of each shared point, gid of its local root, or -1 if not core here)
         rs = root[self.sh_idx].long().clamp(min=0)

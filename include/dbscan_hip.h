@@ -206,6 +206,16 @@ int32_t dbscan_slab_label_device(dbscan_handle* h, const uint8_t* d_zone, const 
 int32_t dbscan_slab_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
                                      const uint8_t* d_zone, int64_t n, double eps,
                                      int32_t min_points, uint8_t* d_core, int32_t* d_root);
+/* dbscan_slab_fit_device_async with only the outputs the merge reads (dbscan_amd/node.py):
+ * d_root[r] = r for every local root r; for the n_shared slab indices d_shared[k] (the points
+ * this rank shares with a neighbour rank) d_core and d_root as in dbscan_slab_fit_device; every
+ * other d_root entry is -1 and every other d_core entry is left unwritten.  Skips moving every
+ * point's root to slab order (one random read per point). */
+int32_t dbscan_slab_fit_shared_device_async(dbscan_handle* h, const double* d_x,
+                                            const double* d_y, const uint8_t* d_zone, int64_t n,
+                                            double eps, int32_t min_points,
+                                            const int64_t* d_shared, int64_t n_shared,
+                                            uint8_t* d_core, int32_t* d_root);
 int32_t dbscan_slab_label_device_async(dbscan_handle* h, const uint8_t* d_zone,
                                        const int64_t* d_gid, const int64_t* d_gs_of_root,
                                        const int64_t* d_all_roots, int64_t n_all_roots,

@@ -20,7 +20,7 @@ class OracleSlabOps:
     """CPU test double of HipSlabOps: the oracle's restatement of the slab semantics, so the
     merge logic (collectives, global union, numbering) runs under gloo without a GPU."""
 
-    def fit(self, x, y, zone, eps, min_points):
+    def fit(self, x, y, zone, eps, min_points, shared=None):  # (full outputs either way)
         import oracle as O
 
         xs, ys, zs = x.numpy(), y.numpy(), zone.numpy()

@@ -118,3 +118,39 @@ def test_train_node_unshardable_and_labeled_csv(labeled_data):
     assert k == rk
     np.testing.assert_array_equal(cl, rc)
     np.testing.assert_array_equal(fl, rf)
+
+
+def test_lean_slab_fit_matches_full():
+    """dbscan_slab_fit_shared_device_async (the node step's form) against the full slab fit on
+    the same slab: identical core/root at the shared points, root[r] == r at exactly the local
+    roots and -1 elsewhere."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import node
+
+    dbscan_amd.load()
+    x, y = gen_blobs(600_000, noise=0.2, seed=5)
+    tx, ty = torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda")
+    cuts = node.make_cuts(tx, 3, 2.55)
+    h = dbscan_amd.Handle(0)
+    ops = node.HipSlabOps(h)
+    for rank in range(3):
+        z, sh = node.zones(tx, rank, cuts, 2.55)
+        idx = torch.nonzero(z != node.OUT).flatten()
+        sx, sy, sz = tx[idx].contiguous(), ty[idx].contiguous(), z[idx].contiguous()
+        shared = torch.nonzero(sh[idx]).flatten()
+        core_f, root_f = [t.clone() for t in ops.fit(sx, sy, sz, 2.55, 10)]
+        core_l, root_l = [t.clone() for t in ops.fit(sx, sy, sz, 2.55, 10, shared=shared)]
+        torch.cuda.synchronize()
+        assert shared.numel() > 0
+        assert torch.equal(core_l[shared], core_f[shared])
+        assert torch.equal(root_l[shared], root_f[shared])
+        ar = torch.arange(root_f.numel(), device="cuda", dtype=torch.int32)
+        is_root = root_f == ar
+        assert torch.equal(root_l == ar, is_root)
+        rest = torch.ones_like(is_root)
+        rest[shared] = False
+        rest &= ~is_root
+        assert bool((root_l[rest] == -1).all())
+    h.close()
