@@ -205,7 +205,115 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < kWaves; ++k) c += h[k][d];
-    hist[(int64_t)d * nblocks + blockIdx.x] = (int32_t)c;
+    hist[(int64_t)blockIdx.x * 256 + d] = (int32_t)c;  // block-major: one coalesced 1 KB row
+}
+
+// Global offset of every (radix tile, digit) from the block-major count table, in one launch:
+// off[b][d] = sum over digits d' < d of all tiles' counts + sum over tiles b' < b of digit d.
+// kOffBlocks workgroups, one digit per thread: each sums its rows of the table (coalesced 1 KB
+// rows) and publishes the per-digit aggregates; every workgroup then reads all aggregates (the
+// grid is far smaller than the GPU, so every workgroup is resident and the wait always ends;
+// a bounded spin flags state[0] instead of hanging), derives the digit bases and its rows'
+// running offsets, and writes them row by row.  Replaces a digit-major table whose upsweep
+// writes scattered each tile's 256 counts over 256 lines (8x write amplification) and whose
+// downsweep reads did the same.
+constexpr int kOffBlocks = 64;  // workgroups
+constexpr int kOffGroups = 4;   // row groups per digit (1024 threads)
+constexpr int kOffRows = 24;    // rows per thread held in registers (more: a second round)
+
+__global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
+    const int32_t* __restrict__ cnt, int64_t nb, int32_t* __restrict__ off,
+    uint64_t* __restrict__ state, uint32_t epoch) {
+    __shared__ int gsum[kOffGroups][256], gtot[kOffGroups][256], gbef[kOffGroups][256];
+    __shared__ int wsum[4];
+    const int d = threadIdx.x & 255, g = threadIdx.x >> 8;
+    const int64_t per = (nb + kOffBlocks - 1) / kOffBlocks;
+    const int64_t b0 = blockIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    const int64_t gper = (per + kOffGroups - 1) / kOffGroups;
+    const int64_t r0 = b0 + g * gper, r1 = r0 + gper < b1 ? r0 + gper : b1;
+    // phase 1: this group's rows of digit d (all loads in flight together)
+    int agg = 0;
+    for (int64_t rb = r0; rb < r1; rb += kOffRows) {
+        int v[kOffRows];
+#pragma unroll
+        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * 256 + d] : 0;
+#pragma unroll
+        for (int k = 0; k < kOffRows; ++k) agg += v[k];
+    }
+    gsum[g][d] = agg;
+    __syncthreads();
+    uint64_t* status = state + 1;
+    if (g == 0) {
+        int a = 0;
+#pragma unroll
+        for (int q = 0; q < kOffGroups; ++q) a += gsum[q][d];
+        __hip_atomic_store(status + blockIdx.x * 256 + d, scan_status(epoch, kStIncl, a),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // phase 2: every workgroup's aggregate of digit d (group g reads a quarter of them)
+    int total = 0, before = 0;
+    constexpr int kPerG = kOffBlocks / kOffGroups;
+    const auto ready = [&](uint64_t v) {
+        return (uint32_t)(v >> 34) == epoch && ((v >> 32) & 3u) != 0;
+    };
+    uint64_t sv[kPerG];
+#pragma unroll
+    for (int q = 0; q < kPerG; ++q)  // all in flight at once; re-polled only if not yet set
+        sv[q] = __hip_atomic_load(status + (g * kPerG + q) * 256 + d, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int q = 0; q < kPerG; ++q) {
+        const int k = g * kPerG + q;
+        uint64_t v = sv[q];
+        for (int spin = 0; !ready(v); ++spin) {
+            if (spin == (1 << 22)) {  // watchdog: never reached while the grid is resident
+                __hip_atomic_fetch_or(state, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = scan_status(epoch, kStIncl, 0);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            v = __hip_atomic_load(status + k * 256 + d, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        }
+        total += (int32_t)(uint32_t)v;
+        before += k < (int)blockIdx.x ? (int32_t)(uint32_t)v : 0;
+    }
+    gtot[g][d] = total;
+    gbef[g][d] = before;
+    __syncthreads();
+    int run = 0;
+    if (g == 0) {  // digit base: exclusive scan of the digit totals over the 256 digits
+        int t = 0, b = 0;
+#pragma unroll
+        for (int q = 0; q < kOffGroups; ++q) {
+            t += gtot[q][d];
+            b += gbef[q][d];
+        }
+        const int incl = wave_incl_scan(t);
+        if ((d & 63) == 63) wsum[d >> 6] = incl;
+        run = incl - t + b;
+        gtot[0][d] = run;  // (reused: this workgroup's offset of digit d)
+    }
+    __syncthreads();
+    if (g == 0) {
+        int r = gtot[0][d];
+        for (int q = 0; q < (d >> 6); ++q) r += wsum[q];
+        gtot[0][d] = r;
+    }
+    __syncthreads();
+    // phase 3: this group's rows, after the earlier groups' rows of this workgroup
+    run = gtot[0][d];
+    for (int q = 0; q < g; ++q) run += gsum[q][d];
+    for (int64_t rb = r0; rb < r1; rb += kOffRows) {
+        int v[kOffRows];
+#pragma unroll
+        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * 256 + d] : 0;
+#pragma unroll
+        for (int k = 0; k < kOffRows; ++k) {
+            if (rb + k < r1) off[(rb + k) * 256 + d] = run;
+            run += v[k];
+        }
+    }
 }
 
 // Downsweep: wave w ranks the contiguous quarter [w*1024, (w+1)*1024) of the 4096-key tile in
@@ -295,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         int woff = 0;
         for (int q = 0; q < w; ++q) woff += sm.wsum[q];
         sm.tile_start[t] = woff + incl - running;
-        sm.gofs[t] = hist_scanned[(int64_t)t * nblocks + blockIdx.x];
+        sm.gofs[t] = hist_scanned[(int64_t)blockIdx.x * 256 + t];  // block-major row
     }
     __syncthreads();
 #pragma unroll
@@ -443,7 +551,9 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
                       DevBuf& hist, ScanState& scan, Profiler* prof, int32_t* inv) {
     if (n <= 0 || max_bits <= 0) return;
     const int64_t nb = (n + kRTile - 1) / kRTile;
-    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)nb * 256 * sizeof(int32_t)));
+    // per-tile digit counts (block-major) and the tiles' global digit offsets
+    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * nb * 256 * sizeof(int32_t)));
+    int32_t* ho = h + nb * 256;
     for (int shift = 0; shift < max_bits; shift += 8) {
         {
             StageTimer st(prof, s, "sort_upsweep");
@@ -453,12 +563,15 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         }
         {
             StageTimer st(prof, s, "sort_scan");
-            exclusive_scan(s, 0, h, h, nb * 256, nullptr, scan);
+            uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 256);
+            klaunch(prof, "radix_offsets", radix_offsets_kernel, dim3(kOffBlocks),
+                    dim3(256 * kOffGroups), 0,
+                    s, (const int32_t*)h, nb, ho, state, scan.epoch);
         }
         {
             StageTimer st(prof, s, "sort_downsweep");
             klaunch(prof, "radix_downsweep", radix_downsweep_kernel, dim3((unsigned)nb),
-                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, h, inv);
+                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, ho, inv);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         uint32_t* tk = key;
