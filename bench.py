@@ -40,9 +40,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # launches per fit, each reading key+perm 8 and writing 8.
 ALG_BYTES = {
     "bbox_partial": 16, "bin": 20, "radix_upsweep": 4, "radix_downsweep": 16, "inverse": 8,
-    "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 21, "edge_union": 0,
-    "quarter_root": 0, "final": 13, "label_sorted": 13, "permute_out": 13,
+    "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 21, "count_wave": 21,
+    "count32": 21, "big_count": 21, "edge_union": 0, "quarter_root": 0, "final": 13,
+    "label_sorted": 13, "permute_out": 13,
 }
+# The clique-grid count kernels each process one class of tiles: their per-launch algorithmic
+# bytes count that class's points only (dbscan_last_stats [11..13]).
+CLASS_PTS = {"count_wave": "pts_small", "count32": "pts_medium", "big_count": "pts_big"}
 PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
 
 def parse():
@@ -195,13 +199,14 @@ def main():
     if prof and dom in prof:
         avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])  # live, in the timed region
         pts = stats.get("n", args.points_per_gpu)
-        alg = ALG_BYTES.get(dom, 0) * pts  # per launch
+        unit_pts = stats.get(CLASS_PTS[dom], pts) if dom in CLASS_PTS else pts
+        alg = ALG_BYTES.get(dom, 0) * unit_pts  # per launch
         achieved = alg / (avg_ms * 1e-3) / 1e9
         traffic = load_traffic(dom, pts) if (world == 1 and not args.node) else None
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
-                "alg_bytes_per_point": ALG_BYTES.get(dom, 0),
+                "alg_bytes_per_point": ALG_BYTES.get(dom, 0), "points_per_launch": unit_pts,
                 "pipeline_frac": round(PIPELINE_ALG_BYTES * pts / (ms_per_step * 1e-3) / 1e9
                                        / HBM_PEAK_GBS, 5)}
 

@@ -656,12 +656,13 @@ int32_t dbscan_slab_label_device_async(dbscan_handle* h, const uint8_t* d_zone,
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max) {
     if (!h || !out) return DBSCAN_EARG;
     if (h->pending && dbscan_sync(h) != DBSCAN_OK) return DBSCAN_EHIP;
-    const int64_t v[11] = {h->stats.n,     h->stats.nf,        h->stats.ncells,
-                           h->stats.ncore, h->stats.nclusters, h->stats.nx,
-                           h->stats.ny,    h->stats.bits,      h->stats.grid_mode,
-                           h->stats.ntiles, h->stats.clique};
+    const int64_t v[14] = {h->stats.n,         h->stats.nf,         h->stats.ncells,
+                           h->stats.ncore,     h->stats.nclusters,  h->stats.nx,
+                           h->stats.ny,        h->stats.bits,       h->stats.grid_mode,
+                           h->stats.ntiles,    h->stats.clique,     h->stats.pts_small,
+                           h->stats.pts_medium, h->stats.pts_big};
     int k = 0;
-    for (; k < max && k < 11; ++k) out[k] = v[k];
+    for (; k < max && k < 14; ++k) out[k] = v[k];
     return k;
 }
 

@@ -491,12 +491,15 @@ constexpr int kClassRounds = 4;  // tile_class_kernel: 64 tiles per lane round, 
 
 template <int CAP>
 __global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __restrict__ tsz,
+                                                            const int32_t* __restrict__ tstart,
                                                             const int32_t* __restrict__ ntiles_p,
                                                             const GridParams* __restrict__ gp,
                                                             TileLists tl,
-                                                            uint8_t* __restrict__ tclass) {
+                                                            uint8_t* __restrict__ tclass,
+                                                            int32_t* __restrict__ class_pts) {
     if (!gp->clique) return;
     __shared__ int wcnt[3][kBlock / 64];
+    __shared__ int wpts[3][kBlock / 64];
     __shared__ int bbase[3];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ntiles = *ntiles_p;
@@ -504,25 +507,39 @@ __global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __res
     for (int base = blockIdx.x * kBlock * kClassRounds; base < ntiles;
          base += gridDim.x * kBlock * kClassRounds) {  // block-uniform loop
         int v[kClassRounds];
-        int cnt[3] = {0, 0, 0};
+        int cnt[3] = {0, 0, 0}, pts[3] = {0, 0, 0};
 #pragma unroll
         for (int r = 0; r < kClassRounds; ++r) {  // tile = base + (r * 4 + w) * 64 + lane
             const int t = base + (r * (kBlock / 64) + w) * 64 + lane;
             v[r] = kTileNone;
+            int own = 0;
             if (t < ntiles) {
                 const int c = tsz[t];
                 v[r] = c <= kSmallCap ? kTileSmall : (c <= CAP ? kTileMedium : kTileBig);
                 tclass[t] = (uint8_t)v[r];
+                own = tstart[t + 1] - tstart[t];
             }
 #pragma unroll
-            for (int k = 0; k < 3; ++k) cnt[k] += __popcll(__ballot(v[r] == k));
+            for (int k = 0; k < 3; ++k) {
+                cnt[k] += __popcll(__ballot(v[r] == k));
+                pts[k] += v[r] == k ? own : 0;
+            }
         }
-        if (lane < 3) wcnt[lane][w] = lane == 0 ? cnt[0] : (lane == 1 ? cnt[1] : cnt[2]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) pts[k] += __shfl_xor(pts[k], o, 64);
+        if (lane < 3) {
+            wcnt[lane][w] = lane == 0 ? cnt[0] : (lane == 1 ? cnt[1] : cnt[2]);
+            wpts[lane][w] = lane == 0 ? pts[0] : (lane == 1 ? pts[1] : pts[2]);
+        }
         __syncthreads();
         if (threadIdx.x < 3) {  // one atomic per class and workgroup
             const int k = threadIdx.x;
             const int tot = wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
             bbase[k] = tot ? atomicAdd(&tl.n[k], tot) : 0;
+            const int p = wpts[k][0] + wpts[k][1] + wpts[k][2] + wpts[k][3];
+            if (p) atomicAdd(&class_pts[k], p);
         }
         __syncthreads();
 #pragma unroll
@@ -2772,7 +2789,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         dim3((unsigned)std::min<int64_t>(
                             (ntile_bound + kBlock * kClassRounds - 1) / (kBlock * kClassRounds),
                             1024)),
-                        dim3(kBlock), 0, s, tsz, &st[kStTiles], gp, tl, tclass);
+                        dim3(kBlock), 0, s, tsz, tstart, &st[kStTiles], gp, tl, tclass,
+                        &st[kStClassPts]);
         }
         {
             StageTimer t(prof, s, "segs");
@@ -2973,6 +2991,9 @@ FitStats read_fit_stats(hipStream_t s, Workspace& ws) {
     stats.ntiles = grid ? v[kStTiles] : 0;
     stats.ncore = v[kStCore];
     stats.nclusters = v[kStClusters];
+    stats.pts_small = grid ? v[kStClassPts] : 0;
+    stats.pts_medium = grid ? v[kStClassPts + 1] : 0;
+    stats.pts_big = grid ? v[kStClassPts + 2] : 0;
     return stats;
 }
 

@@ -50,6 +50,7 @@ enum FitState {
     kStBits = 7,      // radix key width
     kStError = 8,     // the eps grid could not be sized
     kStTileLists = 9,  // [3] clique-grid tiles per count path: small, medium, big
+    kStClassPts = 12,  // [3] their own points (what each count kernel processes)
     kStCount = 16
 };
 
@@ -172,7 +173,7 @@ struct GridParams {
 
 struct FitStats {
     int64_t n = 0, nf = 0, ncells = 0, ncore = 0, nclusters = 0, nx = 0, ny = 0, bits = 0,
-            grid_mode = 0, ntiles = 0, clique = 0;
+            grid_mode = 0, ntiles = 0, clique = 0, pts_small = 0, pts_medium = 0, pts_big = 0;
 };
 
 // One fit.  Full fits (zone == nullptr) write cluster/flag in input order and return the

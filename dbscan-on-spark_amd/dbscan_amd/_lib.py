@@ -136,10 +136,10 @@ class Handle:
         return int(load().dbscan_stream(self._h) or 0)
 
     def stats(self) -> dict:
-        buf = (ctypes.c_int64 * 11)()
-        k = load().dbscan_last_stats(self._h, buf, 11)
+        buf = (ctypes.c_int64 * 14)()
+        k = load().dbscan_last_stats(self._h, buf, 14)
         keys = ["n", "finite", "cells", "core", "clusters", "nx", "ny", "key_bits", "grid_mode",
-                "tiles", "clique"]
+                "tiles", "clique", "pts_small", "pts_medium", "pts_big"]
         return {keys[i]: int(buf[i]) for i in range(k)}
 
     def profile(self, on: bool = True, kernels: bool = False) -> None:

@@ -107,6 +107,7 @@ void* dbscan_stream(dbscan_handle* h);
  *   [4] clusters  [5] grid nx  [6] grid ny  [7] radix key bits  [8] grid mode
  *   (0 = eps grid, 1 = all pairs, 2 = no pairs)  [9] occupied 8x8-cell tiles
  *   [10] 1 if quarter cells are cliques of the predicate (tile union path)
+ *   [11..13] clique grids: points in the small / medium / big tiles (the three count paths)
  * Returns the number of values written (<= max).                               */
 int32_t dbscan_last_stats(dbscan_handle* h, int64_t* out, int32_t max);
 

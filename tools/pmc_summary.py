@@ -23,6 +23,8 @@ def stage_of(kernel):
     without `_kernel`; count_tile_kernel is "count"."""
     if kernel == "count_tile_kernel":
         return "count"
+    if kernel == "count_tile32_kernel":
+        return "count32"
     return kernel[:-len("_kernel")] if kernel.endswith("_kernel") else None
 
 
