@@ -137,3 +137,17 @@ def test_lattice_pairs_at_exactly_eps(dm, handle, div, mp):
     p = rng.permutation(x.size)
     _check(dm, handle, x[p].copy(), y[p].copy(), eps, mp)
     assert handle.stats()["clique"] == 1
+
+
+@pytest.mark.parametrize("offset,eps", [(1e12, 1e-3), (-3e9, 0.05), (0.0, 1e-150)])
+def test_fp32_records_far_from_origin(dm, handle, offset, eps):
+    """Tile-relative fp32 records must not lose the fp64 predicate: clumps far from the origin
+    (coordinate ulps close to eps), and a tiny eps whose squares sit near the fp64 underflow.
+    Exact against the CPU oracle."""
+    rng = np.random.default_rng(abs(int(np.log10(abs(offset) + 1))) + 7)
+    n = 60_000
+    c = rng.uniform(-30 * eps, 30 * eps, size=(12, 2))
+    pts = c[rng.integers(0, 12, n)] + rng.normal(0, 0.8 * eps, size=(n, 2))
+    x = offset + pts[:, 0]
+    y = -offset + pts[:, 1]
+    _check(dm, handle, x, y, eps, 8)
