@@ -2678,8 +2678,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                perm);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        radix_sort_pairs(s, key, perm, key2, perm2, n, 32, &st[kStBits], ws.hist, ws.scan,
-                         prof, inv);
+        uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));
+        int32_t* perm3 = static_cast<int32_t*>(ws.perm3.ensure(n * sizeof(int32_t)));
+        radix_sort_pairs(s, key, perm, key2, perm2, key3, perm3, n, &st[kStBits], ws.hist,
+                         ws.scan, prof, inv);
     } else {
         StageTimer t(prof, s, "bin");
         // all pairs: one cell holding every point, the predicate decides (incl. non-finite)

@@ -147,7 +147,8 @@ struct ScanState {
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
-        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz;
+        tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
+        key3, perm3;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -159,7 +160,7 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag, &bigt, &zs, &tclass, &tsz})
+                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3})
             b->release();
     }
 };
@@ -262,15 +263,16 @@ int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint
 void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64_t n,
                     int32_t* total_dev, ScanState& ss);
 
-// LSD radix sort of (key, val) pairs on the low bits; results end in key/val
-// (ping-pong through key2/val2).  Stable.
-// max_bits bounds the key width on the host (the pass count); bits_dev holds the actual width
-// on the device: passes at or beyond it copy instead of sorting.
+// LSD radix sort of (key, val) pairs: four passes of 8, 8, 9 and 7 bits; bits_dev holds the
+// key width on the device and passes at or beyond it return at once (keys of <= 25 bits: three
+// passes).  The input is (key, val); the passes ping-pong through (key2, val2) and the last
+// sorting pass writes (key3, val3), whose pointers are then swapped into key/val.  Stable.
 // inv (optional): the inverse permutation of the sorted vals (a permutation of 0..n-1),
-// inv[val] = sorted position, written by the final pass.
+// inv[val] = sorted position, written by the last pass.
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
-                      int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, ScanState& scan, Profiler* prof, int32_t* inv = nullptr);
+                      int32_t*& val2, uint32_t*& key3, int32_t*& val3, int64_t n,
+                      const int32_t* bits_dev, DevBuf& hist, ScanState& scan, Profiler* prof,
+                      int32_t* inv = nullptr);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

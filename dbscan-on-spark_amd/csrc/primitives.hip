@@ -12,6 +12,8 @@
 
 #include <cmath>
 #include <cstdio>
+#include <type_traits>
+#include <utility>
 
 namespace dbscan {
 
@@ -184,59 +186,69 @@ void scan_impl(hipStream_t s, const void* in, int32_t* out, int64_t n, int32_t* 
 constexpr int kRItems = RADIX_ITEMS;
 constexpr int kRTile = kBlock * kRItems;
 
+// Digits of W bits (RB = 2^W buckets, W = 7..9): the passes are 8 + 8 + 9 + 7 bits, so keys
+// of up to 25 bits (an eps grid of up to 2^23 cells x 4 quarters: 10^7 points of the bench)
+// sort in three passes; passes at or beyond the device-side key width return at once.
+template <int W>
 __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* __restrict__ key,
                                                                int64_t n, int shift,
                                                                const int32_t* __restrict__ bits_p,
                                                                int64_t nblocks,
                                                                int32_t* __restrict__ hist) {
-    if (shift >= *bits_p) return;  // digit beyond the key width: the downsweep copies
-    __shared__ uint32_t h[kWaves][256];
+    constexpr int RB = 1 << W;
+    if (shift >= *bits_p) return;  // digit beyond the key width: nothing left to sort
+    __shared__ uint32_t h[kWaves][RB];
     const int w = threadIdx.x >> 6;
-    for (int d = threadIdx.x; d < kWaves * 256; d += kBlock) (&h[0][0])[d] = 0;
+    for (int d = threadIdx.x; d < kWaves * RB; d += kBlock) (&h[0][0])[d] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kRTile;
 #pragma unroll 4
     for (int r = 0; r < kRItems; ++r) {
         const int64_t i = base + r * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[w][(key[i] >> shift) & 255u], 1u);
+        if (i < n) atomicAdd(&h[w][(key[i] >> shift) & (RB - 1u)], 1u);
     }
     __syncthreads();
-    const int d = threadIdx.x;
-    uint32_t c = 0;
+    for (int d = threadIdx.x; d < RB; d += kBlock) {
+        uint32_t c = 0;
 #pragma unroll
-    for (int k = 0; k < kWaves; ++k) c += h[k][d];
-    hist[(int64_t)blockIdx.x * 256 + d] = (int32_t)c;  // block-major: one coalesced 1 KB row
+        for (int k = 0; k < kWaves; ++k) c += h[k][d];
+        hist[(int64_t)blockIdx.x * RB + d] = (int32_t)c;  // block-major: one coalesced row
+    }
 }
 
 // Global offset of every (radix tile, digit) from the block-major count table, in one launch:
 // off[b][d] = sum over digits d' < d of all tiles' counts + sum over tiles b' < b of digit d.
-// kOffBlocks workgroups, one digit per thread: each sums its rows of the table (coalesced 1 KB
-// rows) and publishes the per-digit aggregates; every workgroup then reads all aggregates (the
-// grid is far smaller than the GPU, so every workgroup is resident and the wait always ends;
-// a bounded spin flags state[0] instead of hanging), derives the digit bases and its rows'
-// running offsets, and writes them row by row.  Replaces a digit-major table whose upsweep
-// writes scattered each tile's 256 counts over 256 lines (8x write amplification) and whose
-// downsweep reads did the same.
+// kOffBlocks workgroups of 1024 threads, RB digits x (1024 / RB) row groups: each sums its
+// rows of the table (coalesced rows) and publishes the per-digit aggregates; every workgroup
+// then reads all aggregates (the grid is far smaller than the GPU, so every workgroup is
+// resident and the wait always ends; a bounded spin flags state[0] instead of hanging),
+// derives the digit bases and its rows' running offsets, and writes them row by row.  A
+// digit-major table instead scattered each tile's counts over RB lines on the upsweep's
+// writes and the downsweep's reads (8x amplification).
 constexpr int kOffBlocks = 64;  // workgroups
-constexpr int kOffGroups = 4;   // row groups per digit (1024 threads)
+constexpr int kOffThreads = 1024;
 constexpr int kOffRows = 24;    // rows per thread held in registers (more: a second round)
 
-__global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
+template <int W>
+__global__ __launch_bounds__(kOffThreads) void radix_offsets_kernel(
     const int32_t* __restrict__ cnt, int64_t nb, int32_t* __restrict__ off,
-    uint64_t* __restrict__ state, uint32_t epoch) {
-    __shared__ int gsum[kOffGroups][256], gtot[kOffGroups][256], gbef[kOffGroups][256];
-    __shared__ int wsum[4];
-    const int d = threadIdx.x & 255, g = threadIdx.x >> 8;
+    uint64_t* __restrict__ state, uint32_t epoch, const int32_t* __restrict__ bits_p,
+    int shift) {
+    constexpr int RB = 1 << W, G = kOffThreads / RB;
+    if (shift >= *bits_p) return;
+    __shared__ int gsum[G][RB], gtot[G][RB], gbef[G][RB];
+    __shared__ int wsum[RB / 64];
+    const int d = threadIdx.x % RB, g = threadIdx.x / RB;
     const int64_t per = (nb + kOffBlocks - 1) / kOffBlocks;
     const int64_t b0 = blockIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
-    const int64_t gper = (per + kOffGroups - 1) / kOffGroups;
+    const int64_t gper = (per + G - 1) / G;
     const int64_t r0 = b0 + g * gper, r1 = r0 + gper < b1 ? r0 + gper : b1;
     // phase 1: this group's rows of digit d (all loads in flight together)
     int agg = 0;
     for (int64_t rb = r0; rb < r1; rb += kOffRows) {
         int v[kOffRows];
 #pragma unroll
-        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * 256 + d] : 0;
+        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * RB + d] : 0;
 #pragma unroll
         for (int k = 0; k < kOffRows; ++k) agg += v[k];
     }
@@ -246,20 +258,20 @@ __global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
     if (g == 0) {
         int a = 0;
 #pragma unroll
-        for (int q = 0; q < kOffGroups; ++q) a += gsum[q][d];
-        __hip_atomic_store(status + blockIdx.x * 256 + d, scan_status(epoch, kStIncl, a),
+        for (int q = 0; q < G; ++q) a += gsum[q][d];
+        __hip_atomic_store(status + blockIdx.x * RB + d, scan_status(epoch, kStIncl, a),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // phase 2: every workgroup's aggregate of digit d (group g reads a quarter of them)
+    // phase 2: every workgroup's aggregate of digit d (group g reads its share of them)
     int total = 0, before = 0;
-    constexpr int kPerG = kOffBlocks / kOffGroups;
+    constexpr int kPerG = kOffBlocks / G;
     const auto ready = [&](uint64_t v) {
         return (uint32_t)(v >> 34) == epoch && ((v >> 32) & 3u) != 0;
     };
     uint64_t sv[kPerG];
 #pragma unroll
     for (int q = 0; q < kPerG; ++q)  // all in flight at once; re-polled only if not yet set
-        sv[q] = __hip_atomic_load(status + (g * kPerG + q) * 256 + d, __ATOMIC_RELAXED,
+        sv[q] = __hip_atomic_load(status + (g * kPerG + q) * RB + d, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int q = 0; q < kPerG; ++q) {
@@ -272,7 +284,7 @@ __global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            v = __hip_atomic_load(status + k * 256 + d, __ATOMIC_RELAXED,
+            v = __hip_atomic_load(status + k * RB + d, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         total += (int32_t)(uint32_t)v;
@@ -281,18 +293,16 @@ __global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
     gtot[g][d] = total;
     gbef[g][d] = before;
     __syncthreads();
-    int run = 0;
-    if (g == 0) {  // digit base: exclusive scan of the digit totals over the 256 digits
+    if (g == 0) {  // digit base: exclusive scan of the digit totals over the RB digits
         int t = 0, b = 0;
 #pragma unroll
-        for (int q = 0; q < kOffGroups; ++q) {
+        for (int q = 0; q < G; ++q) {
             t += gtot[q][d];
             b += gbef[q][d];
         }
         const int incl = wave_incl_scan(t);
         if ((d & 63) == 63) wsum[d >> 6] = incl;
-        run = incl - t + b;
-        gtot[0][d] = run;  // (reused: this workgroup's offset of digit d)
+        gtot[0][d] = incl - t + b;  // (reused: this workgroup's offset of digit d, partial)
     }
     __syncthreads();
     if (g == 0) {
@@ -302,65 +312,73 @@ __global__ __launch_bounds__(256 * kOffGroups) void radix_offsets_kernel(
     }
     __syncthreads();
     // phase 3: this group's rows, after the earlier groups' rows of this workgroup
-    run = gtot[0][d];
+    int run = gtot[0][d];
     for (int q = 0; q < g; ++q) run += gsum[q][d];
     for (int64_t rb = r0; rb < r1; rb += kOffRows) {
         int v[kOffRows];
 #pragma unroll
-        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * 256 + d] : 0;
+        for (int k = 0; k < kOffRows; ++k) v[k] = rb + k < r1 ? cnt[(rb + k) * RB + d] : 0;
 #pragma unroll
         for (int k = 0; k < kOffRows; ++k) {
-            if (rb + k < r1) off[(rb + k) * 256 + d] = run;
+            if (rb + k < r1) off[(rb + k) * RB + d] = run;
             run += v[k];
         }
     }
 }
 
-// Downsweep: wave w ranks the contiguous quarter [w*1024, (w+1)*1024) of the 4096-key tile in
-// 16 rounds of 64 keys (coalesced), so (wave, round, lane) order IS tile order and per-wave
-// running digit counters give stable ranks: per round, lanes with equal digits are matched by 8
+// Downsweep: wave w ranks the contiguous quarter [w*512, (w+1)*512) of the 2048-key tile in
+// 8 rounds of 64 keys (coalesced), so (wave, round, lane) order IS tile order and per-wave
+// running digit counters give stable ranks: per round, lanes with equal digits are matched by W
 // ballots, the lowest such lane (the leader) bumps the wave's counter for that digit, and each
 // lane's rank = counter before the bump (read from its leader) + its rank among the matches.
 // Then per digit a 4-wave prefix and a block scan of the digit totals place every key in LDS
 // (tile sorted by digit), and each digit run is written coalesced to its global offset.
+// The last sorting pass (shift + W >= the key width) writes the final buffers (key_fin,
+// val_fin) and the inverse permutation; passes after it return at once.
+template <int W>
 struct DownsweepSmem {
-    int32_t cnt[kWaves][256];  // per-wave digit counters -> wave offsets within a digit
+    static constexpr int RB = 1 << W;
+    int32_t cnt[kWaves][RB];  // per-wave digit counters -> wave offsets within a digit
     uint32_t keys[kRTile];
     int32_t vals[kRTile];
-    int32_t tile_start[257];
-    int32_t gofs[256];
+    int32_t tile_start[RB + 1];
+    int32_t gofs[RB];
     int32_t wsum[kWaves];
 };
 
+template <int W>
 __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
-    uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, int64_t n, int shift,
+    uint32_t* __restrict__ key_next, int32_t* __restrict__ val_next,
+    uint32_t* __restrict__ key_fin, int32_t* __restrict__ val_fin, int64_t n, int shift,
     const int32_t* __restrict__ bits_p, int64_t nblocks,
-    const int32_t* __restrict__ hist_scanned, int32_t* __restrict__ inv) {
-    __shared__ DownsweepSmem sm;
+    const int32_t* __restrict__ hist_off, int32_t* __restrict__ inv) {
+    constexpr int RB = 1 << W;
+    constexpr int DPT = RB > kBlock ? RB / kBlock : 1;  // digits per thread in the block scan
+    __shared__ DownsweepSmem<W> sm;
     const int t = threadIdx.x, w = t >> 6, lane = lane_id();
     const int64_t base = (int64_t)blockIdx.x * kRTile;
     const int tile_n = (int)((n - base) < kRTile ? (n - base) : kRTile);
     const int bits = *bits_p;
-    // the final order is known in the last sorting pass (or the first copy when none sorts):
-    // that pass also writes the inverse permutation inv[val] = position
-    const bool last = inv && ((shift < bits && shift + 8 >= bits) || (bits == 0 && shift == 0));
-    if (shift >= bits) {  // every key has this digit 0 (or all ones: the sentinel): copy
+    if (bits == 0 && shift == 0) {  // nothing to sort (no grid key bits): the final copy
         for (int j = t; j < tile_n; j += kBlock) {
             const int32_t v = val[base + j];
-            key_out[base + j] = key[base + j];
-            val_out[base + j] = v;
-            if (last) inv[v] = (int32_t)(base + j);
+            key_fin[base + j] = key[base + j];
+            val_fin[base + j] = v;
+            if (inv) inv[v] = (int32_t)(base + j);
         }
         return;
     }
-#pragma unroll
-    for (int k = 0; k < kWaves; ++k) sm.cnt[k][t] = 0;
+    if (shift >= bits) return;  // an earlier pass was the last
+    const bool last = shift + W >= bits;
+    uint32_t* __restrict__ key_out = last ? key_fin : key_next;
+    int32_t* __restrict__ val_out = last ? val_fin : val_next;
+    for (int k = t; k < kWaves * RB; k += kBlock) (&sm.cnt[0][0])[k] = 0;
     __syncthreads();
 
     uint32_t k_r[kRItems];
     int32_t v_r[kRItems];
-    uint32_t dr[kRItems];  // digit | (rank within the wave's digit run << 8); 0xFFFFFFFF invalid
+    uint32_t dr[kRItems];  // digit | (rank within the wave's digit run << 10); ~0u invalid
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
 #pragma unroll
@@ -369,10 +387,10 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         const bool valid = i < base + tile_n;
         const uint32_t k = valid ? key[i] : kSentinelKey;
         const int32_t v = valid ? val[i] : 0;
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k >> shift) & (RB - 1u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
+        for (int b = 0; b < W; ++b) {
             const bool bit = (d >> b) & 1u;
             const uint64_t bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
@@ -386,31 +404,49 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         old = __shfl(old, leader, 64);
         k_r[r] = k;
         v_r[r] = v;
-        dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 8)) : 0xFFFFFFFFu;
+        dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 10)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    {  // per digit t: wave offsets (prefix over the 4 waves) and the digit's tile total
-        int running = 0;
+    {  // digits t*DPT .. t*DPT+DPT-1: wave offsets (prefix over the 4 waves), tile totals
+        int tot[DPT];
+        int mine = 0;
 #pragma unroll
-        for (int k = 0; k < kWaves; ++k) {
-            const int c = sm.cnt[k][t];
-            sm.cnt[k][t] = running;
-            running += c;
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            int running = 0;
+            if (dd < RB) {
+#pragma unroll
+                for (int k = 0; k < kWaves; ++k) {
+                    const int c = sm.cnt[k][dd];
+                    sm.cnt[k][dd] = running;
+                    running += c;
+                }
+            }
+            tot[j] = running;
+            mine += running;
         }
-        const int incl = wave_incl_scan(running);  // block exclusive scan of the totals
+        const int incl = wave_incl_scan(mine);  // block exclusive scan of the threads' totals
         if (lane == 63) sm.wsum[w] = incl;
         __syncthreads();
         int woff = 0;
         for (int q = 0; q < w; ++q) woff += sm.wsum[q];
-        sm.tile_start[t] = woff + incl - running;
-        sm.gofs[t] = hist_scanned[(int64_t)blockIdx.x * 256 + t];  // block-major row
+        int at = woff + incl - mine;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            if (dd < RB) {
+                sm.tile_start[dd] = at;
+                sm.gofs[dd] = hist_off[(int64_t)blockIdx.x * RB + dd];  // block-major row
+            }
+            at += tot[j];
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kRItems; ++r) {
         if (dr[r] != 0xFFFFFFFFu) {
-            const uint32_t d = dr[r] & 255u;
-            const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 8);
+            const uint32_t d = dr[r] & 1023u;
+            const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 10);
             sm.keys[lpos] = k_r[r];
             sm.vals[lpos] = v_r[r];
         }
@@ -418,12 +454,12 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     __syncthreads();
     for (int j = t; j < tile_n; j += kBlock) {
         const uint32_t k = sm.keys[j];
-        const uint32_t d = (k >> shift) & 255u;
+        const uint32_t d = (k >> shift) & (RB - 1u);
         const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
         const int32_t v = sm.vals[j];
         key_out[g] = k;
         val_out[g] = v;
-        if (last) inv[v] = (int32_t)g;
+        if (last && inv) inv[v] = (int32_t)g;
     }
 }
 
@@ -547,40 +583,53 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 }
 
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
-                      int32_t*& val2, int64_t n, int max_bits, const int32_t* bits_dev,
-                      DevBuf& hist, ScanState& scan, Profiler* prof, int32_t* inv) {
-    if (n <= 0 || max_bits <= 0) return;
+                      int32_t*& val2, uint32_t*& key3, int32_t*& val3, int64_t n,
+                      const int32_t* bits_dev, DevBuf& hist, ScanState& scan, Profiler* prof,
+                      int32_t* inv) {
+    if (n <= 0) return;
     const int64_t nb = (n + kRTile - 1) / kRTile;
-    // per-tile digit counts (block-major) and the tiles' global digit offsets
-    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * nb * 256 * sizeof(int32_t)));
-    int32_t* ho = h + nb * 256;
-    for (int shift = 0; shift < max_bits; shift += 8) {
+    // per-tile digit counts (block-major) and the tiles' global digit offsets, for RB <= 512
+    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * nb * 512 * sizeof(int32_t)));
+    int32_t* ho = h + nb * 512;
+    // ping-pong A = (key, val) -> B = (key2, val2) -> A ...; the last sorting pass writes C
+    uint32_t* kin = key;
+    int32_t* vin = val;
+    uint32_t* kpp = key2;
+    int32_t* vpp = val2;
+    const auto pass = [&](auto wtag, int shift) {
+        constexpr int W = decltype(wtag)::value;
         {
             StageTimer st(prof, s, "sort_upsweep");
-            klaunch(prof, "radix_upsweep", radix_upsweep_kernel, dim3((unsigned)nb), dim3(kBlock),
-                    0, s, key, n, shift, bits_dev, nb, h);
+            klaunch(prof, "radix_upsweep", radix_upsweep_kernel<W>, dim3((unsigned)nb),
+                    dim3(kBlock), 0, s, kin, n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer st(prof, s, "sort_scan");
-            uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 256);
-            klaunch(prof, "radix_offsets", radix_offsets_kernel, dim3(kOffBlocks),
-                    dim3(256 * kOffGroups), 0,
-                    s, (const int32_t*)h, nb, ho, state, scan.epoch);
+            uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 512);
+            klaunch(prof, "radix_offsets", radix_offsets_kernel<W>, dim3(kOffBlocks),
+                    dim3(kOffThreads), 0, s, (const int32_t*)h, nb, ho, state, scan.epoch,
+                    bits_dev, shift);
         }
         {
             StageTimer st(prof, s, "sort_downsweep");
-            klaunch(prof, "radix_downsweep", radix_downsweep_kernel, dim3((unsigned)nb),
-                    dim3(kBlock), 0, s, key, val, key2, val2, n, shift, bits_dev, nb, ho, inv);
+            klaunch(prof, "radix_downsweep", radix_downsweep_kernel<W>, dim3((unsigned)nb),
+                    dim3(kBlock), 0, s, kin, vin, kpp, vpp, key3, val3, n, shift, bits_dev, nb,
+                    ho, inv);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        uint32_t* tk = key;
-        key = key2;
-        key2 = tk;
-        int32_t* tv = val;
-        val = val2;
-        val2 = tv;
-    }
+        std::swap(kin, kpp);
+        std::swap(vin, vpp);
+    };
+    // the 9-bit digit last: the high key bits (tile rows) are the most concentrated digits,
+    // so its 512 digit runs per tile stay long enough to write coalesced
+    pass(std::integral_constant<int, 8>{}, 0);
+    pass(std::integral_constant<int, 8>{}, 8);
+    pass(std::integral_constant<int, 9>{}, 16);
+    pass(std::integral_constant<int, 7>{}, 25);
+    // the sorted pairs are in C whatever the key width
+    std::swap(key, key3);
+    std::swap(val, val3);
 }
 
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
