@@ -77,6 +77,24 @@ void Profiler::flush() {
     pending.clear();
 }
 
+void Profiler::flush_ready() {
+    std::vector<Pending> keep;
+    for (auto& pe : pending) {
+        if (hipEventQuery(pe.b) != hipSuccess) {
+            keep.push_back(pe);
+            continue;
+        }
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            stages[pe.stage].ms += ms;
+            stages[pe.stage].launches += 1;
+        }
+        pool.push_back(pe.a);
+        pool.push_back(pe.b);
+    }
+    pending.swap(keep);
+}
+
 void Profiler::destroy() {
     for (auto& pe : pending) {
         pool.push_back(pe.a);
@@ -161,6 +179,9 @@ struct dbscan_handle {
     dbscan::SlabState slab;
     dbscan::DevBuf hx, hy, hcl, hfl;  // staging for the host-array entry points
     bool pending = false;             // an asynchronous fit whose stats are not read yet
+    bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
+    void* pinned = nullptr;           // small pinned host block (stats, root count)
+    hipEvent_t ready = nullptr;       // marks the root count inside a prepare call
     std::mutex mu;                    // one fit at a time per handle
 };
 
@@ -268,6 +289,8 @@ void dbscan_destroy(dbscan_handle* h) {
     h->hy.release();
     h->hcl.release();
     h->hfl.release();
+    if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->ready) (void)hipEventDestroy(h->ready);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -299,6 +322,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         h->pending = false;  // a newer fit replaces the unread stats of an older one
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
+        h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
         h->pending = true;
@@ -332,6 +356,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
         check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
+        h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
         if (n_clusters_out) *n_clusters_out = (int32_t)k;
@@ -362,6 +387,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
+        h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
                                         hipMemcpyDeviceToHost, h->stream));
@@ -534,6 +560,7 @@ int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double
         if (n > 0 && !d_zone) throw dbscan::ArgError{"NULL zone pointer"};
         dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
                           nullptr, d_core, d_root};
+        h->prepared = false;
         dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
         return DBSCAN_OK;
@@ -555,6 +582,7 @@ int32_t dbscan_slab_fit_device_async(dbscan_handle* h, const double* d_x, const 
         h->pending = false;
         dbscan::FitArgs a{d_x, d_y, d_zone, n, eps, min_points, DBSCAN_MODE_NAIVE, nullptr,
                           nullptr, d_core, d_root};
+        h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         h->pending = true;
         return DBSCAN_OK;
@@ -583,6 +611,7 @@ int32_t dbscan_slab_fit_shared_device_async(dbscan_handle* h, const double* d_x,
         static const int64_t kNone = 0;
         a.shared_idx = n_shared > 0 ? d_shared : &kNone;  // non-null: the lean output
         a.n_shared = n_shared;
+        h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         h->pending = true;
         return DBSCAN_OK;
@@ -605,6 +634,71 @@ int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_
             throw dbscan::ArgError{"NULL array pointer"};
         *n_own_out = dbscan::run_slab_merge_roots(h->stream, h->ws, n, d_zone, d_gid, d_root,
                                                   d_parent, d_gs_of_root, d_own_roots);
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_slab_roots_prepare_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
+                                         const int64_t* d_gid, const int32_t* d_root,
+                                         const int32_t* d_parent, int64_t* d_gs_of_root,
+                                         int32_t mode, int64_t* d_own_roots,
+                                         int64_t* n_own_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (n < 0 || !n_own_out) throw dbscan::ArgError{"bad merge-roots arguments"};
+        if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
+            throw dbscan::ArgError{"bad mode"};
+        if (!h->slab.valid) throw dbscan::ArgError{"no slab fit on this handle"};
+        if (n != h->slab.n) throw dbscan::ArgError{"n differs from the slab fit's point count"};
+        if (n > 0 && (!d_zone || !d_gid || !d_root || !d_parent || !d_gs_of_root || !d_own_roots))
+            throw dbscan::ArgError{"NULL array pointer"};
+        if (!h->pinned)
+            DBSCAN_HIP_CHECK(hipHostMalloc(&h->pinned, 512, hipHostMallocDefault));
+        if (!h->ready) DBSCAN_HIP_CHECK(hipEventCreateWithFlags(&h->ready, hipEventDisableTiming));
+        double* stats_buf = static_cast<double*>(h->pinned);
+        int32_t* total = reinterpret_cast<int32_t*>(stats_buf + dbscan::kFitStatsDoubles);
+        const bool fit_pending = h->pending;
+        if (fit_pending) dbscan::enqueue_fit_stats_copy(h->stream, h->ws, stats_buf);
+        dbscan::enqueue_slab_merge_roots(h->stream, h->ws, n, d_zone, d_gid, d_root, d_parent,
+                                         d_gs_of_root, d_own_roots, total);
+        DBSCAN_HIP_CHECK(hipEventRecord(h->ready, h->stream));
+        // Enqueued behind the count: the GPU labels while the host waits, gathers and numbers.
+        dbscan::enqueue_slab_label_prepare(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gid,
+                                           d_gs_of_root, mode);
+        DBSCAN_HIP_CHECK(hipEventSynchronize(h->ready));
+        if (fit_pending) {
+            h->pending = false;
+            h->stats = dbscan::parse_fit_stats(h->ws, stats_buf);
+            h->slab.nf = h->stats.nf;
+        }
+        h->prof.flush_ready();
+        h->prepared = true;
+        *n_own_out = *total;
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_slab_label_finish_device_async(dbscan_handle* h, const uint8_t* d_zone,
+                                              const int64_t* d_gs_of_root,
+                                              const int64_t* d_all_roots, int64_t n_all_roots,
+                                              int32_t* d_cluster, uint8_t* d_flag) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (!h->prepared) throw dbscan::ArgError{"no dbscan_slab_roots_prepare_device since the slab fit"};
+        if (n_all_roots < 0) throw dbscan::ArgError{"n_all_roots < 0"};
+        if (h->slab.n > 0 && (!d_zone || !d_gs_of_root || !d_cluster || !d_flag ||
+                              (n_all_roots > 0 && !d_all_roots)))
+            throw dbscan::ArgError{"NULL array pointer"};
+        dbscan::run_slab_label_finish(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gs_of_root,
+                                      d_all_roots, n_all_roots, d_cluster, d_flag);
         return DBSCAN_OK;
     });
 }

@@ -2379,8 +2379,10 @@ __device__ __forceinline__ uint32_t cluster_of_root(const uint64_t* __restrict__
 // it to input order with one random 4-B read per point (the packed array was just written and
 // is cache-resident), instead of two scattered partial-line writes (cluster 4 B + flag 1 B).
 // Slab fits (SLAB) label zone-0 points from the merged global component ids.  Slots >= nf are
-// outside the grid: never anyone's neighbour.
-template <bool SLAB>
+// outside the grid: never anyone's neighbour.  ROOTS (slab fits only): the numbering is not
+// known yet, so the packed value names the local root instead, ((root + 1) << 1) | core, and
+// slab_map_kernel turns it into a cluster id once the roots are numbered.
+template <bool SLAB, bool ROOTS = false>
 __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ nbr, int nbr_k,
@@ -2395,8 +2397,9 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const int64_t nf = *nf_p;
     uint32_t v = 0;  // Noise
     if (core[p]) {
-        const uint32_t cl = SLAB ? (uint32_t)label_of_root[lab[p]]
-                                 : cluster_of_root(root_bits, word_rank, lab[p]);
+        const uint32_t cl = ROOTS ? (uint32_t)lab[p] + 1u
+                            : SLAB ? (uint32_t)label_of_root[lab[p]]
+                                   : cluster_of_root(root_bits, word_rank, lab[p]);
         v = (cl << 1) | 1u;
     } else if (p < nf) {
         const int32_t o = perm[p];
@@ -2433,8 +2436,9 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
         }
         const int64_t self = SLAB ? gid[o] : (int64_t)o;
         if (mr >= 0 && (mode != 0 || m < self)) {
-            const uint32_t cl = SLAB ? (uint32_t)label_of_root[mr]
-                                     : cluster_of_root(root_bits, word_rank, mr);
+            const uint32_t cl = ROOTS ? (uint32_t)mr + 1u
+                                : SLAB ? (uint32_t)label_of_root[mr]
+                                       : cluster_of_root(root_bits, word_rank, mr);
             v = cl << 1;  // Border
         }
     }
@@ -2453,6 +2457,33 @@ __global__ __launch_bounds__(kBlock) void permute_out_kernel(
     if (SLAB && zone[i] != 0) return;
     const uint32_t v = packed[inv[i]];
     cluster_out[i] = (int32_t)(v >> 1);
+    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
+}
+
+// Two-part slab label (dbscan_slab_roots_prepare_device + dbscan_slab_label_finish_device_async):
+// the ROOTS-packed labels moved to slab order before the roots are numbered (zone 1/2 entries
+// 0), so the part that waits for the numbering is one coalesced pass.
+__global__ __launch_bounds__(kBlock) void slab_permute_kernel(int64_t n,
+                                                              const int32_t* __restrict__ inv,
+                                                              const uint32_t* __restrict__ packed,
+                                                              const uint8_t* __restrict__ zone,
+                                                              uint32_t* __restrict__ spacked) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    spacked[i] = zone[i] == 0 ? packed[inv[i]] : 0u;
+}
+
+// Slab order: cluster = label_of_root[root], flag Core / Border / Noise as permute_out_kernel.
+__global__ __launch_bounds__(kBlock) void slab_map_kernel(int64_t n,
+                                                          const uint32_t* __restrict__ spacked,
+                                                          const uint8_t* __restrict__ zone,
+                                                          const int32_t* __restrict__ label_of_root,
+                                                          int32_t* __restrict__ cluster_out,
+                                                          uint8_t* __restrict__ flag_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || zone[i] != 0) return;
+    const uint32_t v = spacked[i];
+    cluster_out[i] = v == 0 ? 0 : label_of_root[(v >> 1) - 1u];
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
 
@@ -2969,14 +3000,24 @@ void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
+void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst) {
+    if (ws.fit_n == 0) return;
+    DBSCAN_HIP_CHECK(
+        hipMemcpyAsync(dst, ws.misc.p, kFitStatsDoubles * sizeof(double), hipMemcpyDeviceToHost, s));
+}
+
 FitStats read_fit_stats(hipStream_t s, Workspace& ws) {
+    double buf[kFitStatsDoubles];
+    enqueue_fit_stats_copy(s, ws, buf);
+    if (ws.fit_n != 0) DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    return parse_fit_stats(ws, buf);
+}
+
+FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
     FitStats stats;
     stats.n = ws.fit_n;
     stats.grid_mode = ws.fit_mode;
     if (ws.fit_n == 0) return stats;
-    double buf[24];
-    DBSCAN_HIP_CHECK(hipMemcpyAsync(buf, ws.misc.p, sizeof(buf), hipMemcpyDeviceToHost, s));
-    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
     GridParams g;
     memcpy(&g, buf + 8, sizeof(g));
     int32_t v[kStCount];
@@ -3032,6 +3073,44 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                        gs_of_root, label_of_root, packed);
     klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
+                                const SlabState& st, const uint8_t* zone, const int64_t* gid,
+                                const int64_t* gs_of_root, int32_t mode) {
+    if (!st.valid) throw ArgError{"dbscan_slab_roots_prepare_device: no slab fit on this handle"};
+    if (st.n == 0) return;
+    StageTimer t(prof, s, "slab_label");
+    uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
+    klaunch(prof, "label_sorted", label_sorted_kernel<true, true>, dim3(nblk(st.n)), dim3(kBlock), 0,
+            s, static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
+            static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
+            reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) + kStNf, st.n,
+            st.eps2, mode, static_cast<const int32_t*>(ws.perm_sorted),
+            static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
+            (const uint64_t*)nullptr, (const int32_t*)nullptr, zone, gid, gs_of_root,
+            (const int32_t*)nullptr, packed);
+    uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
+    klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
+            static_cast<const int32_t*>(ws.inv.p), packed, zone, spacked);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
+                           const uint8_t* zone, const int64_t* gs_of_root,
+                           const int64_t* all_roots, int64_t n_roots, int32_t* cluster,
+                           uint8_t* flag) {
+    if (!st.valid) throw ArgError{"dbscan_slab_label_finish_device_async: no slab fit on this handle"};
+    if (st.n == 0) return;
+    StageTimer t(prof, s, "slab_label");
+    int32_t* label_of_root = static_cast<int32_t*>(ws.slab_lor.ensure(st.n * sizeof(int32_t)));
+    klaunch(prof, "slab_root_labels", slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+            st.n, static_cast<const int32_t*>(ws.perm_sorted),
+            static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
+            gs_of_root, all_roots, n_roots, label_of_root);
+    klaunch(prof, "slab_map", slab_map_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
+            static_cast<const uint32_t*>(ws.spacked.p), zone, label_of_root, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 

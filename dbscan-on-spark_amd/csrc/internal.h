@@ -109,6 +109,7 @@ struct Profiler {
     hipEvent_t take();
     int stage_index(const char* name);
     void flush();  // after the stream is synchronized: accumulate and recycle events
+    void flush_ready();  // the same for the completed pairs only (the stream may still run)
     void destroy();
 };
 
@@ -148,7 +149,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3;
+        key3, perm3, spacked;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -160,7 +161,7 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3})
+                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked})
             b->release();
     }
 };
@@ -216,7 +217,21 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
 void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                  SlabState* slab);
 FitStats read_fit_stats(hipStream_t s, Workspace& ws);
+// read_fit_stats in two halves: an asynchronous copy of the stats block to dst (pinned host
+// memory, kFitStatsDoubles doubles), and its parse once the copy has completed.
+constexpr int kFitStatsDoubles = 24;
+void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst);
+FitStats parse_fit_stats(const Workspace& ws, const double* buf);
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);
+// The slab label in two parts around the cluster numbering: prepare (labels in terms of local
+// roots, moved to slab order; needs only gs_of_root) and finish (roots numbered, one map pass).
+void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
+                                const SlabState& st, const uint8_t* zone, const int64_t* gid,
+                                const int64_t* gs_of_root, int32_t mode);
+void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
+                           const uint8_t* zone, const int64_t* gs_of_root,
+                           const int64_t* all_roots, int64_t n_roots, int32_t* cluster,
+                           uint8_t* flag);
 void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabState& st,
                     const uint8_t* zone, const int64_t* gid, const int64_t* gs_of_root,
                     const int64_t* all_roots, int64_t n_roots, int32_t mode, int32_t* cluster,
@@ -252,6 +267,10 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
 int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
                              const int64_t* gid, const int32_t* root, const int32_t* parent,
                              int64_t* gs_of_root, int64_t* own_roots);
+// The same without waiting: the count is copied to *total_dst (pinned host memory) on s.
+void enqueue_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
+                              const int64_t* gid, const int32_t* root, const int32_t* parent,
+                              int64_t* gs_of_root, int64_t* own_roots, int32_t* total_dst);
 
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:

@@ -154,7 +154,19 @@ namespace dbscan {
 int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
                              const int64_t* gid, const int32_t* root, const int32_t* parent,
                              int64_t* gs_of_root, int64_t* own_roots) {
-    if (n == 0) return 0;
+    int32_t total = 0;
+    enqueue_slab_merge_roots(s, ws, n, zone, gid, root, parent, gs_of_root, own_roots, &total);
+    if (n > 0) DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    return total;
+}
+
+void enqueue_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
+                              const int64_t* gid, const int32_t* root, const int32_t* parent,
+                              int64_t* gs_of_root, int64_t* own_roots, int32_t* total_dst) {
+    if (n == 0) {
+        *total_dst = 0;
+        return;
+    }
     const int64_t nb = (n + kRootTile - 1) / kRootTile;
     int32_t* cnt = static_cast<int32_t*>(ws.own_flag.ensure((2 * nb + 2) * sizeof(int32_t)));
     int32_t* off = cnt + nb + 1;
@@ -165,10 +177,7 @@ int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint
     hipLaunchKernelGGL(roots_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, n, zone, gid,
                        root, parent, off, own_roots);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    int32_t total = 0;
-    DBSCAN_HIP_CHECK(hipMemcpyAsync(&total, off + nb, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-    return total;
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(total_dst, off + nb, sizeof(int32_t), hipMemcpyDeviceToHost, s));
 }
 
 }  // namespace dbscan

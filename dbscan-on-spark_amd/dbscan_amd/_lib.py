@@ -54,6 +54,9 @@ SIGNATURES = [
     ("dbscan_merge_union_device", _i32, [_vp, _vp, _i64, _vp, _vp]),
     ("dbscan_merge_reset_device", _i32, [_vp, _vp, _i64, _vp, _vp]),
     ("dbscan_slab_merge_roots_device", _i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("dbscan_slab_roots_prepare_device", _i32,
+     [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    ("dbscan_slab_label_finish_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
 ]
 

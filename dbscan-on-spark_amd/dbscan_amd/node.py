@@ -162,7 +162,8 @@ class HipSlabOps:
     """The product slab fit and merge: libdbscan_hip.so through device tensors.  The slab fit
     and label run asynchronously on the handle's stream, ordered against torch's current stream
     by stream waits (no host synchronization); the merge kernels run on torch's stream.  A step
-    synchronizes the host only for the owned-root count and the all-gather sizes."""
+    synchronizes the host only for the owned-root count (while the label's first part runs on
+    the GPU) and the all-gather sizes."""
 
     def __init__(self, handle: _lib.Handle):
         self.h = handle
@@ -210,15 +211,24 @@ class HipSlabOps:
         _lib.check(_lib.load().dbscan_merge_reset_device(_p(a), _p(b), a.numel(), _p(parent),
                                                          self._stream()))
 
-    def merge_roots(self, zone, gid, root, parent, gs_of_root):
+    def merge_roots(self, zone, gid, root, parent, gs_of_root, mode=None):
+        """The owned global roots.  With mode given, the label's first part (which needs only
+        gs_of_root) is enqueued behind the count and runs while the host gathers and numbers
+        the roots (dbscan_slab_roots_prepare_device); label() then finishes it."""
         n = zone.numel()
         if self._bufs is None or self._bufs.numel() < max(1, n):
             self._bufs = torch.empty(max(1, n), dtype=torch.int64, device=zone.device)
         k = ctypes.c_int64(0)
         self._to_handle()
-        _lib.check(_lib.load().dbscan_slab_merge_roots_device(
-            self.h.ptr, n, _p(zone), _p(gid), _p(root), _p(parent), _p(gs_of_root),
-            _p(self._bufs), ctypes.byref(k)))  # synchronizes the handle stream (the count)
+        if mode is None:
+            _lib.check(_lib.load().dbscan_slab_merge_roots_device(
+                self.h.ptr, n, _p(zone), _p(gid), _p(root), _p(parent), _p(gs_of_root),
+                _p(self._bufs), ctypes.byref(k)))  # synchronizes the handle stream (the count)
+        else:
+            _lib.check(_lib.load().dbscan_slab_roots_prepare_device(
+                self.h.ptr, n, _p(zone), _p(gid), _p(root), _p(parent), _p(gs_of_root),
+                int(mode), _p(self._bufs), ctypes.byref(k)))  # waits for the count only
+        self._prepared = mode
         return self._bufs[:int(k.value)]
 
     def label(self, zone, gid, gs_of_root, all_roots, mode):
@@ -227,9 +237,15 @@ class HipSlabOps:
         flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
         all_roots = all_roots.to(torch.int64).contiguous()
         self._to_handle()
-        _lib.check(_lib.load().dbscan_slab_label_device_async(
-            self.h.ptr, _p(zone), _p(gid), _p(gs_of_root), _p(all_roots), all_roots.numel(),
-            int(mode), _p(cluster), _p(flag)))
+        if getattr(self, "_prepared", None) == mode:
+            _lib.check(_lib.load().dbscan_slab_label_finish_device_async(
+                self.h.ptr, _p(zone), _p(gs_of_root), _p(all_roots), all_roots.numel(),
+                _p(cluster), _p(flag)))
+        else:
+            _lib.check(_lib.load().dbscan_slab_label_device_async(
+                self.h.ptr, _p(zone), _p(gid), _p(gs_of_root), _p(all_roots), all_roots.numel(),
+                int(mode), _p(cluster), _p(flag)))
+        self._prepared = None
         self._from_handle()
         return cluster, flag
 
@@ -305,7 +321,8 @@ class NodeJob:
         self.ops.merge(self.all_a, all_b, self.parent)
         tick("merge")
         # every local root's global s(K); the zone-0 global roots owned here
-        own = self.ops.merge_roots(self.zone, self.gid, root, self.parent, self.gs_of_root)
+        own = self.ops.merge_roots(self.zone, self.gid, root, self.parent, self.gs_of_root,
+                                   mode=self.mode)
         tick("roots")
         # cluster id = 1 + rank of s(K) among all ranks' global roots (each rank's list is
         # already in gid order)

@@ -244,6 +244,27 @@ int32_t dbscan_slab_merge_roots_device(dbscan_handle* h, int64_t n, const uint8_
                                        const int32_t* d_parent, int64_t* d_gs_of_root,
                                        int64_t* d_own_roots, int64_t* n_own_out);
 
+/* dbscan_slab_merge_roots_device and dbscan_slab_label_device_async split around the cluster
+ * numbering, so the host's wait for the owned-root count (and the caller's all-gather of the
+ * roots) overlaps GPU work (dbscan_amd/node.py):
+ * dbscan_slab_roots_prepare_device (after a slab fit on this handle, n = its point count):
+ *   everything dbscan_slab_merge_roots_device does, then enqueues the part of the label that
+ *   needs only d_gs_of_root (each zone-0 point's local root, moved to slab order); returns once
+ *   the count is known (*n_own_out), while that label work is still running.
+ * dbscan_slab_label_finish_device_async (same handle, no fit in between): numbers the local
+ *   roots from d_all_roots (as dbscan_slab_label_device) and writes d_cluster / d_flag of the
+ *   zone-0 points; zone 1/2 entries are left untouched.  Outputs equal
+ *   dbscan_slab_label_device's.  Both replace the relabel of DBSCAN.scala:232-270. */
+int32_t dbscan_slab_roots_prepare_device(dbscan_handle* h, int64_t n, const uint8_t* d_zone,
+                                         const int64_t* d_gid, const int32_t* d_root,
+                                         const int32_t* d_parent, int64_t* d_gs_of_root,
+                                         int32_t mode, int64_t* d_own_roots,
+                                         int64_t* n_own_out);
+int32_t dbscan_slab_label_finish_device_async(dbscan_handle* h, const uint8_t* d_zone,
+                                              const int64_t* d_gs_of_root,
+                                              const int64_t* d_all_roots, int64_t n_all_roots,
+                                              int32_t* d_cluster, uint8_t* d_flag);
+
 /* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
  * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the
  * visit order.  Writes d_x, d_y (device).  Used by bench.py so 10^7..10^9 points need no PCIe. */

@@ -52,7 +52,7 @@ class OracleSlabOps:
         parent[a[ok]] = -1
         parent[b[ok]] = -1
 
-    def merge_roots(self, zone, gid, root, parent, gs_of_root):
+    def merge_roots(self, zone, gid, root, parent, gs_of_root, mode=None):
         n = zone.numel()
         lroots = torch.nonzero(root == torch.arange(n, dtype=root.dtype)).flatten()
         g = gid[lroots]

@@ -154,3 +154,53 @@ def test_lean_slab_fit_matches_full():
         rest &= ~is_root
         assert bool((root_l[rest] == -1).all())
     h.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_two_part_slab_label_matches_one_part(mode):
+    """dbscan_slab_roots_prepare_device + dbscan_slab_label_finish_device_async (the node step's
+    form) against dbscan_slab_merge_roots_device + dbscan_slab_label_device_async on the same
+    slab fits (zones 0/1/2 of a 3-way cut): identical owned roots, labels and flags; zone 1/2
+    entries untouched.  A fit in between invalidates the prepared state."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import _lib, node
+
+    dbscan_amd.load()
+    x, y = gen_blobs(500_000, noise=0.2, seed=11)
+    tx, ty = torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda")
+    cuts = node.make_cuts(tx, 3, 2.55)
+    h = dbscan_amd.Handle(0)
+    ops = node.HipSlabOps(h)
+    for rank in range(3):
+        z, sh = node.zones(tx, rank, cuts, 2.55)
+        idx = torch.nonzero(z != node.OUT).flatten()
+        sx, sy, sz = tx[idx].contiguous(), ty[idx].contiguous(), z[idx].contiguous()
+        gid = idx.to(torch.int64).contiguous()
+        shared = torch.nonzero(sh[idx]).flatten()
+        par = torch.full((x.size,), -1, dtype=torch.int32, device="cuda")
+        out = []
+        for two_part in (False, True):
+            _, root = ops.fit(sx, sy, sz, 2.55, 10, shared=shared)
+            gs = torch.zeros(sx.numel(), dtype=torch.int64, device="cuda")
+            own = ops.merge_roots(sz, gid, root, par, gs, mode=mode if two_part else None)
+            own = own.clone()
+            cl, fl = ops.label(sz, gid, gs, torch.sort(own)[0], mode)
+            torch.cuda.synchronize()
+            out.append((own.cpu(), cl.cpu(), fl.cpu()))
+        assert torch.equal(out[0][0], out[1][0])
+        assert torch.equal(out[0][1], out[1][1])
+        assert torch.equal(out[0][2], out[1][2])
+        outside = (sz != 0).cpu()
+        assert bool((out[1][2][outside] == 3).all()) and bool((out[1][1][outside] == 0).all())
+        assert bool((out[1][2][~outside] <= 2).all())
+    # finish without a prepare since the last fit: an argument error, not stale labels
+    ops.fit(sx, sy, sz, 2.55, 10, shared=shared)
+    cl = torch.zeros(sx.numel(), dtype=torch.int32, device="cuda")
+    fl = torch.zeros(sx.numel(), dtype=torch.uint8, device="cuda")
+    roots = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rc = _lib.load().dbscan_slab_label_finish_device_async(
+        h.ptr, node._p(sz), node._p(gs), node._p(roots), 1, node._p(cl), node._p(fl))
+    assert rc == _lib.DBSCAN_EARG
+    h.close()
