@@ -8,6 +8,7 @@
 #include "../../include/dbscan_hip.h"
 #include "internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -663,8 +664,9 @@ int32_t dbscan_slab_roots_prepare_device(dbscan_handle* h, int64_t n, const uint
         int32_t* total = reinterpret_cast<int32_t*>(stats_buf + dbscan::kFitStatsDoubles);
         const bool fit_pending = h->pending;
         if (fit_pending) dbscan::enqueue_fit_stats_copy(h->stream, h->ws, stats_buf);
+        int32_t* lroots = static_cast<int32_t*>(h->ws.lroots.ensure(std::max<int64_t>(1, n) * sizeof(int32_t)));
         dbscan::enqueue_slab_merge_roots(h->stream, h->ws, n, d_zone, d_gid, d_root, d_parent,
-                                         d_gs_of_root, d_own_roots, total);
+                                         d_gs_of_root, d_own_roots, total, lroots);
         DBSCAN_HIP_CHECK(hipEventRecord(h->ready, h->stream));
         // Enqueued behind the count: the GPU labels while the host waits, gathers and numbers.
         dbscan::enqueue_slab_label_prepare(h->stream, h->ws, &h->prof, h->slab, d_zone, d_gid,
@@ -677,7 +679,8 @@ int32_t dbscan_slab_roots_prepare_device(dbscan_handle* h, int64_t n, const uint
         }
         h->prof.flush_ready();
         h->prepared = true;
-        *n_own_out = *total;
+        h->slab.nlroots = total[1] - total[0];
+        *n_own_out = total[0];
         return DBSCAN_OK;
     });
 }

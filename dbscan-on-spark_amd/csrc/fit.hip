@@ -2529,6 +2529,23 @@ __global__ __launch_bounds__(kBlock) void slab_root_labels_kernel(
     label_of_root[r] = (int32_t)(lo + 1);
 }
 
+// The same from the list of local roots the prepare compacted (slab indices): one thread per
+// root instead of one per sorted slot.
+__global__ __launch_bounds__(kBlock) void slab_root_labels_list_kernel(
+    int64_t m, const int32_t* __restrict__ lroots, const int64_t* __restrict__ gs_of_root,
+    const int64_t* __restrict__ all_roots, int64_t n_roots, int32_t* __restrict__ label_of_root) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    const int32_t r = lroots[i];
+    const int64_t g = gs_of_root[r];
+    int64_t lo = 0, hi = n_roots;  // first index with all_roots[idx] >= g
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (all_roots[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    label_of_root[r] = (int32_t)(lo + 1);
+}
+
 // Grid sizing (see DESIGN.md "grid soundness"), on the device so a fit needs no host sync: cell side >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500) bounds |x'-x| for every pair the fp64 predicate accepts;
 // at most 2^23 tiles of 8x8 cells (u32 keys = tile*256 + cell*4 + quadrant, below the
@@ -2685,6 +2702,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (n == 0) {
         if (slab) {
             slab->valid = a.zone != nullptr;
+            slab->nlroots = -1;
             slab->n = 0;
         }
         return;
@@ -2983,6 +3001,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     if (slab) {
         slab->valid = a.zone != nullptr;
+        slab->nlroots = -1;
         slab->n = n;
         slab->eps2 = eps2;
         slab->nbr = nbr;
@@ -3105,10 +3124,17 @@ void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const S
     if (st.n == 0) return;
     StageTimer t(prof, s, "slab_label");
     int32_t* label_of_root = static_cast<int32_t*>(ws.slab_lor.ensure(st.n * sizeof(int32_t)));
-    klaunch(prof, "slab_root_labels", slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
-            st.n, static_cast<const int32_t*>(ws.perm_sorted),
-            static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
-            gs_of_root, all_roots, n_roots, label_of_root);
+    if (st.nlroots >= 0) {
+        if (st.nlroots > 0)
+            klaunch(prof, "slab_root_labels", slab_root_labels_list_kernel, dim3(nblk(st.nlroots)),
+                    dim3(kBlock), 0, s, st.nlroots, static_cast<const int32_t*>(ws.lroots.p),
+                    gs_of_root, all_roots, n_roots, label_of_root);
+    } else {
+        klaunch(prof, "slab_root_labels", slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0,
+                s, st.n, static_cast<const int32_t*>(ws.perm_sorted),
+                static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
+                gs_of_root, all_roots, n_roots, label_of_root);
+    }
     klaunch(prof, "slab_map", slab_map_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
             static_cast<const uint32_t*>(ws.spacked.p), zone, label_of_root, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());

@@ -149,7 +149,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked;
+        key3, perm3, spacked, lroots;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -161,7 +161,7 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked})
+                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots})
             b->release();
     }
 };
@@ -208,6 +208,7 @@ struct SlabState {
     GridParams g{};
     const int32_t* nbr = nullptr;  // non-core neighbour lists (nullptr: label by stencil scan)
     int nbr_k = 0;
+    int64_t nlroots = -1;  // local roots listed in ws.lroots by the last prepare (-1: none)
 };
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
@@ -267,10 +268,13 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
 int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
                              const int64_t* gid, const int32_t* root, const int32_t* parent,
                              int64_t* gs_of_root, int64_t* own_roots);
-// The same without waiting: the count is copied to *total_dst (pinned host memory) on s.
+// The same without waiting: the count is copied to total_dst[0] (pinned host memory) on s.
+// lroots != nullptr: every local root's slab index too, in slab order (the label's root
+// numbering reads only these), and total_dst[1] = total_dst[0] + their count.
 void enqueue_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,
                               const int64_t* gid, const int32_t* root, const int32_t* parent,
-                              int64_t* gs_of_root, int64_t* own_roots, int32_t* total_dst);
+                              int64_t* gs_of_root, int64_t* own_roots, int32_t* total_dst,
+                              int32_t* lroots);
 
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:

@@ -171,6 +171,7 @@ class HipSlabOps:
                                              device=torch.device("cuda", handle.device))
         self._out = None
         self._bufs = None
+        self._lab = None  # (cluster, flag, zone) reused across the steps of one slab
 
     def _to_handle(self):
         self._hs.wait_stream(torch.cuda.current_stream())
@@ -233,11 +234,17 @@ class HipSlabOps:
 
     def label(self, zone, gid, gs_of_root, all_roots, mode):
         n = zone.numel()
-        cluster = torch.zeros(n, dtype=torch.int32, device=zone.device)
-        flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
+        prepared = getattr(self, "_prepared", None) == mode
+        if prepared and self._lab is not None and self._lab[2] is zone:
+            # the same slab again (a job's steps): zone 1/2 entries still hold their fill
+            cluster, flag = self._lab[0], self._lab[1]
+        else:
+            cluster = torch.zeros(n, dtype=torch.int32, device=zone.device)
+            flag = torch.full((n,), 3, dtype=torch.uint8, device=zone.device)
+            self._lab = (cluster, flag, zone) if prepared else None
         all_roots = all_roots.to(torch.int64).contiguous()
         self._to_handle()
-        if getattr(self, "_prepared", None) == mode:
+        if prepared:
             _lib.check(_lib.load().dbscan_slab_label_finish_device_async(
                 self.h.ptr, _p(zone), _p(gs_of_root), _p(all_roots), all_roots.numel(),
                 _p(cluster), _p(flag)))
@@ -326,7 +333,9 @@ class NodeJob:
         tick("roots")
         # cluster id = 1 + rank of s(K) among all ranks' global roots (each rank's list is
         # already in gid order)
-        all_roots, _ = torch.sort(self.comm.allgather_varlen(own))
+        all_roots = self.comm.allgather_varlen(own)
+        if self.comm.world > 1:  # one rank's list is already in gid order
+            all_roots, _ = torch.sort(all_roots)
         self.ops.merge_reset(self.all_a, all_b, self.parent)
         tick("numbering")
         self.cluster, self.flag = self.ops.label(self.zone, self.gid, self.gs_of_root, all_roots,
