@@ -111,8 +111,7 @@ __device__ __forceinline__ void for_candidates(const Seg& s, F f) {
 __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ x,
                                                      const double* __restrict__ y, int64_t n,
                                                      const GridParams* __restrict__ gp,
-                                                     uint32_t* __restrict__ key,
-                                                     int32_t* __restrict__ perm) {
+                                                     uint32_t* __restrict__ key) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const GridParams g = *gp;
@@ -131,8 +130,7 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
         const uint32_t local = ((cy & 7u) << 3) | (cx & 7u);
         k = (tile << 8) | (local << 2) | ((qy & 1u) << 1) | (qx & 1u);
     }
-    key[i] = k;
-    perm[i] = (int32_t)i;
+    key[i] = k;  // the index payload is implicit: the sort's first pass generates it
 }
 
 __global__ __launch_bounds__(kBlock) void iota_key_kernel(int64_t n, uint32_t kval,
@@ -2723,14 +2721,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         {
             StageTimer t(prof, s, "bin");
-            klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key,
-                               perm);
+            klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));
         int32_t* perm3 = static_cast<int32_t*>(ws.perm3.ensure(n * sizeof(int32_t)));
         radix_sort_pairs(s, key, perm, key2, perm2, key3, perm3, n, &st[kStBits], ws.hist,
-                         ws.scan, prof, inv);
+                         ws.scan, prof, inv, /*iota=*/true);
     } else {
         StageTimer t(prof, s, "bin");
         // all pairs: one cell holding every point, the predicate decides (incl. non-finite)

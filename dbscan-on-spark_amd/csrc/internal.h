@@ -291,11 +291,12 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 // passes).  The input is (key, val); the passes ping-pong through (key2, val2) and the last
 // sorting pass writes (key3, val3), whose pointers are then swapped into key/val.  Stable.
 // inv (optional): the inverse permutation of the sorted vals (a permutation of 0..n-1),
-// inv[val] = sorted position, written by the last pass.
+// inv[val] = sorted position, written by the last pass.  iota: the input vals are the identity
+// 0..n-1 and are not read (the first pass generates them; val is then only a ping-pong buffer).
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, uint32_t*& key3, int32_t*& val3, int64_t n,
                       const int32_t* bits_dev, DevBuf& hist, ScanState& scan, Profiler* prof,
-                      int32_t* inv = nullptr);
+                      int32_t* inv = nullptr, bool iota = false);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

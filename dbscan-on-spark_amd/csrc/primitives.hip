@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     const int bits = *bits_p;
     if (bits == 0 && shift == 0) {  // nothing to sort (no grid key bits): the final copy
         for (int j = t; j < tile_n; j += kBlock) {
-            const int32_t v = val[base + j];
+            const int32_t v = val ? val[base + j] : (int32_t)(base + j);
             key_fin[base + j] = key[base + j];
             val_fin[base + j] = v;
             if (inv) inv[v] = (int32_t)(base + j);
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
         const int64_t i = wbase + r * 64 + lane;
         const bool valid = i < base + tile_n;
         const uint32_t k = valid ? key[i] : kSentinelKey;
-        const int32_t v = valid ? val[i] : 0;
+        const int32_t v = valid ? (val ? val[i] : (int32_t)i) : 0;  // val null: the identity
         const uint32_t d = (k >> shift) & (RB - 1u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -585,8 +585,9 @@ void exclusive_scan(hipStream_t s, int mode, const void* in, int32_t* out, int64
 void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& key2,
                       int32_t*& val2, uint32_t*& key3, int32_t*& val3, int64_t n,
                       const int32_t* bits_dev, DevBuf& hist, ScanState& scan, Profiler* prof,
-                      int32_t* inv) {
+                      int32_t* inv, bool iota) {
     if (n <= 0) return;
+    bool first = true;
     const int64_t nb = (n + kRTile - 1) / kRTile;
     // per-tile digit counts (block-major) and the tiles' global digit offsets, for RB <= 512
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * nb * 512 * sizeof(int32_t)));
@@ -614,10 +615,11 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
         {
             StageTimer st(prof, s, "sort_downsweep");
             klaunch(prof, "radix_downsweep", radix_downsweep_kernel<W>, dim3((unsigned)nb),
-                    dim3(kBlock), 0, s, kin, vin, kpp, vpp, key3, val3, n, shift, bits_dev, nb,
-                    ho, inv);
+                    dim3(kBlock), 0, s, kin, (first && iota) ? (const int32_t*)nullptr : vin, kpp,
+                    vpp, key3, val3, n, shift, bits_dev, nb, ho, inv);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
+        first = false;
         std::swap(kin, kpp);
         std::swap(vin, vpp);
     };
