@@ -183,6 +183,18 @@ __global__ __launch_bounds__(kBlock) void zone_mark_kernel(int64_t n,
 // heads_down ranks each slot within its tile with wave ballots and writes the group tables.
 constexpr int kHeadTile = 4096;
 
+// XCD-aware block order (edge_union_kernel): workgroups are dispatched round-robin over the 8
+// XCDs (block b on XCD b % 8), each with its own L2.  The remapped index gives every XCD a
+// contiguous range of tiles, so tiles that share halo cells run under the same L2: edge_union
+// 0.208 -> 0.193 ms (r12).  The count kernels stay round-robin: their class lists put the dense
+// tiles together, and contiguous ranges unbalanced the XCDs (count32 0.32 -> 0.42 ms).  A
+// bijection of 0..gridDim.x-1 for any grid size.
+__device__ __forceinline__ int xcd_block() {
+    const int G = gridDim.x, b = blockIdx.x;
+    const int x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + (x < r ? x : r) + j;
+}
+
 struct Heads {
     bool c, q, t;
 };
@@ -2196,7 +2208,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     int* lp = nlp[w];
     const auto gcore = [core](int j) { return core[j] != 0; };
     // one (tile, side) per wave and loop trip: waves never wait for each other
-    for (int tw = blockIdx.x * (kBlock / 64) + w; tw < 2 * ntiles;
+    for (int tw = xcd_block() * (kBlock / 64) + w; tw < 2 * ntiles;
          tw += gridDim.x * (kBlock / 64)) {
         const int t = tw >> 1, side = tw & 1;
         int nA = 0, ntot = 0;
