@@ -63,6 +63,13 @@ def test_null_handle_errors():
     rc = L.dbscan_fit_device(None, None, None, 0, 0.3, 10, 0, None, None, None)
     assert rc == _lib.DBSCAN_EARG
     assert L.dbscan_last_stats(None, None, 0) == _lib.DBSCAN_EARG
+    n_own = ctypes.c_int64(0)
+    rc = L.dbscan_slab_roots_prepare_device(None, 0, None, None, None, None, None, 0, None,
+                                            ctypes.byref(n_own))
+    assert rc == _lib.DBSCAN_EARG
+    assert b"NULL handle" in L.dbscan_last_error()
+    rc = L.dbscan_slab_label_finish_device_async(None, None, None, None, 0, None, None)
+    assert rc == _lib.DBSCAN_EARG
 
 
 @pytest.mark.skipif(_lib.load().dbscan_device_count() > 0, reason="GPU present")
