@@ -173,7 +173,8 @@ __global__ __launch_bounds__(256) void gen_blobs_kernel(BlobParams bp, int64_t n
 
 struct dbscan_handle {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // where the handle's work runs
+    hipStream_t own_stream = nullptr;  // the stream the handle created (and destroys)
     dbscan::Workspace ws;
     dbscan::Profiler prof;
     dbscan::FitStats stats;
@@ -271,7 +272,8 @@ dbscan_handle* dbscan_create(int32_t device) {
     }
     h->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    h->stream = h->own_stream;
     if (e != hipSuccess) {
         set_err(std::string("hipStreamCreate failed: ") + hipGetErrorString(e));
         delete h;
@@ -284,6 +286,7 @@ void dbscan_destroy(dbscan_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
     h->prof.destroy();
     h->ws.release();
     h->hx.release();
@@ -292,11 +295,12 @@ void dbscan_destroy(dbscan_handle* h) {
     h->hfl.release();
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->ready) (void)hipEventDestroy(h->ready);
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
 }
 
 void* dbscan_stream(dbscan_handle* h) { return h ? (void*)h->stream : nullptr; }
+
 
 namespace {
 // Completes an asynchronous fit on the host side: waits for the stream, reads its stats
@@ -308,6 +312,21 @@ void settle(dbscan_handle* h) {
     h->prof.flush();
 }
 }  // namespace
+
+int32_t dbscan_set_stream(dbscan_handle* h, void* stream, int32_t own) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        h->prof.flush();
+        h->stream = own ? h->own_stream : static_cast<hipStream_t>(stream);
+        return DBSCAN_OK;
+    });
+}
 
 int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
                                 int64_t n, double eps, int32_t min_points, int32_t mode,

@@ -33,6 +33,7 @@ SIGNATURES = [
     ("dbscan_fit_device_async", _i32, [_vp, _vp, _vp, _i64, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_sync", _i32, [_vp]),
     ("dbscan_stream", _vp, [_vp]),
+    ("dbscan_set_stream", _i32, [_vp, _vp, _i32]),
     ("dbscan_last_stats", _i32, [_vp, _vp, _i32]),
     ("dbscan_profile_enable", _i32, [_vp, _i32]),
     ("dbscan_profile_only", _i32, [_vp, ctypes.c_char_p]),

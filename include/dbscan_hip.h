@@ -101,6 +101,11 @@ int32_t dbscan_sync(dbscan_handle* h);
 
 /* The handle's hipStream_t (as void*), for callers that order their own work around it. */
 void* dbscan_stream(dbscan_handle* h);
+/* Run the handle's work on the caller's stream (a hipStream_t of the handle's device, as void*;
+ * NULL is the device's null stream) from now on, so a caller whose own work is on that stream
+ * needs no cross-stream waits; own != 0 returns to the handle's own stream (stream ignored).
+ * Waits for the work already enqueued.  The handle never destroys a caller's stream. */
+int32_t dbscan_set_stream(dbscan_handle* h, void* stream, int32_t own);
 
 /* Statistics of the handle's last fit:
  *   [0] n  [1] finite points in the grid  [2] occupied cells  [3] core points

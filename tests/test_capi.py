@@ -70,6 +70,7 @@ def test_null_handle_errors():
     assert b"NULL handle" in L.dbscan_last_error()
     rc = L.dbscan_slab_label_finish_device_async(None, None, None, None, 0, None, None)
     assert rc == _lib.DBSCAN_EARG
+    assert L.dbscan_set_stream(None, None, 1) == _lib.DBSCAN_EARG
 
 
 @pytest.mark.skipif(_lib.load().dbscan_device_count() > 0, reason="GPU present")
