@@ -28,6 +28,7 @@ Naive noise rule and the cluster numbering -- unlike the reference's merge, SURV
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import List, Optional
 
@@ -278,6 +279,7 @@ class NodeJob:
         self.comm, self.ops = comm, ops
         self.cluster = self.flag = None
         self.n_clusters = 0
+        self._cs = None  # the roots' gather stream (N > 1, device tensors)
         # Static per job: the shared points (slab indices), the a-side of every rank's records
         # and the record counts, so each step exchanges only the b-side at known sizes.
         dev = x.device
@@ -344,9 +346,25 @@ class NodeJob:
         tick("roots")
         # cluster id = 1 + rank of s(K) among all ranks' global roots (each rank's list is
         # already in gid order)
-        all_roots = self.comm.allgather_varlen(own)
-        if self.comm.world > 1:  # one rank's list is already in gid order
-            all_roots, _ = torch.sort(all_roots)
+        if self.comm.world > 1:
+            # DBSCAN_NODE_COMM_STREAM=1: the gather and sort on a stream of their own, so the
+            # collectives need not wait for the label's first part still running on the current
+            # stream (own is complete: merge_roots waited for it).  Off by default: two gloo
+            # ranks sharing one GPU measured 6.0-6.2 ms per step with it, 4.5-4.7 without
+            # (tools/node2_ab.sh); the RCCL case is for a multi-GPU A/B.
+            if self._cs is None:
+                use = own.is_cuda and os.environ.get("DBSCAN_NODE_COMM_STREAM", "0") == "1"
+                self._cs = torch.cuda.Stream(device=own.device) if use else False
+            main = torch.cuda.current_stream(own.device) if own.is_cuda else None
+            if self._cs:
+                with torch.cuda.stream(self._cs):
+                    all_roots, _ = torch.sort(self.comm.allgather_varlen(own))
+                main.wait_stream(self._cs)
+                all_roots.record_stream(main)
+            else:
+                all_roots, _ = torch.sort(self.comm.allgather_varlen(own))
+        else:  # one rank's list is already in gid order
+            all_roots = own
         self.ops.merge_reset(self.all_a, all_b, self.parent)
         tick("numbering")
         self.cluster, self.flag = self.ops.label(self.zone, self.gid, self.gs_of_root, all_roots,
