@@ -285,7 +285,9 @@ dbscan_handle* dbscan_create(int32_t device) {
 void dbscan_destroy(dbscan_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    // The bound stream may be the null stream (dbscan_set_stream(h, NULL, 0), e.g. torch's
+    // default stream): synchronizing it is valid and waits for the handle's kernels there.
+    (void)hipStreamSynchronize(h->stream);
     if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
     h->prof.destroy();
     h->ws.release();

@@ -2644,51 +2644,38 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 // Host orchestration
 // ---------------------------------------------------------------------------------------
 
-// LDS staging capacity of the count pass (points of a tile + halo; tiles over it take the
-// global-memory path).  DBSCAN_COUNT_CAP = 2048 or 1024 overrides the 1536 default for
-// measurements; results are identical for every choice.
-// DBSCAN_COUNT_ABLATE (timing experiments only; results are wrong): 1 = staging only, no
-// neighbour scans; 2 = scans without neighbour lists.
-static int count_ablate() {
-    static const int v = [] {
-        const char* e = std::getenv("DBSCAN_COUNT_ABLATE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-// DBSCAN_UNION_W: register budget (waves/SIMD) of the tile/edge union kernels, 6 by default
-// (tile_union 88 -> 78 VGPRs, edge_union 100 -> 80): blobs 0.35 / 0.31 ms -> 0.31 / 0.23 ms;
-// 8 spills and is slower (tools/union_w_sweep.sh, r05).  5 and 7 for measurements.
-static int union_w() {
-    static const int v = [] {
-        const char* e = std::getenv("DBSCAN_UNION_W");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-static int count_cap() {
-    static const int v = [] {
-        const char* e = std::getenv("DBSCAN_COUNT_CAP");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-// DBSCAN_F32=0: count clique grids with the fp64 staging (A/B measurements)
-static bool f32_count() {
-    static const bool v = [] {
-        const char* e = std::getenv("DBSCAN_F32");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-// DBSCAN_FUSE=0: run quarter_init and tile_union as their own kernels (A/B measurements)
-static bool fuse_union() {
-    static const bool v = [] {
-        const char* e = std::getenv("DBSCAN_FUSE");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
+// A/B experiment options.  They are COMPILE-TIME only (-D on the hipcc line of an A/B build
+// loaded through DBSCAN_LIB_PATH, tools/build_ab.sh): no environment variable can change what
+// the shipped library computes.  The product build uses the defaults below.
+// DBSCAN_AB_COUNT_CAP: LDS staging capacity of the fp64 count pass (2048 or 1024 instead of
+//   1536; results identical for every choice).
+// DBSCAN_AB_COUNT_ABLATE (timing experiments only; results are WRONG): 1 = staging only, no
+//   neighbour scans; 2 = scans without neighbour lists; 4 = count32 returns at once.
+// DBSCAN_AB_UNION_W: register budget (waves/SIMD) of the tile/edge union kernels, 6 by default
+//   (tile_union 88 -> 78 VGPRs, edge_union 100 -> 80: blobs 0.35 / 0.31 -> 0.31 / 0.23 ms;
+//   8 spills and is slower, tools/union_w_sweep.sh, r05); 5 and 7 for measurements.
+// DBSCAN_AB_F32=0: count clique grids with the fp64 staging.
+// DBSCAN_AB_FUSE=0: run quarter_init and tile_union as their own kernels.
+#ifndef DBSCAN_AB_COUNT_ABLATE
+#define DBSCAN_AB_COUNT_ABLATE 0
+#endif
+#ifndef DBSCAN_AB_UNION_W
+#define DBSCAN_AB_UNION_W 0
+#endif
+#ifndef DBSCAN_AB_COUNT_CAP
+#define DBSCAN_AB_COUNT_CAP 0
+#endif
+#ifndef DBSCAN_AB_F32
+#define DBSCAN_AB_F32 1
+#endif
+#ifndef DBSCAN_AB_FUSE
+#define DBSCAN_AB_FUSE 1
+#endif
+static constexpr int count_ablate() { return DBSCAN_AB_COUNT_ABLATE; }
+static constexpr int union_w() { return DBSCAN_AB_UNION_W; }
+static constexpr int count_cap() { return DBSCAN_AB_COUNT_CAP; }
+static constexpr bool f32_count() { return DBSCAN_AB_F32 != 0; }
+static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
 
 // Enqueues one whole fit on stream s and never waits on the device: the grid, the finite count
 // nf and every table size live in device memory (ws.misc), so launch sizes derive from n alone

@@ -177,9 +177,24 @@ class HipSlabOps:
         else:
             self._hs = torch.cuda.ExternalStream(handle.stream,
                                                  device=torch.device("cuda", handle.device))
+        self._bound = share_stream
         self._out = None
         self._bufs = None
         self._lab = None  # (cluster, flag, zone) reused across the steps of one slab
+
+    def close(self):
+        """Give the handle its own stream back (share_stream=True bound it to torch's stream,
+        which the caller may destroy later).  Waits for the handle's work first."""
+        if self._bound and self.h.ptr:
+            self.h.sync()
+            _lib.check(_lib.load().dbscan_set_stream(self.h.ptr, None, 1))
+            self._bound = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _to_handle(self):
         cur = torch.cuda.current_stream()
@@ -357,6 +372,8 @@ class NodeJob:
                 self._cs = torch.cuda.Stream(device=own.device) if use else False
             main = torch.cuda.current_stream(own.device) if own.is_cuda else None
             if self._cs:
+                self._cs.wait_stream(main)  # own was produced on main
+                own.record_stream(self._cs)
                 with torch.cuda.stream(self._cs):
                     all_roots, _ = torch.sort(self.comm.allgather_varlen(own))
                 main.wait_stream(self._cs)

@@ -104,7 +104,8 @@ void* dbscan_stream(dbscan_handle* h);
 /* Run the handle's work on the caller's stream (a hipStream_t of the handle's device, as void*;
  * NULL is the device's null stream) from now on, so a caller whose own work is on that stream
  * needs no cross-stream waits; own != 0 returns to the handle's own stream (stream ignored).
- * Waits for the work already enqueued.  The handle never destroys a caller's stream. */
+ * Waits for the work already enqueued.  The handle never destroys a caller's stream: the caller
+ * must keep it alive while it is bound (until dbscan_set_stream(h, NULL, 1) or dbscan_destroy). */
 int32_t dbscan_set_stream(dbscan_handle* h, void* stream, int32_t own);
 
 /* Statistics of the handle's last fit:
