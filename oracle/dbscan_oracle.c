@@ -265,6 +265,10 @@ typedef struct {
     int64_t* cstart; /* start slot of each cell, cstart[ncells] = nfinite */
     int64_t ncells;
     int64_t* cell_of; /* cell index per point (or -1) */
+    double* sx;       /* coordinates in sorted-slot order (cache locality only) */
+    double* sy;
+    uint8_t* score;   /* core flag per sorted slot */
+    int64_t next;     /* dynamic cell counter of the running phase */
     uint8_t* core;
     int64_t* counts;
     int64_t* parent;
@@ -306,6 +310,54 @@ typedef struct {
     int64_t lo, hi;
     int phase;
 } job;
+
+/* Grid fits, cell-major: a worker takes chunks of cells (dynamic, for the dense cells of
+ * skewed data), computes each cell's stencil ranges once and runs the phase for every point of
+ * the cell over the sorted-slot coordinates.  Same predicate, same per-point results as the
+ * point-major loop below; only the iteration order (and so the cache behaviour) differs. */
+static void* grid_cell_worker(void* arg) {
+    job* jb = (job*)arg;
+    grid_ctx* g = jb->g;
+    const int phase = jb->phase;
+    const double* sx = g->sx;
+    const double* sy = g->sy;
+    for (;;) {
+        int64_t c0 = __atomic_fetch_add(&g->next, 64, __ATOMIC_RELAXED);
+        if (c0 >= g->ncells) break;
+        int64_t c1 = c0 + 64 < g->ncells ? c0 + 64 : g->ncells;
+        for (int64_t c = c0; c < c1; ++c) {
+            int64_t b[3], e[3];
+            int nr = stencil_ranges(g, c, b, e);
+            for (int64_t s = g->cstart[c]; s < g->cstart[c + 1]; ++s) {
+                const int64_t i = g->order[s];
+                const double px = sx[s], py = sy[s];
+                if (phase == 0) { /* neighbour counts */
+                    int64_t cnt = 0;
+                    for (int r = 0; r < nr; ++r)
+                        for (int64_t t = b[r]; t < e[r]; ++t) cnt += within(px, py, sx[t], sy[t], g->eps2);
+                    g->counts[i] = cnt;
+                    g->core[i] = g->score[s] = cnt >= (int64_t)g->min_points;
+                    continue;
+                }
+                if ((phase == 1) != (g->score[s] != 0)) continue;
+                int64_t best = -1;
+                for (int r = 0; r < nr; ++r)
+                    for (int64_t t = b[r]; t < e[r]; ++t) {
+                        if (t == s || !g->score[t] || !within(px, py, sx[t], sy[t], g->eps2)) continue;
+                        const int64_t j = g->order[t];
+                        if (phase == 1) {
+                            if (j < i) uf_union(g->parent, i, j);
+                        } else {
+                            int64_t sk = uf_find(g->parent, j);
+                            if (best < 0 || sk < best) best = sk;
+                        }
+                    }
+                if (phase == 2) g->bmin[i] = best;
+            }
+        }
+    }
+    return NULL;
+}
 
 static void* grid_worker(void* arg) {
     job* jb = (job*)arg;
@@ -375,11 +427,22 @@ static void run_phase(grid_ctx* g, int phase, int nthreads) {
         jobs[t].hi = (t + 1) * chunk < g->n ? (t + 1) * chunk : g->n;
         jobs[t].phase = phase;
     }
+    /* grid fits: cell-major over the occupied cells (non-finite points keep count 0) */
+    void* (*fn)(void*) = (g->ncells > 0 && !g->all_pairs) ? grid_cell_worker : grid_worker;
+    g->next = 0;
+    if (fn == grid_cell_worker && phase == 0) /* points outside the grid: count 0 */
+        for (int64_t i = 0; i < g->n; ++i)
+            if (g->cell_of[i] < 0) {
+                g->counts[i] = 0;
+                g->core[i] = 0 >= (int64_t)g->min_points;
+            }
+    if (fn == grid_cell_worker && phase != 0) /* callers may edit core[] between phases */
+        for (int64_t t = 0; t < g->nfinite; ++t) g->score[t] = g->core[g->order[t]];
     if (nthreads == 1) {
-        grid_worker(&jobs[0]);
+        fn(&jobs[0]);
         return;
     }
-    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, grid_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, fn, &jobs[t]);
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
 
@@ -485,6 +548,13 @@ static void grid_build(grid_ctx* gp, const double* x, const double* y, int64_t n
             }
             g.cstart[nc] = nf;
             g.ncells = nc;
+            g.sx = (double*)malloc(sizeof(double) * (size_t)nf);
+            g.sy = (double*)malloc(sizeof(double) * (size_t)nf);
+            g.score = (uint8_t*)calloc((size_t)nf, 1);
+            for (int64_t t = 0; t < nf; ++t) {
+                g.sx[t] = x[g.order[t]];
+                g.sy[t] = y[g.order[t]];
+            }
         }
     }
     *gp = g;
@@ -500,6 +570,9 @@ static void grid_free(grid_ctx* g) {
     free(g->okey);
     free(g->ckey);
     free(g->cstart);
+    free(g->sx);
+    free(g->sy);
+    free(g->score);
 }
 
 int32_t oracle_fit_grid(const double* x, const double* y, int64_t n, double eps,

@@ -86,6 +86,16 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
+def default_threads() -> int:
+    """Host threads for the pthreads formulations: the cores this process may run on, at most
+    16 (the GPU box's CPU share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def fit_sequential(x, y, eps, min_points, mode=NAIVE):
     """Literal BFS restatement. Returns (cluster int32[n], flag uint8[n], n_clusters)."""
     x, y = _xy(x, y)
@@ -114,7 +124,7 @@ def fit_grid(x, y, eps, min_points, mode=NAIVE, nthreads=None, with_counts=False
     cl = np.zeros(n, np.int32)
     fl = np.zeros(n, np.uint8)
     cnt = np.zeros(n, np.int64) if with_counts else None
-    nt = nthreads or min(8, os.cpu_count() or 1)
+    nt = nthreads or default_threads()
     k = lib().oracle_fit_grid(_ptr(x), _ptr(y), n, float(eps), int(min_points), int(mode), nt,
                               _ptr(cl), _ptr(fl), _ptr(cnt))
     return (cl, fl, int(k), cnt) if with_counts else (cl, fl, int(k))
@@ -179,7 +189,7 @@ def ref_train(x, y, eps, min_points, max_points_per_partition, nthreads=None):
     npart = np.zeros(1, np.int64)
     mp = 4096
     rects = np.zeros((mp, 4), np.float64)
-    nt = nthreads or min(8, os.cpu_count() or 1)
+    nt = nthreads or default_threads()
     k = lib().ref_train(_ptr(x), _ptr(y), n, float(eps), int(min_points),
                         int(max_points_per_partition), nt, _ptr(cl), _ptr(fl), _ptr(oc),
                         _ptr(npart), _ptr(rects), mp)
@@ -197,7 +207,7 @@ def slab_fit(x, y, zone, eps, min_points, nthreads=None):
     n = x.size
     core = np.zeros(n, np.uint8)
     root = np.zeros(n, np.int32)
-    nt = nthreads or min(8, os.cpu_count() or 1)
+    nt = nthreads or default_threads()
     lib().oracle_slab_fit(_ptr(x), _ptr(y), _ptr(zone), n, float(eps), int(min_points), nt,
                           _ptr(core), _ptr(root))
     return core, root

@@ -586,15 +586,113 @@ int64_t ref_train(const double* x, const double* y, int64_t n, double eps, int32
     int64_t* rec_node = (int64_t*)malloc(sizeof(int64_t) * (size_t)rec_cap);
     uint8_t* rec_flag = (uint8_t*)malloc((size_t)rec_cap);
 
-    for (int64_t g = 0; g < np; ++g) { /* each merge group (newPartition), in id order */
-        double inner_g[4], *main_g = &rects[4 * g];
-        shrink(main_g, eps, inner_g);
+    /* The reference tests every margin for every clustered point (a Spark flatMap over the
+     * margins list, O(points x partitions)).  Same decisions here, indexed: the mains are
+     * bucketed on the 2*eps cell grid (corner_index is monotone, so a main containing a point
+     * is listed in that point's cell), each point tests only its cell's mains with the exact
+     * predicates, and the (group, partition, point) records are put back in the reference's
+     * iteration order -- groups in id order, partitions in id order, points in partition
+     * order -- by a stable counting sort on the group. */
+    int64_t nmrec = 0;
+    int64_t* mr_g = NULL;
+    int64_t* mr_p = NULL;
+    int64_t* mr_k = NULL;
+    {
+        const double mrs = 2 * eps;
+        int64_t imin = INT64_MAX, imax = INT64_MIN, jmin = INT64_MAX, jmax = INT64_MIN;
         for (int64_t p = 0; p < np; ++p)
             for (int64_t k = 0; k < f.msize[p]; ++k) {
                 int64_t i = f.members[p][k];
-                if (!(rect_contains_pt(main_g, x[i], y[i]) &&
-                      !rect_almost_contains_pt(inner_g, x[i], y[i])))
-                    continue;
+                int64_t ci = corner_index(x[i], mrs), cj = corner_index(y[i], mrs);
+                if (ci < imin) imin = ci;
+                if (ci > imax) imax = ci;
+                if (cj < jmin) jmin = cj;
+                if (cj > jmax) jmax = cj;
+            }
+        int64_t W = imin <= imax ? imax - imin + 1 : 1, H = jmin <= jmax ? jmax - jmin + 1 : 1;
+        if (imin > imax) imin = imax = jmin = jmax = 0;
+        int64_t* bstart = (int64_t*)calloc((size_t)(W * H + 1), sizeof(int64_t));
+        for (int pass = 0; pass < 2; ++pass) { /* count, then fill */
+            int64_t* bl = pass ? (int64_t*)malloc(sizeof(int64_t) * (size_t)(bstart[W * H] + 1)) : NULL;
+            int64_t* cur = NULL;
+            if (pass) {
+                cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(W * H));
+                memcpy(cur, bstart, sizeof(int64_t) * (size_t)(W * H));
+            }
+            for (int64_t g = 0; g < np; ++g) {
+                const double* mg = &rects[4 * g];
+                int64_t i0 = corner_index(mg[0], mrs) - 1, i1 = corner_index(mg[2], mrs) + 1;
+                int64_t j0 = corner_index(mg[1], mrs) - 1, j1 = corner_index(mg[3], mrs) + 1;
+                if (i0 < imin) i0 = imin;
+                if (j0 < jmin) j0 = jmin;
+                if (i1 > imax) i1 = imax;
+                if (j1 > jmax) j1 = jmax;
+                for (int64_t j = j0; j <= j1; ++j)
+                    for (int64_t i = i0; i <= i1; ++i) {
+                        int64_t c = (j - jmin) * W + (i - imin);
+                        if (pass) bl[cur[c]++] = g;
+                        else bstart[c + 1]++;
+                    }
+            }
+            if (!pass) {
+                for (int64_t c = 0; c < W * H; ++c) bstart[c + 1] += bstart[c];
+                continue;
+            }
+            free(cur);
+            /* records, partition-major; gcount for the stable sort by group */
+            int64_t* gcount = (int64_t*)calloc((size_t)(np + 1), sizeof(int64_t));
+            int64_t cap2 = 1024, m2 = 0;
+            int64_t* tg = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap2);
+            int64_t* tp = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap2);
+            int64_t* tk = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap2);
+            for (int64_t p = 0; p < np; ++p)
+                for (int64_t k = 0; k < f.msize[p]; ++k) {
+                    int64_t i = f.members[p][k];
+                    int64_t c = (corner_index(y[i], mrs) - jmin) * W + (corner_index(x[i], mrs) - imin);
+                    for (int64_t t = bstart[c]; t < bstart[c + 1]; ++t) {
+                        int64_t g = bl[t];
+                        double inner_g[4];
+                        shrink(&rects[4 * g], eps, inner_g);
+                        if (!(rect_contains_pt(&rects[4 * g], x[i], y[i]) &&
+                              !rect_almost_contains_pt(inner_g, x[i], y[i])))
+                            continue;
+                        if (m2 == cap2) {
+                            cap2 *= 2;
+                            tg = (int64_t*)realloc(tg, sizeof(int64_t) * (size_t)cap2);
+                            tp = (int64_t*)realloc(tp, sizeof(int64_t) * (size_t)cap2);
+                            tk = (int64_t*)realloc(tk, sizeof(int64_t) * (size_t)cap2);
+                        }
+                        tg[m2] = g;
+                        tp[m2] = p;
+                        tk[m2] = k;
+                        ++m2;
+                        gcount[g + 1]++;
+                    }
+                }
+            for (int64_t g = 0; g < np; ++g) gcount[g + 1] += gcount[g];
+            mr_g = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m2 + 1));
+            mr_p = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m2 + 1));
+            mr_k = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m2 + 1));
+            for (int64_t r = 0; r < m2; ++r) {
+                int64_t o = gcount[tg[r]]++;
+                mr_g[o] = tg[r];
+                mr_p[o] = tp[r];
+                mr_k[o] = tk[r];
+            }
+            nmrec = m2;
+            free(tg);
+            free(tp);
+            free(tk);
+            free(gcount);
+            free(bl);
+        }
+        free(bstart);
+    }
+    for (int64_t r = 0; r < nmrec; ++r) { /* each merge group (newPartition), in id order */
+        const int64_t g = mr_g[r], p = mr_p[r], k = mr_k[r];
+        {
+            {
+                int64_t i = f.members[p][k];
                 uint8_t fl = f.fl[p][k];
                 int64_t node = fl != 2 ? base[p] + f.cl[p][k] - 1 : -1;
                 if (fl != 2) { /* findAdjacencies */
@@ -627,7 +725,11 @@ int64_t ref_train(const double* x, const double* y, int64_t n, double eps, int32
                     out_flag[i] = fl;
                 }
             }
+        }
     }
+    free(mr_g);
+    free(mr_p);
+    free(mr_k);
     for (int64_t i = 0; i < n; ++i) { /* flush the last group records */
         if (out_grp[i] < 0) continue;
         if (nrec == rec_cap) {

@@ -1,0 +1,119 @@
+"""BASELINE.json configs at their full sizes, checked bit-exactly against the CPU oracle.
+
+The inputs are the device generator's (dbscan_generate_blobs_device, SURVEY §8d G(n, noise,
+dense, seed)): the same bits bench.py times, copied to the host for the oracle
+(oracle_fit_grid, the closed form of LocalDBSCANNaive.scala:37-118 on an eps grid, pthreads on
+the host cores).  Cluster numbers are compared exactly (Naive, visit order = input order), so
+core flags, border/noise flags and the cluster-opening order all match the reference's
+sequential fit.
+
+  config 2  G(10^7, 0, -, 1), one fit                             (bench.py default)
+  config 3  G(10^8, 0.2, -, 2), 8 x-slabs through dbscan_train_node (the whole-node entry;
+            bench.py --gpus 8 times the same data set, one slab per GPU) + one per-GPU share
+            G(1.25*10^7, 0.2, -, 2) as a single fit
+  config 4  G(5*10^7, 0, dense=8, 3), one fit: one giant component per dense blob
+  config 5  the per-GPU share at the same density, G(1.25*10^8, 0.2, -, 4), one fit (the
+            10^9-point 8-GPU job itself is not checked against the oracle here)
+
+Size-independent properties ride along: core flags are invariant under a permutation of the
+visit order, and a second fit of the same data is identical (idempotence)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EPS, MINPTS = 2.55, 10
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dbscan_amd
+
+    if dbscan_amd.load().dbscan_device_count() < 1:
+        pytest.fail("no GPU visible to libdbscan_hip.so")
+    return dbscan_amd
+
+
+@pytest.fixture(scope="module")
+def handle(dm):
+    h = dm.Handle(0)
+    yield h
+    h.close()
+
+
+def _device_data(handle, n, noise, dense, seed):
+    from dbscan_amd import device as D
+
+    return D.generate_blobs(n, noise, dense, seed, handle)
+
+
+def _fit_device(handle, tx, ty, mode=0):
+    import torch
+
+    from dbscan_amd import device as D
+
+    cl, fl, k = D.fit_tensors(tx, ty, EPS, MINPTS, mode, handle)
+    torch.cuda.synchronize()
+    return cl.cpu().numpy(), fl.cpu().numpy(), k
+
+
+def _assert_equal(cl, fl, k, ref):
+    rc, rf, rk = ref
+    assert k == rk
+    bad = np.flatnonzero((cl != rc) | (fl != rf))
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:10]}"
+
+
+def _single_fit_vs_oracle(handle, n, noise, dense, seed, permute=False):
+    import torch
+
+    tx, ty = _device_data(handle, n, noise, dense, seed)
+    cl, fl, k = _fit_device(handle, tx, ty)
+    hx, hy = tx.cpu().numpy(), ty.cpu().numpy()
+    ref = O.fit_grid(hx, hy, EPS, MINPTS, 0)
+    _assert_equal(cl, fl, k, ref)
+    cl2, fl2, k2 = _fit_device(handle, tx, ty)  # idempotent
+    assert k2 == k and np.array_equal(cl2, cl) and np.array_equal(fl2, fl)
+    if permute:  # core flags do not depend on the visit order
+        p = torch.randperm(n, generator=torch.Generator().manual_seed(seed)).cuda()
+        _, flp, _ = _fit_device(handle, tx[p].contiguous(), ty[p].contiguous())
+        np.testing.assert_array_equal(flp == 1, (fl == 1)[p.cpu().numpy()])
+    return k, fl
+
+
+def test_config2_bench_data(handle):
+    """The bench's own input: device-generated G(10^7, no noise, seed 1)."""
+    k, fl = _single_fit_vs_oracle(handle, 10_000_000, 0.0, 1.0, 1)
+    assert k > 1000 and 0.8 < float((fl == 1).mean()) < 0.95
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_size(handle):
+    """G(5*10^7, dense = 8, seed 3): the skewed set (k_bar ~ 339 in the dense blobs), one fit."""
+    _single_fit_vs_oracle(handle, 50_000_000, 0.0, 8.0, 3, permute=True)
+
+
+@pytest.mark.timeout(600)
+def test_config3_share(handle):
+    """One GPU's share of config 3 at the same density: G(1.25*10^7, 20% noise, seed 2)."""
+    _single_fit_vs_oracle(handle, 12_500_000, 0.2, 1.0, 2, permute=True)
+
+
+@pytest.mark.timeout(900)
+def test_config3_full_size_train_node(dm, handle):
+    """G(10^8, 20% uniform noise, seed 2) through dbscan_train_node with 8 x-slabs (eps halos,
+    exact merge) on the one test GPU: global labels equal the oracle's single fit."""
+    tx, ty = _device_data(handle, 100_000_000, 0.2, 1.0, 2)
+    hx, hy = tx.cpu().numpy(), ty.cpu().numpy()
+    del tx, ty
+    cl, fl, k = dm.train_node(hx, hy, EPS, MINPTS, 0, 8)
+    ref = O.fit_grid(hx, hy, EPS, MINPTS, 0)
+    _assert_equal(cl, fl, k, ref)
+
+
+@pytest.mark.timeout(900)
+def test_config5_share(handle):
+    """One GPU's share of config 5 at the same density: G(1.25*10^8, 20% noise, seed 4)."""
+    _single_fit_vs_oracle(handle, 125_000_000, 0.2, 1.0, 4)
