@@ -4,23 +4,34 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]): G(n = 10^7 x N, 32 Gaussian blobs, no noise,
-seed 1), eps = 2.55 (k_bar ~ 49), minPoints = 10, LocalDBSCANNaive semantics, visit order =
-generation order (i.i.d. draws).  A step = one full local fit of the resident points (HBM in ->
-labels in HBM).  N = 1: one dbscan_fit_device_async per step (the fit never synchronizes with
-the host; the K steps are enqueued back to back and the timed region ends with one sync).  N > 1: the slab-sharded node path
-(dbscan_amd/node.py): per-GPU slab fits with 2*eps halos + RCCL all-gathers of the boundary
-records + global union-find + relabel; per-GPU work is fixed (weak scaling).
+Workloads (BASELINE.json configs, SURVEY.md §8d generator G(n, noise, dense, seed), eps = 2.55
+(k_bar ~ 49), minPoints = 10, LocalDBSCANNaive semantics, visit order = generation order):
+  N = 1  config 2: G(10^7, no noise, seed 1), one local fit per step
+         (dbscan_fit_device_async; the K steps are enqueued back to back, one sync at the end).
+  N > 1  config 3 weak-scaled: G(1.25*10^7 x N, 20% uniform noise, seed 2) -- exactly config 3
+         (10^8 points) at N = 8 -- through the slab-sharded node path (dbscan_amd/node.py): per-
+         GPU slab fits with eps halos + RCCL all-gathers of the boundary records + global
+         union-find + relabel; per-GPU work fixed (weak scaling).
+A step is one pass of the hot path over the resident points (HBM in -> labels in HBM): `value`.
+`end_to_end` times host SoA -> host labels on the same data (PCIe included; N = 1:
+dbscan_fit_h, N > 1: H2D of the global arrays, slab selection, the node step, D2H of the
+owned labels); it is reported beside `value`, never as it.
 
 roofline: the dominant kernel of the timed region, timed with HIP events on the library's own
-stream -- carried on the kernels' own dispatch packets (hipExtLaunchKernelGGL), so timing adds
-no idle gaps between kernels; achieved = algorithmic bytes per launch (SURVEY §8d per-point
-figure x points) / the kernel's average launch duration.
-cpu_baseline (rank 0, N = 1): the oracle's restatement of the reference path -- the
-EvenSplitPartitioner (maxPointsPerPartition = 8192) + LocalDBSCANNaive.fit O(m^2) per partition
-(oracle/reference_pipeline.c), on host threads, for a bounded time on the same points.
+stream, carried on the kernels' own dispatch packets (hipExtLaunchKernelGGL: no idle gaps);
+achieved = algorithmic bytes per launch (SURVEY §8d per-point figure x points) / the kernel's
+average launch duration.  `traffic` (HBM bytes per launch from rocprofv3 PMC) and `valu`
+(fp32/fp64 lane-ops from SQ counters) come from profiles/pmc_traffic.json, used only when its
+entry was measured on this workload size AND from the same kernel sources (src_sha).
+cpu_baseline (rank 0, N = 1): the reference's whole DBSCAN.train path restated in C
+(oracle/reference_pipeline.c: EvenSplitPartitioner with maxPointsPerPartition = 8192, eps
+halos, LocalDBSCANNaive.fit O(m^2) per partition on a thread pool, the margin merge and
+relabel) on the same points, on the host cores this process may use; plus the strong CPU
+comparator (the closed form on an eps grid, oracle_fit_grid) on the same threads.
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -31,13 +42,16 @@ sys.path.insert(0, os.path.join(ROOT, "dbscan-on-spark_amd"))
 
 METRIC = "points clustered/sec (whole node) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU peaks in lane-operations per second (one lane of one VALU instruction; an FMA is ONE
+# lane-op here): fp64 vector 78.6 TFLOP/s counting FMA as 2 -> 39.3e12; fp32 157.3 -> 78.6e12.
+VALU_PEAK = {"f64": 39.3e12, "f32": 78.65e12}
 # Algorithmic bytes per point and launch, by kernel (SURVEY.md §8d's per-phase figures; each
 # array crosses HBM once).  count = 21: the count kernel also builds the quarter
 # records and the tile-local quarter union (fused), so it carries §8d's count (sorted x,y 16 +
 # core 1) and union (parent 4; the union's x,y read is the count's, already in LDS).
 # edge_union and quarter_root touch tile-edge strips and quarter reps only.  The §8d output 30
-# is carried by final (13), the rank scan and label_sorted/permute_out.  Radix passes: 4
-# launches per fit, each reading key+perm 8 and writing 8.
+# is carried by final (13), the rank scan and label_sorted/permute_out.  Radix passes: each
+# reads key+perm 8 and writes 8.
 ALG_BYTES = {
     "bbox_partial": 16, "bin": 20, "radix_upsweep": 4, "radix_downsweep": 16, "inverse": 8,
     "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 21, "count_wave": 21,
@@ -49,20 +63,49 @@ ALG_BYTES = {
 CLASS_PTS = {"count_wave": "pts_small", "count32": "pts_medium", "big_count": "pts_big"}
 PIPELINE_ALG_BYTES = 132  # whole pipeline, B_alg per point
 
+
+def src_stamp() -> str:
+    """Content hash of the sources libdbscan_hip.so is built from (the GPU box has no .git):
+    PMC entries are used only when they were measured on these exact sources."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "dbscan-on-spark_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + [os.path.join(csrc, "internal.h"),
+                   os.path.join(csrc, "Makefile"), os.path.join(ROOT, "include", "dbscan_hip.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def host_threads() -> int:
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS when set
+    (the GPU box exports its per-GPU CPU share there; its affinity shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--points-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--points-per-gpu", type=int, default=None,
+                    help="default: 10^7 at N = 1 (config 2), 1.25*10^7 at N > 1 (config 3)")
     ap.add_argument("--eps", type=float, default=2.55)
     ap.add_argument("--min-points", type=int, default=10)
-    ap.add_argument("--noise", type=float, default=0.0)
+    ap.add_argument("--noise", type=float, default=None, help="default 0 (N = 1), 0.2 (N > 1)")
     ap.add_argument("--dense", type=float, default=1.0)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline work")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=None, help="default 1 (N = 1), 2 (N > 1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: host_threads()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=3, help="end-to-end steps (0: skip)")
     ap.add_argument("--no-profile", action="store_true", help="no kernel timing events")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (the breakdown)")
@@ -71,43 +114,64 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic(kernel, n_points):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (tools/profile.sh + tools/pmc_summary.py), only if it was measured on this workload size."""
+def load_pmc(stage, n_points, stamp):
+    """The committed rocprofv3 summary for `stage` (tools/pmc_summary.py), or (None, reason)
+    unless it was measured on this workload size and these kernel sources."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(kernel, {})
-        if e.get("n_points", 10_000_000) != n_points:
-            return None
-        return e.get("bytes_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/pmc_traffic.json"
+    e = d.get("stages", {}).get(stage)
+    if e is None:
+        return None, f"{stage} not profiled"
+    if d.get("src_sha") != stamp:
+        return None, f"stale: profiled on sources {d.get('src_sha')}, running {stamp}"
+    if d.get("n_points") != n_points:
+        return None, f"profiled at n = {d.get('n_points')}, running n = {n_points}"
+    return e, d.get("source")
 
 
-def cpu_baseline(x, y, eps, min_points, budget, threads):
+def cpu_baseline(x, y, eps, min_points, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
     import oracle as O  # CPU baseline leg only
 
-    rects, counts = O.ref_partition(x, y, eps, 8192)
-    r = O.ref_fit_partitions_timed(x, y, eps, min_points, rects, counts, threads, budget)
+    t0 = time.perf_counter()
+    r = O.ref_train(x, y, eps, min_points, 8192, threads)
+    t_ref = time.perf_counter() - t0
+    lost = int((r["records"] == 0).sum())
+    t0 = time.perf_counter()
+    g = O.fit_grid(x, y, eps, min_points, 0, threads)
+    t_grid = time.perf_counter() - t0
+    # the GPU result on the same points equals the grid closed form (tests/test_gpu_configs.py)
     return {
-        "value": r["main_points"] / r["seconds"] if r["seconds"] > 0 else None,
+        "value": x.size / t_ref,
         "unit": "points/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"reference path restated in C (oracle/reference_pipeline.c): "
-                   f"EvenSplitPartitioner(maxPointsPerPartition=8192) over the same {x.size} "
-                   f"points -> {len(counts)} partitions; LocalDBSCANNaive.fit O(m^2) on the first "
-                   f"{r['parts']} partitions ({r['main_points']} main / {r['outer_points']} "
-                   f"points incl. eps halos) in {r['seconds']:.2f} s on {threads} threads; "
-                   f"merge not timed"),
+        "seconds": round(t_ref, 3),
+        "sample": (f"the reference's whole DBSCAN.train path restated in C "
+                   f"(oracle/reference_pipeline.c) over the same {x.size} points: "
+                   f"EvenSplitPartitioner(maxPointsPerPartition=8192) -> {len(r['rects'])} "
+                   f"partitions, eps halos, LocalDBSCANNaive.fit O(m^2) per partition on "
+                   f"{threads} threads, margin merge + relabel, in {t_ref:.2f} s; value = input "
+                   f"points / s (the restated partitioner's split-line defect, SURVEY §8f-2, "
+                   f"drops {lost} points; the reference's own O(#cells) partitioner scan and "
+                   f"O(points x partitions) margin scan are replaced by indexed forms with the "
+                   f"same decisions)"),
+        "strong_comparator": {
+            "value": x.size / t_grid, "unit": "points/s", "cores": threads,
+            "seconds": round(t_grid, 3), "n_clusters": g[2],
+            "what": "closed form on an eps grid (oracle_fit_grid, pthreads), same points"},
     }
 
 
 def main():
     args = parse()
+    import numpy as np
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,6 +179,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    node_path = world > 1 or args.node
+    if args.points_per_gpu is None:
+        args.points_per_gpu = 12_500_000 if world > 1 else 10_000_000
+    if args.noise is None:
+        args.noise = 0.2 if world > 1 else 0.0
+    if args.seed is None:
+        args.seed = 2 if world > 1 else 1
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     import dbscan_amd
@@ -131,7 +202,7 @@ def main():
             dist.init_process_group(args.backend)
 
     n_total = args.points_per_gpu * world
-    if world == 1 and not args.node:
+    if not node_path:
         x, y = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
         cl = torch.empty(n_total, dtype=torch.int32, device="cuda")
         fl = torch.empty(n_total, dtype=torch.uint8, device="cuda")
@@ -182,11 +253,16 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64,
+
+    def max_over_ranks(v):
+        if not dist:
+            return v
+        t = torch.tensor([v], dtype=torch.float64,
                          device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        return float(t.item())
+
+    el = max_over_ranks(el)
     if isinstance(k, torch.Tensor):
         k = int(k.item())
     prof = h.profile_read() if not args.no_profile else {}
@@ -195,42 +271,78 @@ def main():
 
     ms_per_step = el / args.steps * 1e3
     value = n_total * args.steps / el
-    roof = None
+    roof, valu = None, None
     if prof and dom in prof:
         avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])  # live, in the timed region
         pts = stats.get("n", args.points_per_gpu)
         unit_pts = stats.get(CLASS_PTS[dom], pts) if dom in CLASS_PTS else pts
         alg = ALG_BYTES.get(dom, 0) * unit_pts  # per launch
         achieved = alg / (avg_ms * 1e-3) / 1e9
-        traffic = load_traffic(dom, pts) if (world == 1 and not args.node) else None
+        pmc, pmc_src = load_pmc(dom, pts, src_stamp()) if not node_path else (None, "node path")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                "traffic_source": pmc_src,
                 "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
                 "alg_bytes_per_point": ALG_BYTES.get(dom, 0), "points_per_launch": unit_pts,
                 "pipeline_frac": round(PIPELINE_ALG_BYTES * pts / (ms_per_step * 1e-3) / 1e9
                                        / HBM_PEAK_GBS, 5)}
+        if pmc and pmc.get("valu_insts_per_launch"):
+            vi = pmc["valu_insts_per_launch"]  # wave-instructions by type, per launch
+            lanes = {t: 64.0 * sum(v for kk, v in vi.items() if kk.endswith(t.upper()))
+                     for t in ("f32", "f64")}
+            rate = {t: lanes[t] / (avg_ms * 1e-3) for t in lanes}
+            frac = sum(rate[t] / VALU_PEAK[t] for t in rate)
+            valu = {"bound": "valu", "kernel": dom, "unit": "T lane-ops/s",
+                    "achieved": {t: round(rate[t] / 1e12, 3) for t in rate},
+                    "peak": {t: VALU_PEAK[t] / 1e12 for t in VALU_PEAK},
+                    "frac": round(frac, 5),
+                    "lane_ops_per_launch": {t: lanes[t] for t in lanes},
+                    "note": ("lane-ops = 64 x VALU wave-instructions (SQ_INSTS_VALU_{ADD,MUL,FMA,"
+                             "TRANS}_F32/F64, full exec mask assumed: an upper bound) over the "
+                             "live average launch time; frac = f32/peak_f32 + f64/peak_f64 "
+                             "(both share the VALU)"),
+                    "sq": pmc.get("sq"), "source": pmc_src}
+
+    e2e = None
+    if args.e2e_steps > 0:
+        e2e = end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks,
+                         x if not node_path else None, y if not node_path else None)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.node:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not node_path:
         sx, sy = x.cpu().numpy(), y.cpu().numpy()
-        cpu = cpu_baseline(sx, sy, args.eps, args.min_points, args.cpu_budget, args.cpu_threads)
+        threads = args.cpu_threads or host_threads()
+        cpu = cpu_baseline(sx, sy, args.eps, args.min_points, threads)
 
     if rank == 0:
+        if world > 1 or node_path:
+            workload = (f"config 3 weak-scaled: G({n_total} points = {args.points_per_gpu} per "
+                        f"GPU x {world}, 32 Gaussian blobs, noise={args.noise}, dense="
+                        f"{args.dense}, seed={args.seed}) -- BASELINE config 3 (10^8 points, "
+                        f"20% noise, 8 GPUs) exactly at N = 8")
+        else:
+            workload = (f"config 2: G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
+                        f"dense={args.dense}, seed={args.seed})")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "points/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (device generator G(n, noise, dense, seed), SURVEY §8d)",
             "config": {
-                "workload": (f"G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
-                             f"dense={args.dense}, seed={args.seed}), eps={args.eps}, "
-                             f"minPoints={args.min_points}, LocalDBSCANNaive semantics"),
+                "workload": workload + f", eps={args.eps}, minPoints={args.min_points}, "
+                                       "LocalDBSCANNaive semantics",
                 "n_points": n_total, "eps": args.eps, "min_points": args.min_points,
-                "parallelism": ("single GPU" if world == 1 and not args.node else
-                                f"slab x{world} + {'RCCL' if args.backend == 'nccl' else args.backend} merge"),
+                "parallelism": ("single GPU, one local fit" if not node_path else
+                                f"x-slabs x{world} with eps halos" +
+                                (f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
+                                 "all-gathers + global union-find" if world > 1 else
+                                 " (one slab: no exchange)")),
                 "clusters": k, "core_points": stats.get("core"),
                 "occupied_cells": stats.get("cells"), "occupied_tiles": stats.get("tiles")},
             "roofline": roof,
+            "valu": valu,
+            "end_to_end": e2e,
             "cpu_baseline": cpu,
             "kernels_ms_per_step": {k2: round(v, 4) for k2, v in
                                     sorted(kernels.items(), key=lambda kv: -kv[1])},
@@ -241,6 +353,73 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x, y):
+    """Host SoA -> host labels on the same data (PCIe included), median over e2e_steps after one
+    untimed step.  N = 1: dbscan_fit_h from pageable numpy arrays (the JNI case: Java arrays are
+    pageable) and from pinned host memory.  Node path: each rank copies the global arrays to its
+    GPU, selects its slab (zones), runs the node step and copies its owned labels back."""
+    import numpy as np
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import device as D
+
+    out = {"steps": args.e2e_steps}
+    if not node_path:
+        hx, hy = x.cpu().numpy(), y.cpu().numpy()
+        px = torch.empty(n_total, dtype=torch.float64, pin_memory=True)
+        py = torch.empty(n_total, dtype=torch.float64, pin_memory=True)
+        px.numpy()[:] = hx
+        py.numpy()[:] = hy
+        for tag, ax, ay in (("pageable", hx, hy), ("pinned", px.numpy(), py.numpy())):
+            ts = []
+            for i in range(args.e2e_steps + 1):
+                t0 = time.perf_counter()
+                dbscan_amd.fit_arrays(ax, ay, args.eps, args.min_points, 0, handle=h)
+                if i:
+                    ts.append(time.perf_counter() - t0)
+            t = float(np.median(ts))
+            out[tag] = {"value": round(n_total / t, 1), "ms_per_step": round(t * 1e3, 3)}
+        out["value"] = out["pageable"]["value"]
+        out["path"] = ("dbscan_fit_h: host x,y (16 B/point) -> H2D -> fit -> D2H cluster,flag "
+                       "(5 B/point), synchronous; value = the pageable-memory rate")
+        return out
+    from dbscan_amd import node
+
+    xa, ya = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
+    hx, hy = xa.cpu().numpy(), ya.cpu().numpy()
+    del xa, ya
+    torch.cuda.empty_cache()
+    comm = node.Comm(dist)
+    ops = node.HipSlabOps(h)
+    ts = []
+    for i in range(args.e2e_steps + 1):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tx = torch.from_numpy(hx).cuda()
+        ty = torch.from_numpy(hy).cuda()
+        job = node.NodeJob.from_global(tx, ty, args.eps, args.min_points, 0, comm, ops)
+        del tx, ty
+        job.run()
+        gid, cl, fl = job.owned()
+        gid, cl, fl = gid.cpu(), cl.cpu(), fl.cpu()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = max_over_ranks(time.perf_counter() - t0)
+        if i:
+            ts.append(el)
+        del job
+    ops.close()
+    t = float(np.median(ts))
+    out.update({"value": round(n_total / t, 1), "ms_per_step": round(t * 1e3, 3),
+                "path": ("each rank: H2D of the global host arrays (pageable), slab selection "
+                         "on its GPU, the node step, D2H of its owned labels; max over ranks")})
+    return out
 
 
 if __name__ == "__main__":

@@ -1,16 +1,23 @@
 """Summarize a tools/profile.sh run into profiles/ (committed evidence).
 
-    python tools/pmc_summary.py gpurun_out/prof r01
+    python tools/pmc_summary.py gpurun_out/prof rNN
 
 Writes
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
-  profiles/<tag>_pmc.csv            per-kernel average FETCH_SIZE / WRITE_SIZE per dispatch
-  profiles/pmc_traffic.json         HBM bytes per launch for the bench's stages, read by bench.py
+  profiles/<tag>_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_pmc.csv           per kernel template instance: dispatches, average duration,
+                                   FETCH_SIZE / WRITE_SIZE / SQ counters per dispatch, HBM bytes
+  profiles/pmc_traffic.json        per bench stage (bench.py's kernel names): HBM bytes, VALU
+                                   wave-instructions and SQ counters per launch, stamped with the
+                                   kernel sources' hash (bench.src_stamp()) and the workload size;
+                                   bench.py uses an entry only when both match.
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: rocprofv3 reports KB, and on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM); other
 access widths are uncalibrated there, so the figure is an estimate for gather-heavy kernels.
+A stage with several template instances (the radix passes) gets the launch-weighted average
+per launch, which is what bench.py's per-launch timing averages too.
 """
 import csv
+import glob
 import json
 import os
 import shutil
@@ -18,34 +25,35 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-def stage_of(kernel):
-    """bench.py's per-kernel name (the klaunch names in csrc/fit.hip): the kernel's base name
-    without `_kernel`; count_tile_kernel is "count"."""
-    if kernel == "count_tile_kernel":
-        return "count"
-    if kernel == "count_tile32_kernel":
-        return "count32"
-    return kernel[:-len("_kernel")] if kernel.endswith("_kernel") else None
+STAGE_OF = {"count_tile_kernel": "count", "count_tile32_kernel": "count32",
+            "tile_union_kernel": "tile_union", "edge_union_kernel": "edge_union",
+            "slab_root_labels_list_kernel": "slab_root_labels"}
 
 
-
-
-def base(name):
+def symbol(name):
+    """'void dbscan::(anonymous namespace)::foo_kernel<1536, 6>(args)' -> 'foo_kernel<1536, 6>'"""
     n = name.replace("(anonymous namespace)::", "")
     if n.startswith("void "):
         n = n[5:]
-    n = n.split("(")[0]
-    n = n.split("::")[-1]
-    return n.split("<")[0].strip()
+    depth, cut = 0, len(n)
+    for i, c in enumerate(n):  # the argument list starts at the first '(' outside <...>
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == "(" and depth == 0:
+            cut = i
+            break
+    n = n[:cut].strip()
+    head = n.split("<")[0]
+    return head.split("::")[-1] + n[len(head):]
 
 
-def per_kernel(path, counter):
-    acc = defaultdict(list)
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter:
-                acc[base(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+def stage_of(sym):
+    base = sym.split("<")[0]
+    if base in STAGE_OF:
+        return STAGE_OF[base]
+    return base[:-len("_kernel")] if base.endswith("_kernel") else None
 
 
 def main():
@@ -54,30 +62,62 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-    stats = {}
-    with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as f:
-        for r in csv.DictReader(f):
-            stats[base(r["Name"])] = float(r["AverageNs"])
-    rows, traffic = [], {}
-    for k in sorted(set(fetch) | set(write)):
-        fb = fetch.get(k, 0.0) * 2 * 1024
-        wb = write.get(k, 0.0) * 1024
-        rows.append((k, fetch.get(k, 0.0), write.get(k, 0.0), fb + wb, stats.get(k)))
-        st = stage_of(k)
-        if st:
-            traffic[st] = {"kernel": k, "bytes_per_launch": round(fb + wb),
-                           "fetch_kb": fetch.get(k), "write_kb": write.get(k),
-                           "avg_ns": stats.get(k), "source": f"profiles/{tag}_pmc.csv"}
+    stamp = open(os.path.join(src, "src_sha")).read().strip()
+    line = [l for l in open(os.path.join(src, "trace.log")) if l.startswith("{")][-1]
+    n_points = json.loads(line)["config"]["n_points"]
+    # durations and dispatch counts per instance from the kernel trace
+    dur, cnt = defaultdict(float), defaultdict(int)
+    for r in csv.DictReader(open(glob.glob(os.path.join(src, "trace", "**", "run_kernel_trace.csv"),
+                                           recursive=True)[0])):
+        s = symbol(r["Kernel_Name"])
+        dur[s] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+        cnt[s] += 1
+    # counters: mean per dispatch, per instance
+    ctr = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "**", "run_counter_collection.csv"),
+                              recursive=True)):
+        for r in csv.DictReader(open(f)):
+            ctr[symbol(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    names = sorted(set(ctr) | set(cnt), key=lambda s: -dur.get(s, 0.0))
+    cols = sorted({c for s in ctr for c in ctr[s]})
+    rows = []
+    for s in names:
+        avg = {c: (sum(v) / len(v)) for c, v in ctr[s].items()}
+        hbm = (2 * avg.get("FETCH_SIZE", 0.0) + avg.get("WRITE_SIZE", 0.0)) * 1024
+        rows.append((s, cnt.get(s, 0), dur[s] / cnt[s] if cnt.get(s) else None, hbm, avg))
     with open(os.path.join(prof, f"{tag}_pmc.csv"), "w") as f:
-        f.write("kernel,fetch_size_kb_avg,write_size_kb_avg,hbm_bytes_per_launch_est,avg_ns\n")
-        for r in rows:
-            f.write(f"{r[0]},{r[1]:.1f},{r[2]:.1f},{r[3]:.0f},{r[4] if r[4] else ''}\n")
+        w = csv.writer(f)
+        w.writerow(["kernel", "dispatches_in_trace", "avg_ns", "hbm_bytes_per_launch_est"] + cols)
+        for s, c, a, hbm, avg in rows:
+            w.writerow([s, c, f"{a:.0f}" if a else "", f"{hbm:.0f}"] +
+                       [f"{avg[k]:.1f}" if k in avg else "" for k in cols])
+    stages = defaultdict(lambda: {"instances": {}})
+    for s, c, a, hbm, avg in rows:
+        st = stage_of(s)
+        if not st or not c:
+            continue
+        stages[st]["instances"][s] = {"launches_in_trace": c, "avg_ns": a,
+                                      "hbm_bytes_per_launch": round(hbm), "counters": avg}
+    out = {}
+    for st, d in stages.items():
+        inst = d["instances"]
+        tot = sum(v["launches_in_trace"] for v in inst.values())
+        wavg = lambda key: sum(v[key] * v["launches_in_trace"] for v in inst.values()) / tot
+        cavg = lambda c: sum(v["counters"].get(c, 0.0) * v["launches_in_trace"]
+                             for v in inst.values()) / tot
+        valu = {c[len("SQ_INSTS_VALU_"):]: round(cavg(c), 1) for c in cols
+                if c.startswith("SQ_INSTS_VALU_") and c.split("_")[-1] in ("F32", "F64")}
+        sq = {c: round(cavg(c), 1) for c in cols if c.startswith("SQ_")}
+        out[st] = {"hbm_bytes_per_launch": round(wavg("hbm_bytes_per_launch")),
+                   "avg_ns": round(wavg("avg_ns"), 1), "valu_insts_per_launch": valu, "sq": sq,
+                   "instances": {k: {kk: vv for kk, vv in v.items() if kk != "counters"}
+                                 for k, v in inst.items()}}
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1, sort_keys=True)
-    for r in rows:
-        print(f"{r[0]:28s} fetchKB={r[1]:12.1f} writeKB={r[2]:12.1f} est_bytes={r[3]:14.0f}")
+        json.dump({"src_sha": stamp, "n_points": n_points,
+                   "source": f"profiles/{tag}_pmc.csv", "stages": out}, f, indent=1,
+                  sort_keys=True)
+    for s, c, a, hbm, avg in rows[:25]:
+        print(f"{s:40s} n={c:4d} avg_ns={a or 0:10.0f} hbm={hbm:14.0f}")
 
 
 if __name__ == "__main__":
