@@ -45,6 +45,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # VALU peaks in lane-operations per second (one lane of one VALU instruction; an FMA is ONE
 # lane-op here): fp64 vector 78.6 TFLOP/s counting FMA as 2 -> 39.3e12; fp32 157.3 -> 78.6e12.
 VALU_PEAK = {"f64": 39.3e12, "f32": 78.65e12}
+SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 # Algorithmic bytes per point and launch, by kernel (SURVEY.md §8d's per-phase figures; each
 # array crosses HBM once).  count = 21: the count kernel also builds the quarter
 # records and the tile-local quarter union (fused), so it carries §8d's count (sorted x,y 16 +
@@ -293,16 +294,28 @@ def main():
                      for t in ("f32", "f64")}
             rate = {t: lanes[t] / (avg_ms * 1e-3) for t in lanes}
             frac = sum(rate[t] / VALU_PEAK[t] for t in rate)
+            sq = pmc.get("sq") or {}
+            # every VALU wave-instruction (float, integer, moves) holds its SIMD >= 2 cycles
+            # (64 lanes over SIMD-32): issue share of 1024 SIMDs x 2.4 GHz x launch time
+            issue = (2.0 * sq.get("SQ_INSTS_VALU", 0.0) /
+                     (1024 * SIMD_CLOCK_HZ * avg_ms * 1e-3)) if sq else None
             valu = {"bound": "valu", "kernel": dom, "unit": "T lane-ops/s",
                     "achieved": {t: round(rate[t] / 1e12, 3) for t in rate},
                     "peak": {t: VALU_PEAK[t] / 1e12 for t in VALU_PEAK},
                     "frac": round(frac, 5),
                     "lane_ops_per_launch": {t: lanes[t] for t in lanes},
+                    "int32_lane_ops_per_launch": 64.0 * sq.get("SQ_INSTS_VALU_INT32", 0.0),
+                    "valu_issue_frac": round(issue, 4) if issue is not None else None,
+                    "wave_time": ({k: round(sq[k] / sq["SQ_WAVE_CYCLES"], 4) for k in
+                                   ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
+                                  if sq.get("SQ_WAVE_CYCLES") else None),
                     "note": ("lane-ops = 64 x VALU wave-instructions (SQ_INSTS_VALU_{ADD,MUL,FMA,"
                              "TRANS}_F32/F64, full exec mask assumed: an upper bound) over the "
                              "live average launch time; frac = f32/peak_f32 + f64/peak_f64 "
-                             "(both share the VALU)"),
-                    "sq": pmc.get("sq"), "source": pmc_src}
+                             "(both share the VALU); valu_issue_frac = every VALU instruction "
+                             "(integer included) x 2 cycles over the 1024 SIMDs' cycles; "
+                             "wave_time = share of wave cycles parked / issue-stalled / issuing"),
+                    "source": pmc_src}
 
     e2e = None
     if args.e2e_steps > 0:
