@@ -226,13 +226,18 @@ int32_t guarded(dbscan_handle* h, F&& f) {
     }
 }
 
+// local = the local-fit entry points, which also take DBSCAN_MODE_ARCHERY_F32BOX (its
+// directed neighbour relation has no slab/merge form)
 void check_fit_args(int64_t n, double eps, int32_t mode, const void* a, const void* b,
-                    const void* c, const void* d) {
+                    const void* c, const void* d, bool local = false) {
     (void)eps;
     if (n < 0) throw dbscan::ArgError{"n < 0"};
     if (n > DBSCAN_MAX_POINTS) throw dbscan::ArgError{"n exceeds DBSCAN_MAX_POINTS"};
-    if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY)
-        throw dbscan::ArgError{"mode must be DBSCAN_MODE_NAIVE or DBSCAN_MODE_ARCHERY"};
+    if (mode == DBSCAN_MODE_ARCHERY_F32BOX && !local)
+        throw dbscan::ArgError{"DBSCAN_MODE_ARCHERY_F32BOX is for the local fit entry points only"};
+    if (mode != DBSCAN_MODE_NAIVE && mode != DBSCAN_MODE_ARCHERY &&
+        mode != DBSCAN_MODE_ARCHERY_F32BOX)
+        throw dbscan::ArgError{"mode must be DBSCAN_MODE_NAIVE, _ARCHERY or _ARCHERY_F32BOX"};
     if (n > 0 && (!a || !b || !c || !d)) throw dbscan::ArgError{"NULL array pointer"};
 }
 
@@ -339,7 +344,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
     }
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
-        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
+        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag, true);
         if (h->pending && h->prof.pending.size() > 4096) settle(h);  // bound the event backlog
         h->pending = false;  // a newer fit replaces the unread stats of an older one
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
@@ -375,7 +380,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
         settle(h);
-        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag);
+        check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag, true);
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
         h->prepared = false;
@@ -396,7 +401,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
     return guarded(h, [&]() -> int32_t {
         std::lock_guard<std::mutex> lk(h->mu);
         settle(h);
-        check_fit_args(n, eps, mode, x, y, cluster_out, flag_out);
+        check_fit_args(n, eps, mode, x, y, cluster_out, flag_out, true);
         if (n == 0) {
             if (n_clusters_out) *n_clusters_out = 0;
             h->stats = dbscan::FitStats();

@@ -46,6 +46,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 namespace dbscan {
 
@@ -57,6 +58,8 @@ constexpr int kTslot = 65;        // per-tile cell-start table stride (64 cells 
 constexpr int kQReg = 4;          // own-quarter core points kept in registers for pair tests
 constexpr int64_t kTileGrid = 8192;  // workgroups of the per-tile kernels (grid stride)
 constexpr int kMaxNbr = 11;  // neighbour lists of non-cores kept while minPoints - 1 <= this
+constexpr int32_t kModeArcheryBox = 2;     // DBSCAN_MODE_ARCHERY_F32BOX
+constexpr int64_t kBoxEdgeCap = 1 << 22;   // one-way core-core pairs a box fit can hold
 
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
 // two rounded multiplies, one rounded add, <=.  The whole library is built with
@@ -2470,6 +2473,151 @@ __global__ __launch_bounds__(kBlock) void permute_out_kernel(
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
 
+// ---------------------------------------------------------------------------------------
+// LocalDBSCANArchery with its float32 R-tree search box (DBSCAN_MODE_ARCHERY_F32BOX).
+// The tree stores Point(p.x.toFloat, p.y.toFloat) (LocalDBSCANArchery.scala:38-41) and a
+// query searches Box((x-eps).toFloat, (y-eps).toFloat, (x+eps).toFloat, (y+eps).toFloat)
+// (:118-124), filtered by the fp64 predicate (:114-116).  So o is a neighbour of p iff
+// d2 <= eps2 AND o's float point lies in p's float box -- a DIRECTED relation: near the box
+// edge one of the two directions can fail.  Containment is taken inclusive on all four sides
+// (archery 0.3.0's source is absent: the one unpinned assumption).
+//   core(p)  <=> |N(p)| >= minPoints (N(p) from p's own box)
+//   clusters: components of the core-core pairs that hold in BOTH directions, plus the
+//             one-way core-core pairs, recorded here and resolved on the host exactly as the
+//             sequential expansion does (components in s order; a new cluster claims every
+//             component reachable over one-way pairs that no earlier cluster claimed)
+//   non-core b: Border of the smallest cluster number among cores c with b in N(c), else Noise
+// (the archery re-claim rule, :103-106).  One thread per point over the global stencil
+// pieces: this mode is a parity path, not the bench path.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool in_f32_box(double px, double py, double ox, double oy,
+                                           double eps) {
+#pragma clang fp contract(off)
+    const float x1 = (float)(px - eps), y1 = (float)(py - eps);
+    const float x2 = (float)(px + eps), y2 = (float)(py + eps);
+    const float fx = (float)ox, fy = (float)oy;
+    return x1 <= fx && fx <= x2 && y1 <= fy && fy <= y2;
+}
+
+__global__ __launch_bounds__(kBlock) void box_count_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, double eps, double eps2,
+    int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
+    int32_t* __restrict__ block_cores) {
+    __shared__ int wcores[kBlock / 64];
+    const int64_t nf = *nf_p;
+    int mine = 0;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
+         p += (int64_t)gridDim.x * kBlock) {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int cnt = 0;
+        if (min_points > 0)
+            for_candidates(s, [&](int j) {
+                const double2 q = xy[j];
+                cnt += (within_eps(me.x, me.y, q.x, q.y, eps2) &&
+                        in_f32_box(me.x, me.y, q.x, q.y, eps)) ? 1 : 0;
+                return cnt < min_points;
+            });
+        const bool is_core = cnt >= min_points;
+        parent[p] = (int32_t)p;
+        core[p] = is_core ? 1 : 0;
+        mine += is_core ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        block_cores[blockIdx.x] = tot;
+    }
+}
+
+// Core-core pairs: both directions -> union (once, from the larger slot); one direction only
+// -> the directed pair (source slot, target slot) is recorded by its source, up to `cap`
+// (the count keeps growing past it, so an overflow is detected on the host).
+__global__ __launch_bounds__(kBlock) void box_union_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, double eps, double eps2,
+    const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
+    int32_t* __restrict__ parent, int2* __restrict__ edges, int32_t* __restrict__ n_edges,
+    int32_t cap) {
+    const int64_t nf = *nf_p;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
+         p += (int64_t)gridDim.x * kBlock) {
+        if (!core[p]) continue;
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        int rp = uf_find(parent, (int)p);
+        for_candidates(s, [&](int j) {
+            if (j == (int)p || !core[j]) return true;
+            const double2 q = xy[j];
+            if (!within_eps(me.x, me.y, q.x, q.y, eps2)) return true;
+            const bool fwd = in_f32_box(me.x, me.y, q.x, q.y, eps);  // q in N(p)
+            const bool bwd = in_f32_box(q.x, q.y, me.x, me.y, eps);  // p in N(q)
+            if (fwd && bwd) {
+                if (j < (int)p) {
+                    const int rj = uf_find(parent, j);
+                    if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
+                }
+            } else if (fwd) {
+                const int k = atomicAdd(n_edges, 1);
+                if (k < cap) edges[k] = make_int2((int)p, j);
+            }
+            return true;
+        });
+    }
+}
+
+// The recorded pairs as (component number of the source, of the target), 0-based in s order.
+__global__ __launch_bounds__(kBlock) void box_edge_ranks_kernel(
+    const int2* __restrict__ edges, int32_t m, const int32_t* __restrict__ lab,
+    const uint64_t* __restrict__ root_bits, const int32_t* __restrict__ word_rank,
+    int2* __restrict__ out) {
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    const int2 e = edges[k];
+    out[k] = make_int2((int)cluster_of_root(root_bits, word_rank, lab[e.x]) - 1,
+                       (int)cluster_of_root(root_bits, word_rank, lab[e.y]) - 1);
+}
+
+// Labels (packed per sorted slot like label_sorted_kernel): cores their component's cluster
+// number; non-cores the smallest cluster number among cores c whose box holds them.  cmap
+// (one-way pairs present): component number -> cluster number; else the identity.
+__global__ __launch_bounds__(kBlock) void box_label_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, int64_t n, double eps,
+    double eps2, const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
+    const uint64_t* __restrict__ root_bits, const int32_t* __restrict__ word_rank,
+    const int32_t* __restrict__ cmap, uint32_t* __restrict__ packed) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    auto number = [&](int j) -> uint32_t {
+        const uint32_t c = cluster_of_root(root_bits, word_rank, lab[j]);
+        return cmap ? (uint32_t)cmap[c - 1] : c;
+    };
+    uint32_t v = 0;  // Noise
+    if (core[p]) {
+        v = (number((int)p) << 1) | 1u;
+    } else if (p < *nf_p) {
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        uint32_t best = 0xFFFFFFFFu;
+        for_candidates(s, [&](int j) {
+            if (!core[j]) return true;
+            const double2 q = xy[j];
+            if (within_eps(q.x, q.y, me.x, me.y, eps2) && in_f32_box(q.x, q.y, me.x, me.y, eps)) {
+                const uint32_t c = number(j);
+                best = c < best ? c : best;
+            }
+            return true;
+        });
+        if (best != 0xFFFFFFFFu) v = best << 1;  // Border
+    }
+    packed[p] = v;
+}
+
 // Two-part slab label (dbscan_slab_roots_prepare_device + dbscan_slab_label_finish_device_async):
 // the ROOTS-packed labels moved to slab order before the roots are numbered (zone 1/2 entries
 // 0), so the part that waits for the numbering is one coalesced pass.
@@ -2677,6 +2825,67 @@ static constexpr int count_cap() { return DBSCAN_AB_COUNT_CAP; }
 static constexpr bool f32_count() { return DBSCAN_AB_F32 != 0; }
 static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
 
+// Archery float32 box, after the rank scan: the one-way core-core pairs decide which component
+// a cluster's expansion claims beyond its own.  Usually there are none (returns nullptr: the
+// cluster number is the component number).  Otherwise the sequential rule on the component
+// graph: components in s order; an unclaimed one opens the next cluster, which then claims every
+// unclaimed component reachable over one-way pairs (LocalDBSCANArchery.scala:45-63, 82-110).
+// The only host synchronization of a fit, and only in this mode.
+static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* st, const int32_t* lab,
+                                 const uint64_t* root_bits, const int32_t* word_rank) {
+    int32_t hst[kStCount];
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(hst, st, sizeof(hst), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t m = hst[kStBoxEdges], k = hst[kStClusters];
+    if (m == 0) return nullptr;
+    if (m > kBoxEdgeCap)
+        throw ArgError{"archery float32 box: more one-way core pairs than the library holds"};
+    int2* edges = static_cast<int2*>(ws.box_edges.p);
+    int2* ranks = edges + kBoxEdgeCap;
+    hipLaunchKernelGGL(box_edge_ranks_kernel, dim3(nblk(m)), dim3(kBlock), 0, s, edges,
+                       (int32_t)m, lab, root_bits, word_rank, ranks);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    std::vector<int2> e((size_t)m);
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(e.data(), ranks, m * sizeof(int2), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    // CSR of the component graph (self pairs inside a component carry no information)
+    std::vector<int32_t> head((size_t)k + 1, 0), adj;
+    for (const int2& v : e)
+        if (v.x != v.y) ++head[(size_t)v.x + 1];
+    for (int64_t c = 0; c < k; ++c) head[(size_t)c + 1] += head[(size_t)c];
+    adj.resize((size_t)head[(size_t)k]);
+    {
+        std::vector<int32_t> fill(head.begin(), head.end() - 1);
+        for (const int2& v : e)
+            if (v.x != v.y) adj[(size_t)fill[(size_t)v.x]++] = v.y;
+    }
+    std::vector<int32_t> cmap((size_t)k, 0), stack;
+    int32_t next = 0;
+    for (int64_t c = 0; c < k; ++c) {
+        if (cmap[(size_t)c]) continue;
+        cmap[(size_t)c] = ++next;
+        stack.assign(1, (int32_t)c);
+        while (!stack.empty()) {
+            const int32_t u = stack.back();
+            stack.pop_back();
+            for (int32_t q = head[(size_t)u]; q < head[(size_t)u + 1]; ++q) {
+                const int32_t w = adj[(size_t)q];
+                if (!cmap[(size_t)w]) {
+                    cmap[(size_t)w] = next;
+                    stack.push_back(w);
+                }
+            }
+        }
+    }
+    int32_t* d_map = static_cast<int32_t*>(ws.box_map.ensure((size_t)k * sizeof(int32_t) + 4));
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(d_map, cmap.data(), (size_t)k * sizeof(int32_t),
+                                    hipMemcpyHostToDevice, s));
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(&st[kStClusters], &next, sizeof(int32_t),
+                                    hipMemcpyHostToDevice, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));  // (the host vectors go out of scope)
+    return d_map;
+}
+
 // Enqueues one whole fit on stream s and never waits on the device: the grid, the finite count
 // nf and every table size live in device memory (ws.misc), so launch sizes derive from n alone
 // and kernels bound themselves by the device-side counts.  The grid is sized by grid_kernel
@@ -2765,13 +2974,17 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
     // the tile-local quarter union runs inside the count kernels (slab fits: the fp32 count
     // kernels, which read the sorted zones; the fp64 fused kernel would union zone-2 points)
-    const bool fuse =
-        mode == kGridEps && fuse_union() && count_cap() == 0 && (!a.zone || f32_count());
+    // archery's float32 search box (mode 2): its own count / union / label kernels over the
+    // global stencil pieces; none of the clique-quarter or fp32-record paths
+    const bool box = a.mode == kModeArcheryBox;
+    const bool fuse = !box && mode == kGridEps && fuse_union() && count_cap() == 0 &&
+                      (!a.zone || f32_count());
     uint8_t* zs = (a.zone && fuse) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
     // clique grids: the fp32-record count kernels by tile class (tile_class_kernel);
     // DBSCAN_F32=0 keeps the fp64 count_tile_kernel for A/B measurements
     const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
-    const int nbr_k = (a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
+    const int nbr_k =
+        (!box && a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
     TileLists tl{};
     uint8_t* tclass = nullptr;
     if (f32) {
@@ -2867,7 +3080,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 default: break;
             }
             const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp};
-            if (f32) {
+            if (box) {
+                klaunch(prof, "box_count", box_count_kernel, dim3(tile_grid), dim3(kBlock), 0, s,
+                        xy, cell, seg, nf_p, a.eps, eps2, a.min_points, core, parent,
+                        block_cores);
+            } else if (f32) {
                 // clique grids by tile stage size: small tiles one wave each (count_wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
                 // big_union); other grids: count (fp64)
@@ -2905,7 +3122,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
                                core);
     }
-    if (mode == kGridEps) {  // quarter-cell unions (no-ops unless the grid made them cliques)
+    if (mode == kGridEps && !box) {  // quarter-cell unions (no-ops unless the grid made them cliques)
         if (!fuse) {
             StageTimer t(prof, s, "quarter_init");
             klaunch(prof, "quarter_init", quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
@@ -2937,8 +3154,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
         StageTimer t(prof, s, "union");
-        klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 4096u)), dim3(kBlock), 0, s, xy, cell, seg, nf_p, gp,
-                           eps2, perm, core, parent);
+        if (box) {
+            int2* edges = static_cast<int2*>(ws.box_edges.ensure(2 * kBoxEdgeCap * sizeof(int2)));
+            klaunch(prof, "box_union", box_union_kernel, dim3(std::min(nblk(n), 4096u)),
+                    dim3(kBlock), 0, s, xy, cell, seg, nf_p, a.eps, eps2, perm, core, parent,
+                    edges, &st[kStBoxEdges], (int32_t)kBoxEdgeCap);
+        } else {
+            klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 4096u)), dim3(kBlock), 0,
+                    s, xy, cell, seg, nf_p, gp, eps2, perm, core, parent);
+        }
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     if (!a.zone) {
@@ -2957,7 +3181,17 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             StageTimer t(prof, s, "rank");
             exclusive_scan(s, 2, root_bits, word_rank, nw, &st[kStClusters], ws.scan);
         }
-        {
+        if (box) {
+            StageTimer t(prof, s, "output");
+            const int32_t* cmap = resolve_box_pairs(s, ws, st, lab, root_bits, word_rank);
+            uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
+            klaunch(prof, "box_label", box_label_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
+                    cell, seg, nf_p, n, a.eps, eps2, core, lab, root_bits, word_rank, cmap,
+                    packed);
+            klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0,
+                    s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        } else {
             StageTimer t(prof, s, "output");
             uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
             klaunch(prof, "label_sorted", label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,

@@ -51,6 +51,7 @@ enum FitState {
     kStError = 8,     // the eps grid could not be sized
     kStTileLists = 9,  // [3] clique-grid tiles per count path: small, medium, big
     kStClassPts = 12,  // [3] their own points (what each count kernel processes)
+    kStBoxEdges = 15,  // archery float32 box: one-way core-core pairs recorded
     kStCount = 16
 };
 
@@ -149,7 +150,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots;
+        key3, perm3, spacked, lroots, box_edges, box_map;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -161,7 +162,8 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots})
+                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
+                          &box_edges, &box_map})
             b->release();
     }
 };

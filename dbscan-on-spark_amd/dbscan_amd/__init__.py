@@ -4,6 +4,6 @@ Drop-in for the reference's hot path `new LocalDBSCANNaive(eps, minPoints).fit(p
 (DBSCAN.scala:153-154).  Compute lives in libdbscan_hip.so (hand-written HIP kernels, C-ABI
 in include/dbscan_hip.h); this package is the host-side mirror of the reference interface.
 """
-from ._lib import (DBSCANError, Handle, MODE_ARCHERY, MODE_NAIVE, LIB_PATH, load)  # noqa: F401
+from ._lib import (DBSCANError, Handle, MODE_ARCHERY, MODE_ARCHERY_F32BOX, MODE_NAIVE, LIB_PATH, load)  # noqa: F401
 from .local import (DBSCANLabeledPoint, DBSCANPoint, Flag, LocalDBSCANArchery,  # noqa: F401
                     LocalDBSCANNaive, Unknown, fit_arrays, train_node)

@@ -17,6 +17,9 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "dbscan_hip.h")
 
 DBSCAN_OK, DBSCAN_EARG, DBSCAN_EHIP, DBSCAN_EOOM = 0, -1, -2, -3
 MODE_NAIVE, MODE_ARCHERY = 0, 1
+# LocalDBSCANArchery with its float32 R-tree search box (LocalDBSCANArchery.scala:38-41,118-124):
+# local fits only
+MODE_ARCHERY_F32BOX = 2
 
 # (name, restype, argtypes) for every symbol include/dbscan_hip.h declares.
 _vp, _i32, _i64, _d, _u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, \

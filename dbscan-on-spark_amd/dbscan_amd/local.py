@@ -156,7 +156,15 @@ class LocalDBSCANNaive(_LocalDBSCAN):
 
 
 class LocalDBSCANArchery(_LocalDBSCAN):
-    """LocalDBSCANArchery(eps, minPoints).fit(points).  Visit order = input order (archery's
-    R-tree entry order is not reproducible; its labels match up to permutation)."""
+    """LocalDBSCANArchery(eps, minPoints).fit(points): neighbours are the points whose float32
+    coordinates lie in the float32 box (x-eps, y-eps, x+eps, y+eps) AND pass the fp64 predicate
+    (LocalDBSCANArchery.scala:38-41,114-124), Noise re-claimed as Border (:103-106).  Visit
+    order = input order (archery's R-tree entry order is not reproducible; its labels match up
+    to permutation).  f32_box=False: the exact fp64 neighbour set (DBSCAN_MODE_ARCHERY)."""
 
-    _mode = _lib.MODE_ARCHERY
+    _mode = _lib.MODE_ARCHERY_F32BOX
+
+    def __init__(self, eps: float, minPoints: int, handle: Optional[_lib.Handle] = None,
+                 f32_box: bool = True):
+        super().__init__(eps, minPoints, handle)
+        self._mode = _lib.MODE_ARCHERY_F32BOX if f32_box else _lib.MODE_ARCHERY

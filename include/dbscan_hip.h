@@ -46,6 +46,11 @@ extern "C" {
 
 #define DBSCAN_MODE_NAIVE 0   /* LocalDBSCANNaive   (used by DBSCAN.train, DBSCAN.scala:154) */
 #define DBSCAN_MODE_ARCHERY 1 /* LocalDBSCANArchery (LocalDBSCANArcherySuite)               */
+/* LocalDBSCANArchery with its float32 R-tree search box applied before the fp64 filter
+ * (LocalDBSCANArchery.scala:38-41,114-124): a directed neighbour relation.  Local fits only
+ * (dbscan_fit, dbscan_fit_h, dbscan_fit_device, dbscan_fit_device_async -- the async form waits
+ * on the device once, to resolve one-way pairs); slab and node entry points reject it. */
+#define DBSCAN_MODE_ARCHERY_F32BOX 2
 
 /* return codes */
 #define DBSCAN_OK 0

@@ -26,6 +26,10 @@
  *   oracle_fit_bruteforce   order-parametrised closed form with all-pairs counts
  *   oracle_fit_grid         the same closed form on an eps grid, pthreads (large n; also the
  *                           "strong CPU comparator" of BASELINE.md)
+ *   oracle_fit_bfs_grid     the literal sequential BFS of (1) with its neighbour queries on the
+ *                           eps grid (large n, every mode: the reference for archery's float32
+ *                           search box, whose directed neighbour relation the closed form
+ *                           does not cover)
  * tests/ fuzz all three against each other and against the golden fixture.
  *
  * MUST be compiled with -ffp-contract=off (see oracle/Makefile): the JVM never fuses
@@ -129,8 +133,8 @@ int32_t oracle_fit_sequential(const double* x, const double* y, int64_t n, doubl
                     /* Naive :108-111 (cluster == Unknown) is dead code: cluster was set above. */
                 }
                 if (mode != MODE_NAIVE && cluster[j] == 0) {
-                    /* LocalDBSCANArchery.scala (file lines 223-226): outside the !visited
-                     * test, so an earlier Noise point is re-claimed as Border. */
+                    /* LocalDBSCANArchery.scala:103-106: outside the !visited test, so an
+                     * earlier Noise point is re-claimed as Border. */
                     cluster[j] = c;
                     flag[j] = FLAG_BORDER;
                 }
@@ -588,6 +592,97 @@ int32_t oracle_fit_grid(const double* x, const double* y, int64_t n, double eps,
     int32_t k = finish_labels(n, g.core, g.parent, g.bmin, mode, cluster, flag);
     grid_free(&g);
     return k;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * 3b. The literal sequential BFS of section 1 with grid neighbour queries.  Within one
+ *     expandCluster the order in which neighbours are taken does not change which points the
+ *     expansion claims (every unvisited point reachable through cores, plus, for archery,
+ *     every Noise point a claimed core reaches), so enumerating a neighbourhood over the 3x3
+ *     stencil instead of array order gives the same labels.  mode 2 (archery's float32 search
+ *     box, LocalDBSCANArchery.scala:38-41,114-124) makes the neighbour relation directed:
+ *     N(p) = {o : d2 <= eps2 and (float)o in p's float32 box}.
+ * ------------------------------------------------------------------------------------------ */
+static int64_t grid_neighbors(const grid_ctx* g, int64_t p, double eps, int mode, int64_t* out) {
+    int64_t m = 0;
+    if (g->cell_of[p] < 0) return 0;
+    int64_t b[3], e[3];
+    int nr = stencil_ranges(g, g->cell_of[p], b, e);
+    for (int r = 0; r < nr; ++r)
+        for (int64_t t = b[r]; t < e[r]; ++t) {
+            int64_t o = g->order[t];
+            if (is_neighbor(g->x, g->y, p, o, eps, g->eps2, mode)) {
+                if (out) out[m] = o;
+                ++m;
+            }
+        }
+    return m;
+}
+
+int32_t oracle_fit_bfs_grid(const double* x, const double* y, int64_t n, double eps,
+                            int32_t min_points, int32_t mode, int32_t* cluster, uint8_t* flag) {
+    grid_ctx g;
+    grid_build(&g, x, y, n, eps, min_points);
+    if (g.all_pairs || g.no_pairs) { /* one all-pairs cell or no pairs: the O(n^2) form */
+        grid_free(&g);
+        return oracle_fit_sequential(x, y, n, eps, min_points, mode, cluster, flag);
+    }
+    size_t nn = (size_t)(n > 0 ? n : 1);
+    uint8_t* visited = (uint8_t*)calloc(nn, 1);
+    int64_t* queue = (int64_t*)malloc(sizeof(int64_t) * nn);
+    int64_t* cnt = (int64_t*)malloc(sizeof(int64_t) * nn);
+    int64_t cap = 1024;
+    int64_t* nb = (int64_t*)malloc(sizeof(int64_t) * (size_t)cap);
+    for (int64_t i = 0; i < n; ++i) {
+        cluster[i] = 0;
+        flag[i] = FLAG_NOTFLAGGED;
+        cnt[i] = grid_neighbors(&g, i, eps, mode, NULL);
+    }
+    int32_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (visited[i]) continue;
+        visited[i] = 1;
+        if (cnt[i] < (int64_t)min_points) {
+            flag[i] = FLAG_NOISE;
+            continue;
+        }
+        const int32_t c = ++total;
+        flag[i] = FLAG_CORE;
+        cluster[i] = c;
+        int64_t qh = 0, qt = 0;
+        queue[qt++] = i;
+        while (qh < qt) {
+            const int64_t centre = queue[qh++];
+            if (cnt[centre] > cap) {
+                cap = cnt[centre];
+                nb = (int64_t*)realloc(nb, sizeof(int64_t) * (size_t)cap);
+            }
+            int64_t m = grid_neighbors(&g, centre, eps, mode, nb);
+            for (int64_t k = 0; k < m; ++k) {
+                const int64_t j = nb[k];
+                if (!visited[j]) {
+                    visited[j] = 1;
+                    cluster[j] = c;
+                    if (cnt[j] >= (int64_t)min_points) {
+                        flag[j] = FLAG_CORE;
+                        queue[qt++] = j;
+                    } else {
+                        flag[j] = FLAG_BORDER;
+                    }
+                }
+                if (mode != MODE_NAIVE && cluster[j] == 0) {
+                    cluster[j] = c;
+                    flag[j] = FLAG_BORDER;
+                }
+            }
+        }
+    }
+    free(visited);
+    free(queue);
+    free(cnt);
+    free(nb);
+    grid_free(&g);
+    return total;
 }
 
 /* ------------------------------------------------------------------------------------------

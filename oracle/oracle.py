@@ -56,6 +56,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_fit_bruteforce.restype = i32
         L.oracle_fit_grid.argtypes = [dp, dp, i64, ctypes.c_double, i32, i32, i32, vp, vp, vp]
         L.oracle_fit_grid.restype = i32
+        L.oracle_fit_bfs_grid.argtypes = [dp, dp, i64, ctypes.c_double, i32, i32, vp, vp]
+        L.oracle_fit_bfs_grid.restype = i32
         L.ref_partition.argtypes = [dp, dp, i64, ctypes.c_double, i64, vp, vp, i64]
         L.ref_partition.restype = i64
         L.ref_partition_cells.argtypes = [dp, dp, dp, i64, i64, ctypes.c_double, vp, vp, i64]
@@ -104,6 +106,18 @@ def fit_sequential(x, y, eps, min_points, mode=NAIVE):
     fl = np.zeros(n, np.uint8)
     k = lib().oracle_fit_sequential(_ptr(x), _ptr(y), n, float(eps), int(min_points), int(mode),
                                     _ptr(cl), _ptr(fl))
+    return cl, fl, int(k)
+
+
+def fit_bfs_grid(x, y, eps, min_points, mode=NAIVE):
+    """The literal BFS with neighbour queries on the eps grid (every mode, incl. ARCHERY_F32BOX:
+    archery's float32 search box).  Returns (cluster int32[n], flag uint8[n], n_clusters)."""
+    x, y = _xy(x, y)
+    n = x.size
+    cl = np.zeros(n, np.int32)
+    fl = np.zeros(n, np.uint8)
+    k = lib().oracle_fit_bfs_grid(_ptr(x), _ptr(y), n, float(eps), int(min_points), int(mode),
+                                  _ptr(cl), _ptr(fl))
     return cl, fl, int(k)
 
 

@@ -66,3 +66,34 @@ def gen_blobs(n, noise=0.0, dense=1.0, seed=1, k=32):
     perm = rng.permutation(n)
     allp = allp[perm]
     return allp[:, 0].copy(), allp[:, 1].copy()
+
+
+def neg_eps_set(seed, n=600, scale=1e6, eps=-0.02):
+    """Archery float32-box stress set: points near float32 rounding midpoints far from the
+    origin with a NEGATIVE eps.  The fp64 predicate treats eps like |eps|, but archery's float32
+    box (x-eps .. x+eps, LocalDBSCANArchery.scala:118-124) is inverted: empty, or one float
+    wide where both edges round to the same float.  So the neighbour relation is directed and
+    many pairs hold one way only (the case the one-way-pair resolution exists for)."""
+    rng = np.random.default_rng(seed)
+    u = float(np.spacing(np.float32(scale)))
+    k = int(rng.integers(3, 9))
+    cx = scale + (rng.integers(0, 50, k) + 0.5) * u
+    cy = -scale + (rng.integers(0, 50, k) + 0.5) * u
+    lab = rng.integers(0, k, n)
+    x = cx[lab] + rng.normal(0, abs(eps) * 0.7, n)
+    y = cy[lab] + rng.normal(0, abs(eps) * 0.7, n)
+    return x, y
+
+
+def one_way_pairs(x, y, eps):
+    """Number of ordered pairs (p, o) with o in N(p) but p not in N(o) under archery's float32
+    box + fp64 predicate (numpy, O(n^2): small sets only)."""
+    f = np.float32
+    dx = x[None, :] - x[:, None]
+    dy = y[None, :] - y[:, None]
+    w = dx * dx + dy * dy <= eps * eps
+    x1, x2 = (x - eps).astype(f)[:, None], (x + eps).astype(f)[:, None]
+    y1, y2 = (y - eps).astype(f)[:, None], (y + eps).astype(f)[:, None]
+    fx, fy = x.astype(f)[None, :], y.astype(f)[None, :]
+    fwd = w & (x1 <= fx) & (fx <= x2) & (y1 <= fy) & (fy <= y2)
+    return int((fwd != fwd.T).sum())

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from conftest import EPS_03F, gen_blobs, load_edge_cases
+from conftest import EPS_03F, gen_blobs, load_edge_cases, neg_eps_set, one_way_pairs
 
 # csv column 3 is archery's entry-order numbering; input-order
 # Naive ids {1,2,3} correspond to csv labels {1,3,2}; Noise stays 0.
@@ -112,6 +112,66 @@ def test_naive_archery_differ_only_in_noise_reclaim():
     assert np.all(fn[diff] == O.NOISE) and np.all(fa[diff] == O.BORDER)
     same = ~diff
     np.testing.assert_array_equal(cn[same], ca[same])
+
+
+# ------------------------- archery's float32 search box (mode 2) --------------------------
+@pytest.mark.parametrize("seed", range(12))
+def test_bfs_grid_equals_sequential(seed):
+    """The grid-query BFS (the large-n oracle of every mode) equals the literal O(n^2) BFS,
+    modes 0/1/2, on blob fuzz (some far from the origin) and on negative-eps box sets."""
+    rng = np.random.default_rng(500 + seed)
+    n = int(rng.integers(100, 800))
+    c = rng.uniform(-3, 3, size=(4, 2)) + (rng.uniform(1e3, 1e6) if seed % 2 else 0.0)
+    pts = c[rng.integers(0, 4, n)] + rng.normal(0, rng.uniform(0.05, 0.4), size=(n, 2))
+    x, y = pts[:, 0].copy(), pts[:, 1].copy()
+    eps = float(rng.uniform(0.05, 0.3))
+    mp = int(rng.integers(1, 10))
+    cases = [(x, y, eps, mp), neg_eps_set(seed, 400) + (-0.02, 1 + seed % 4)]
+    for cx, cy, e, m in cases:
+        for mode in (O.NAIVE, O.ARCHERY, O.ARCHERY_F32BOX):
+            a = O.fit_sequential(cx, cy, e, m, mode)
+            b = O.fit_bfs_grid(cx, cy, e, m, mode)
+            np.testing.assert_array_equal(b[1], a[1])
+            np.testing.assert_array_equal(b[0], a[0])
+            assert a[2] == b[2]
+
+
+@pytest.mark.parametrize("offset", [0.0, 1e3, 1e5, 1e7])
+def test_f32_box_never_excludes_with_positive_eps(offset):
+    """With eps >= 0 archery's float32 box only widens the fp64 neighbourhood (float rounding is
+    monotone and the box is inclusive), so mode 2 equals mode 1 bit for bit -- here on blobs at
+    growing distances from the origin; SURVEY's 'ulp-scale box edge' difference does not arise.
+    A negative eps inverts the box: there the modes differ (next test)."""
+    rng = np.random.default_rng(int(offset) % 1000 + 1)
+    n = 2000
+    c = rng.uniform(-2, 2, size=(6, 2)) + offset
+    pts = c[rng.integers(0, 6, n)] + rng.normal(0, 0.2, size=(n, 2))
+    x, y = pts[:, 0].copy(), pts[:, 1].copy()
+    for eps in (0.05, float(np.float32(0.3)), 0.1 + 2.0 ** -30):
+        a = O.fit_bfs_grid(x, y, eps, 5, O.ARCHERY_F32BOX)
+        b = O.fit_grid(x, y, eps, 5, O.ARCHERY)
+        for u, v in zip(a, b):
+            np.testing.assert_array_equal(u, v)
+        assert one_way_pairs(x[:1500], y[:1500], eps) == 0
+
+
+def test_f32_box_negative_eps_is_directed():
+    """The negative-eps sets do produce one-way pairs, and mode 2 then differs from mode 1."""
+    x, y = neg_eps_set(1)
+    assert one_way_pairs(x, y, -0.02) > 0
+    a = O.fit_sequential(x, y, -0.02, 3, O.ARCHERY_F32BOX)
+    b = O.fit_sequential(x, y, -0.02, 3, O.ARCHERY)
+    assert (a[1] != b[1]).any()
+
+
+def test_f32_box_labeled_csv(labeled_data, labeled_expected):
+    """LocalDBSCANArcherySuite 'should cluster' with the float32 box: the same labels as the
+    exact fp64 set (677 Core / 54 Border / 18 Noise)."""
+    x, y, _ = labeled_data
+    cl, fl, k = O.fit_sequential(x, y, EPS_03F, 10, O.ARCHERY_F32BOX)
+    np.testing.assert_array_equal(cl, labeled_expected["cluster_archery"])
+    np.testing.assert_array_equal(fl, labeled_expected["flag_archery"])
+    assert k == 3
 
 
 # ---------------------------------- reference driver --------------------------------------
