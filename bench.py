@@ -92,7 +92,7 @@ def host_threads() -> int:
     return max(1, n)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -112,7 +112,19 @@ def parse():
                     help="untimed steps with every kernel timed (the breakdown)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--node", action="store_true", help="use the node path even at N = 1")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def workload_defaults(args, world):
+    """Fill the unset workload flags: config 2 at N = 1 (G(10^7, no noise, seed 1)); config 3
+    weak-scaled at N > 1 (1.25*10^7 points per GPU, 20% noise, seed 2: G(10^8) at N = 8)."""
+    if args.points_per_gpu is None:
+        args.points_per_gpu = 12_500_000 if world > 1 else 10_000_000
+    if args.noise is None:
+        args.noise = 0.2 if world > 1 else 0.0
+    if args.seed is None:
+        args.seed = 2 if world > 1 else 1
+    return args
 
 
 def load_pmc(stage, n_points, stamp):
@@ -181,12 +193,7 @@ def main():
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     node_path = world > 1 or args.node
-    if args.points_per_gpu is None:
-        args.points_per_gpu = 12_500_000 if world > 1 else 10_000_000
-    if args.noise is None:
-        args.noise = 0.2 if world > 1 else 0.0
-    if args.seed is None:
-        args.seed = 2 if world > 1 else 1
+    workload_defaults(args, world)
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     import dbscan_amd

@@ -5,12 +5,15 @@
 //   DBSCANPoint          DBSCANPoint.scala:21-32        x = vector(0), y = vector(1)
 //   DBSCANLabeledPoint   DBSCANLabeledPoint.scala:24-47 flag, cluster (Unknown = 0), visited
 //   LocalDBSCANNaive     LocalDBSCANNaive.scala:31-120  fit(points) in input order
-//   LocalDBSCANArchery   LocalDBSCANArchery.scala:32-126
+//   LocalDBSCANArchery   LocalDBSCANArchery.scala:32-126 (float32 search box: mode 2)
+//   DBSCANRectangle      DBSCANRectangle.scala:23-53
+//   DBSCAN::train        DBSCAN.scala:40-48,72-283: labeledPoints (input order) + partitions
 // A vector with fewer than two coordinates throws std::out_of_range (the reference's
 // IndexOutOfBounds from vector(1)); HIP failures throw std::runtime_error with
 // dbscan_last_error().  There is no CPU fallback.
 #pragma once
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -109,20 +112,109 @@ class LocalDBSCANNaive {
     Handle* h_;
 };
 
-// new LocalDBSCANArchery(eps, minPoints).fit(points)  (LocalDBSCANArchery.scala:32,36);
-// visit order = input order (archery's R-tree entry order is not reproducible).
+// new LocalDBSCANArchery(eps, minPoints).fit(points)  (LocalDBSCANArchery.scala:32,36): the
+// float32 R-tree search box + fp64 filter (:38-41,114-124); f32Box = false takes the exact fp64
+// neighbour set.  Visit order = input order (archery's R-tree entry order is not reproducible).
 class LocalDBSCANArchery {
    public:
-    LocalDBSCANArchery(double eps, int minPoints, Handle* h = nullptr)
-        : eps_(eps), minPoints_(minPoints), h_(h) {}
+    LocalDBSCANArchery(double eps, int minPoints, Handle* h = nullptr, bool f32Box = true)
+        : eps_(eps), minPoints_(minPoints), h_(h), f32Box_(f32Box) {}
     std::vector<DBSCANLabeledPoint> fit(const std::vector<DBSCANPoint>& points) const {
-        return detail::fit(h_, eps_, minPoints_, DBSCAN_MODE_ARCHERY, points);
+        return detail::fit(h_, eps_, minPoints_,
+                           f32Box_ ? DBSCAN_MODE_ARCHERY_F32BOX : DBSCAN_MODE_ARCHERY, points);
     }
 
    private:
     double eps_;
     int minPoints_;
     Handle* h_;
+    bool f32Box_;
+};
+
+// DBSCANRectangle.scala:23 -- (x, y) lower-left, (x2, y2) upper-right
+struct DBSCANRectangle {
+    double x, y, x2, y2;
+    bool operator==(const DBSCANRectangle& o) const {
+        return x == o.x && y == o.y && x2 == o.x2 && y2 == o.y2;
+    }
+};
+
+// DBSCAN.train(data, eps, minPoints, maxPointsPerPartition) (DBSCAN.scala:40-48).
+//   partitions()    the reference's (id, rectangle) list: EvenSplitPartitioner over the 2*eps
+//                   cell histogram, in list order (DBSCAN.scala:91-104, 283)
+//   labeledPoints() every input point once, in input order, from dbscan_train_node: x-slabs
+//                   over the visible GPUs with eps halos and an exact merge, equal to ONE
+//                   LocalDBSCANNaive fit of all points.  (The reference's own merge can drop or
+//                   duplicate points and report halo cores as Border; cluster
+//                   ids here are the input-order Naive numbering, equal to the reference's up
+//                   to permutation.)
+//   nShards = 0: one slab per visible GPU.
+class DBSCAN {
+   public:
+    static DBSCAN train(const std::vector<DBSCANPoint>& data, double eps, int minPoints,
+                        int maxPointsPerPartition, int nShards = 0, Handle* h = nullptr) {
+        DBSCAN m(eps, minPoints, maxPointsPerPartition);
+        const int64_t n = (int64_t)data.size();
+        std::vector<double> xs((size_t)n), ys((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            xs[(size_t)i] = data[(size_t)i].x();
+            ys[(size_t)i] = data[(size_t)i].y();
+        }
+        std::vector<int32_t> cl((size_t)n);
+        std::vector<uint8_t> fl((size_t)n);
+        int64_t k = 0;
+        if (dbscan_train_node(xs.data(), ys.data(), n, eps, minPoints, DBSCAN_MODE_NAIVE, nShards,
+                              cl.data(), fl.data(), &k) != DBSCAN_OK)
+            throw std::runtime_error(std::string("dbscan_train_node: ") + dbscan_last_error());
+        m.labeled_.reserve((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            DBSCANLabeledPoint lp(data[(size_t)i]);
+            lp.cluster = cl[(size_t)i];
+            lp.flag = static_cast<Flag>(fl[(size_t)i]);
+            lp.visited = true;
+            m.labeled_.push_back(std::move(lp));
+        }
+        m.nClusters_ = k;
+        std::unique_ptr<Handle> own;
+        if (!h) {
+            own.reset(new Handle(0));
+            h = own.get();
+        }
+        std::vector<double> rects;
+        std::vector<int64_t> counts;
+        int64_t cap = 0, np = 0;
+        do {  // the return value is the full partition count: grow and call again if needed
+            cap = np > cap ? np : (cap ? cap : 256);
+            rects.assign((size_t)cap * 4, 0.0);
+            counts.assign((size_t)cap, 0);
+            np = dbscan_partition(h->get(), xs.data(), ys.data(), n, eps, maxPointsPerPartition,
+                                  rects.data(), counts.data(), cap);
+            if (np < 0)
+                throw std::runtime_error(std::string("dbscan_partition: ") + dbscan_last_error());
+        } while (np > cap);
+        for (int64_t i = 0; i < np; ++i)
+            m.partitions_.push_back({(int)i, DBSCANRectangle{rects[(size_t)(4 * i)],
+                                                             rects[(size_t)(4 * i + 1)],
+                                                             rects[(size_t)(4 * i + 2)],
+                                                             rects[(size_t)(4 * i + 3)]}});
+        return m;
+    }
+    const std::vector<DBSCANLabeledPoint>& labeledPoints() const { return labeled_; }
+    const std::vector<std::pair<int, DBSCANRectangle>>& partitions() const { return partitions_; }
+    int64_t numClusters() const { return nClusters_; }
+    double minimumRectangleSize() const { return 2 * eps; }  // DBSCAN.scala:289
+    DBSCANLabeledPoint predict(const std::vector<double>&) const {  // DBSCAN.scala:300-302
+        throw std::logic_error("DBSCAN.predict is not implemented (as in the reference)");
+    }
+    const double eps;
+    const int minPoints;
+    const int maxPointsPerPartition;
+
+   private:
+    DBSCAN(double e, int mp, int mpp) : eps(e), minPoints(mp), maxPointsPerPartition(mpp) {}
+    std::vector<DBSCANLabeledPoint> labeled_;
+    std::vector<std::pair<int, DBSCANRectangle>> partitions_;
+    int64_t nClusters_ = 0;
 };
 
 }  // namespace dbscan

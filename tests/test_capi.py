@@ -98,8 +98,11 @@ def test_cpp_mirror_compiles_against_the_library(tmp_path):
     """include/dbscan_local.hpp (the C++ host mirror of the reference interface) compiles and
     links against libdbscan_hip.so with plain g++ (no HIP headers needed by callers)."""
     src = tmp_path / "t.cpp"
-    src.write_text('#include "dbscan_local.hpp"\nint main(){ dbscan::LocalDBSCANNaive f(0.3, 10);'
-                   ' (void)f; return dbscan_version() == 100 ? 0 : 1; }\n')
+    src.write_text('#include "dbscan_local.hpp"\nint main(int argc, char**){'
+                   ' dbscan::LocalDBSCANNaive f(0.3, 10); (void)f;'
+                   ' if (argc > 5) { std::vector<dbscan::DBSCANPoint> v;'
+                   ' auto m = dbscan::DBSCAN::train(v, 0.3, 10, 250); return (int)m.numClusters(); }'
+                   ' return dbscan_version() == 100 ? 0 : 1; }\n')
     exe = tmp_path / "t"
     libdir = os.path.dirname(_lib.LIB_PATH)
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o",

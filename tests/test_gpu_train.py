@@ -1,0 +1,95 @@
+"""DBSCAN.train(data, eps, minPoints, maxPointsPerPartition) -- the reference's whole-job API
+(DBSCAN.scala:40-48) -- in its Python and C++ mirrors, on the GPU.  Mirrors DBSCANSuite."dbscan"
+(DBSCANSuite.scala:30-60): the csv with eps = 0.3F, minPoints = 10, maxPointsPerPartition = 250;
+labels equal the csv's up to permutation (the suite itself maps ids through `corresponding`),
+and the partitions equal the reference's EvenSplitPartitioner list."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import EPS_03F, ROOT, gen_blobs
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dbscan_suite_labeled_csv(labeled_data):
+    import dbscan_amd
+
+    x, y, lab = labeled_data
+    vectors = [[a, b, c] for a, b, c in zip(x, y, lab)]  # Vectors.dense(line.split(','))
+    model = dbscan_amd.DBSCAN.train(vectors, eps=EPS_03F, minPoints=10, maxPointsPerPartition=250)
+    pts = model.labeledPoints
+    assert len(pts) == len(vectors) and [p.vector for p in pts] == [tuple(v) for v in vectors]
+    pairs = {(p.cluster, int(v[2])) for p, v in zip(pts, vectors)}
+    assert len(pairs) == 4 and len({a for a, _ in pairs}) == 4 and (0, 0) in pairs  # bijection
+    assert sum(p.flag == dbscan_amd.Flag.Core for p in pts) == 677
+    assert sum(p.flag == dbscan_amd.Flag.Noise for p in pts) == 18
+    rects, counts = O.ref_partition(x, y, EPS_03F, 250)
+    assert [i for i, _ in model.partitions] == [0, 1, 2, 3]
+    assert [tuple(r) for _, r in model.partitions] == [tuple(map(float, r)) for r in rects]
+    assert model.minimumRectangleSize == 2 * EPS_03F
+    with pytest.raises(NotImplementedError):
+        model.predict([0.0, 0.0])
+
+
+@pytest.mark.parametrize("shards", [0, 3])
+def test_train_numpy_blobs_equals_one_fit(shards):
+    import dbscan_amd
+
+    x, y = gen_blobs(300_000, noise=0.2, seed=31)
+    model = dbscan_amd.DBSCAN.train(np.stack([x, y], 1), 2.55, 10, 8192, n_shards=shards)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
+    assert model.n_clusters == rk
+    np.testing.assert_array_equal(model.cluster, rc)
+    np.testing.assert_array_equal(model.flag, rf)
+    rects, _ = O.ref_partition(x, y, 2.55, 8192)
+    np.testing.assert_array_equal(np.array([tuple(r) for _, r in model.partitions]), rects)
+    with pytest.raises(IndexError):
+        dbscan_amd.DBSCAN.train(np.zeros((5, 1)), 1.0, 2, 10)
+
+
+def test_cpp_train_mirror(tmp_path, labeled_data):
+    """include/dbscan_local.hpp's dbscan::DBSCAN::train (g++ only, linked to libdbscan_hip.so)
+    on the csv: labels equal the Python mirror's, partitions the reference's."""
+    from dbscan_amd import _lib
+
+    x, y, lab = labeled_data
+    data = tmp_path / "pts.txt"
+    np.savetxt(data, np.stack([x, y], 1), fmt="%.17g")
+    src = tmp_path / "train.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <fstream>
+#include "dbscan_local.hpp"
+int main(int argc, char** argv) {
+    std::ifstream in(argv[1]);
+    std::vector<dbscan::DBSCANPoint> pts;
+    double a, b;
+    while (in >> a >> b) pts.emplace_back(std::vector<double>{a, b});
+    auto m = dbscan::DBSCAN::train(pts, (double)0.3f, 10, 250);
+    for (const auto& p : m.labeledPoints()) std::printf("%d %d\n", p.cluster, (int)p.flag);
+    for (const auto& pr : m.partitions())
+        std::printf("P %d %.17g %.17g %.17g %.17g\n", pr.first, pr.second.x, pr.second.y,
+                    pr.second.x2, pr.second.y2);
+    return 0;
+}
+''')
+    exe = tmp_path / "train"
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(exe), "-L", libdir, "-ldbscan_hip", f"-Wl,-rpath,{libdir}"],
+                   check=True)
+    out = subprocess.run([str(exe), str(data)], check=True, capture_output=True,
+                         text=True).stdout.split("\n")
+    lab_lines = [l.split() for l in out if l and not l.startswith("P")]
+    cl = np.array([int(a) for a, _ in lab_lines])
+    fl = np.array([int(b) for _, b in lab_lines])
+    rc, rf, _ = O.fit_sequential(x, y, EPS_03F, 10, 0)
+    np.testing.assert_array_equal(cl, rc)
+    np.testing.assert_array_equal(fl, rf)
+    parts = [tuple(map(float, l.split()[2:])) for l in out if l.startswith("P")]
+    rects, _ = O.ref_partition(x, y, EPS_03F, 250)
+    assert parts == [tuple(map(float, r)) for r in rects]
