@@ -14,8 +14,9 @@ Workloads (BASELINE.json configs, SURVEY.md §8d generator G(n, noise, dense, se
          union-find + relabel; per-GPU work fixed (weak scaling).
 A step is one pass of the hot path over the resident points (HBM in -> labels in HBM): `value`.
 `end_to_end` times host SoA -> host labels on the same data (PCIe included; N = 1:
-dbscan_fit_h, N > 1: H2D of the global arrays, slab selection, the node step, D2H of the
-owned labels); it is reported beside `value`, never as it.
+dbscan_fit_h; N > 1: each rank's H2D of its 1/N chunk of the input, an all_to_all routing the
+points to their slabs, the node step, an all_to_all returning the labels to the chunk owners,
+D2H); it is reported beside `value`, never as it.
 
 roofline: the dominant kernel of the timed region, timed with HIP events on the library's own
 stream, carried on the kernels' own dispatch packets (hipExtLaunchKernelGGL: no idle gaps);
@@ -393,26 +394,44 @@ def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x
         py = torch.empty(n_total, dtype=torch.float64, pin_memory=True)
         px.numpy()[:] = hx
         py.numpy()[:] = hy
-        for tag, ax, ay in (("pageable", hx, hy), ("pinned", px.numpy(), py.numpy())):
+        # output arrays allocated and touched once, reused by every step (a JNI caller's Java
+        # arrays are resident); "fresh_outputs" allocates them per call (np.zeros: the copy back
+        # then faults in 50 MB of new pages)
+        ocl = np.zeros(n_total, np.int32)
+        ofl = np.zeros(n_total, np.uint8)
+        ocl[:] = 1
+        ofl[:] = 1
+        for tag, ax, ay, fresh in (("pageable", hx, hy, False), ("pinned", px.numpy(), py.numpy(),
+                                   False), ("fresh_outputs", hx, hy, True)):
             ts = []
             for i in range(args.e2e_steps + 1):
                 t0 = time.perf_counter()
-                dbscan_amd.fit_arrays(ax, ay, args.eps, args.min_points, 0, handle=h)
+                if fresh:
+                    dbscan_amd.fit_arrays(ax, ay, args.eps, args.min_points, 0, handle=h)
+                else:
+                    dbscan_amd.fit_arrays(ax, ay, args.eps, args.min_points, 0, handle=h,
+                                          cluster_out=ocl, flag_out=ofl)
                 if i:
                     ts.append(time.perf_counter() - t0)
             t = float(np.median(ts))
             out[tag] = {"value": round(n_total / t, 1), "ms_per_step": round(t * 1e3, 3)}
         out["value"] = out["pageable"]["value"]
-        out["path"] = ("dbscan_fit_h: host x,y (16 B/point) -> H2D -> fit -> D2H cluster,flag "
-                       "(5 B/point), synchronous; value = the pageable-memory rate")
+        out["path"] = ("dbscan_fit_h: host x,y (16 B/point, pageable) -> H2D -> fit -> D2H "
+                       "cluster,flag (5 B/point) into resident caller arrays, synchronous")
         return out
     from dbscan_amd import node
 
     xa, ya = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
-    hx, hy = xa.cpu().numpy(), ya.cpu().numpy()
+    comm = node.Comm(dist)
+    bounds = node.NodeJob.chunk_bounds(n_total, comm.world)
+    c0, c1 = bounds[comm.rank], bounds[comm.rank + 1]
+    # this rank's chunk of the global input in host memory (pageable, as a caller's arrays),
+    # and resident host output arrays for its labels
+    hx, hy = xa[c0:c1].cpu().numpy(), ya[c0:c1].cpu().numpy()
     del xa, ya
     torch.cuda.empty_cache()
-    comm = node.Comm(dist)
+    ocl = np.ones(c1 - c0, np.int32)
+    ofl = np.ones(c1 - c0, np.uint8)
     ops = node.HipSlabOps(h)
     ts = []
     for i in range(args.e2e_steps + 1):
@@ -422,11 +441,13 @@ def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x
         t0 = time.perf_counter()
         tx = torch.from_numpy(hx).cuda()
         ty = torch.from_numpy(hy).cuda()
-        job = node.NodeJob.from_global(tx, ty, args.eps, args.min_points, 0, comm, ops)
+        job = node.NodeJob.from_chunk(tx, ty, c0, n_total, args.eps, args.min_points, 0, comm,
+                                      ops)
         del tx, ty
         job.run()
-        gid, cl, fl = job.owned()
-        gid, cl, fl = gid.cpu(), cl.cpu(), fl.cpu()
+        cl, fl = job.chunk_labels(c0, c1 - c0, bounds)
+        torch.from_numpy(ocl).copy_(cl)
+        torch.from_numpy(ofl).copy_(fl)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -437,8 +458,11 @@ def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x
     ops.close()
     t = float(np.median(ts))
     out.update({"value": round(n_total / t, 1), "ms_per_step": round(t * 1e3, 3),
-                "path": ("each rank: H2D of the global host arrays (pageable), slab selection "
-                         "on its GPU, the node step, D2H of its owned labels; max over ranks")})
+                "path": ("each rank: H2D of its 1/N chunk of the host input (pageable), one "
+                         "all_to_all routing every point to the slabs holding it (cuts from an "
+                         "all-gathered sample), the node step, one all_to_all returning the "
+                         "labels to the chunk owners, D2H into resident host arrays; max over "
+                         "ranks")})
     return out
 
 

@@ -86,15 +86,21 @@ def default_handle(device: int = 0) -> _lib.Handle:
 
 
 def fit_arrays(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
-               handle: Optional[_lib.Handle] = None) -> Tuple[np.ndarray, np.ndarray, int]:
-    """Fit host arrays (input order = visit order). Returns (cluster int32, flag uint8, k)."""
+               handle: Optional[_lib.Handle] = None, cluster_out: Optional[np.ndarray] = None,
+               flag_out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Fit host arrays (input order = visit order). Returns (cluster int32, flag uint8, k).
+    cluster_out / flag_out: caller-owned output arrays to fill (reused across calls, as a JNI
+    caller's Java arrays are: no fresh pages to fault in during the copy back)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.ascontiguousarray(y, dtype=np.float64)
     if x.shape != y.shape or x.ndim != 1:
         raise ValueError("x and y must be 1-D arrays of equal length")
     n = x.size
-    cl = np.zeros(n, np.int32)
-    fl = np.zeros(n, np.uint8)
+    cl = cluster_out if cluster_out is not None else np.zeros(n, np.int32)
+    fl = flag_out if flag_out is not None else np.zeros(n, np.uint8)
+    if cl.dtype != np.int32 or fl.dtype != np.uint8 or cl.shape != (n,) or fl.shape != (n,) \
+            or not (cl.flags.c_contiguous and fl.flags.c_contiguous):
+        raise ValueError("cluster_out / flag_out: contiguous int32[n] / uint8[n]")
     k = ctypes.c_int32(0)
     h = handle or default_handle()
     _lib.check(_lib.load().dbscan_fit_h(

@@ -144,6 +144,23 @@ class Comm:
             return t
         return self.allgather_fixed(t, self.sizes(t.shape[-1]))
 
+    def alltoall_rows(self, t: torch.Tensor, send_counts: List[int]) -> torch.Tensor:
+        """t: rows grouped by destination rank (send_counts[d] rows to rank d).  Returns the
+        rows every rank sent here, in source-rank order: one all_to_all_single of the counts,
+        one of the rows (RCCL over xGMI for 'nccl')."""
+        if self.world == 1:
+            return t
+        dev = t.device
+        cdev = "cpu" if self.host else t.device
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=cdev)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc)
+        rcounts = [int(v) for v in rc.cpu().tolist()]
+        tt = t.cpu() if self.host else t.contiguous()
+        out = torch.empty((sum(rcounts),) + tuple(t.shape[1:]), dtype=t.dtype, device=tt.device)
+        self.dist.all_to_all_single(out, tt, rcounts, list(send_counts))
+        return out.to(dev)
+
     def allgather_fixed(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
         """allgather_varlen when every rank's length is already known (no size exchange)."""
         if self.world == 1:
@@ -326,6 +343,68 @@ class NodeJob:
                   comm, ops, x_all.numel())
         job.cuts = cuts
         return job
+
+    @staticmethod
+    def chunk_bounds(n_total: int, world: int) -> List[int]:
+        """Rank r's contiguous chunk of the global input is [b[r], b[r+1])."""
+        return [r * n_total // world for r in range(world + 1)]
+
+    @classmethod
+    def from_chunk(cls, x, y, start: int, n_total: int, eps, min_points, mode, comm: Comm, ops,
+                   sample: int = 1 << 20) -> "NodeJob":
+        """Host-to-slab path: each rank holds only the contiguous chunk [start, start + len(x))
+        of the global input (global visit order), e.g. just copied from host memory.  The cuts
+        come from an all-gathered sample of every chunk; every point goes to the ranks whose
+        zones 0/1/2 hold it in ONE all_to_all of 24-B records (x, y bits, gid/zone/shared),
+        so a rank receives its slab in ascending gid (segments in source-rank order, each
+        ascending): the same slab from_global selects, without any rank holding all points."""
+        world = comm.world
+        m = x.numel()
+        dev = x.device
+        xf = x[torch.isfinite(x)]
+        per = max(1, sample // world)
+        smp = xf[::max(1, xf.numel() // per)][:per].contiguous()
+        allx = comm.allgather_varlen(smp)
+        cuts = make_cuts(allx, world, eps, sample=max(1, allx.numel()))
+        gid = torch.arange(start, start + m, dtype=torch.int64, device=dev)
+        xb, yb = x.contiguous().view(torch.int64), y.contiguous().view(torch.int64)
+        recs, counts = [], []
+        for d in range(world):
+            if cuts:
+                z, sh = zones(x, d, cuts, eps)
+            else:  # unshardable eps: everything on rank 0
+                z = torch.full(x.shape, OUT if d else 0, dtype=torch.uint8, device=dev)
+                sh = torch.zeros(x.shape, dtype=torch.bool, device=dev)
+            idx = torch.nonzero(z != OUT).flatten()
+            code = gid[idx] * 8 + z[idx].long() * 2 + sh[idx].long()
+            recs.append(torch.stack([xb[idx], yb[idx], code], 1))
+            counts.append(int(idx.numel()))
+        recv = comm.alltoall_rows(torch.cat(recs), counts)
+        code = recv[:, 2].contiguous()
+        job = cls(recv[:, 0].contiguous().view(torch.float64),
+                  recv[:, 1].contiguous().view(torch.float64),
+                  ((code >> 1) & 3).to(torch.uint8), code >> 3, (code & 1) != 0, eps,
+                  min_points, mode, comm, ops, n_total)
+        job.cuts = cuts
+        return job
+
+    def chunk_labels(self, start: int, m: int, bounds: List[int]):
+        """The labels of the chunk [start, start + m) this rank holds, in input order: every
+        rank sends its owned (gid, cluster, flag) to the chunk owner (one all_to_all), which
+        scatters them into place.  Returns (cluster int32[m], flag uint8[m]) on the device."""
+        gid, cl, fl = self.owned()
+        dev = gid.device
+        b = torch.tensor(bounds[1:-1], dtype=torch.int64, device=dev)
+        dest = torch.searchsorted(b, gid, right=True)
+        counts = torch.bincount(dest, minlength=self.comm.world).cpu().tolist()
+        rec = torch.stack([gid, (cl.to(torch.int64) << 8) | fl.to(torch.int64)], 1)
+        recv = self.comm.alltoall_rows(rec, counts)
+        loc = recv[:, 0] - start
+        out_cl = torch.zeros(m, dtype=torch.int32, device=dev)
+        out_fl = torch.zeros(m, dtype=torch.uint8, device=dev)
+        out_cl[loc] = (recv[:, 1] >> 8).to(torch.int32)
+        out_fl[loc] = (recv[:, 1] & 255).to(torch.uint8)
+        return out_cl, out_fl
 
     @classmethod
     def synthetic(cls, n_total, noise, dense, seed, eps, min_points, handle, dist,

@@ -91,7 +91,22 @@ def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
         x, y = x.cuda(), y.cuda()
     else:
         ops = OracleSlabOps()
-    job = node.NodeJob.from_global(x, y, eps, min_points, mode, node.Comm(dist), ops)
+    comm = node.Comm(dist)
+    if os.environ.get("NODE_WORKER_CHUNKS") == "1":  # host-to-slab path: this rank's chunk only
+        bounds = node.NodeJob.chunk_bounds(x.numel(), world)
+        c0, c1 = bounds[rank], bounds[rank + 1]
+        job = node.NodeJob.from_chunk(x[c0:c1], y[c0:c1], c0, x.numel(), eps, min_points, mode,
+                                      comm, ops)
+        k = job.run()
+        cl, fl = job.chunk_labels(c0, c1 - c0, bounds)
+        k2 = job.run()
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), gid=np.arange(c0, c1),
+                 cluster=cl.cpu().numpy(), flag=fl.cpu().numpy(), k=np.array([k, k2]),
+                 n_slab=np.array([job.x.numel()]), cuts=np.array(job.cuts, dtype=np.float64))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    job = node.NodeJob.from_global(x, y, eps, min_points, mode, comm, ops)
     k = job.run()
     k2 = job.run()  # a second step on the same handle must give the same answer
     g, c, f = (t.cpu().numpy() for t in job.owned())

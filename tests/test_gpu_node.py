@@ -24,6 +24,21 @@ def test_gpu_node_equals_single_fit(tmp_path, world, mode, n):
     assert ks == {rk}
 
 
+@pytest.mark.parametrize("world,mode", [(2, 0), (3, 1)])
+def test_gpu_node_chunks_equals_single_fit(tmp_path, world, mode):
+    """Host-to-slab path with the HIP slab kernels: each rank starts from its chunk of the input,
+    all_to_all routes points to slabs and labels back (gloo between ranks on the one GPU)."""
+    n = 500_000
+    x, y = gen_blobs(n, noise=0.2, seed=n + world + 5)
+    cl, fl, seen, ks, parts = run_ranks(tmp_path, x, y, world, 2.55, 10, mode, use_gpu=True,
+                                        timeout=600, chunks=True)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, mode)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+
+
 def test_gpu_node_single_rank(tmp_path):
     x, y = gen_blobs(300_000, noise=0.1, seed=77)
     cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, 2.55, 10, 0, use_gpu=True)

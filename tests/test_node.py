@@ -27,11 +27,13 @@ def _free_port():
     return p
 
 
-def run_ranks(tmp_path, x, y, world, eps, min_points, mode, use_gpu=False, timeout=300):
+def run_ranks(tmp_path, x, y, world, eps, min_points, mode, use_gpu=False, timeout=300,
+              chunks=False):
     data = tmp_path / "data.npz"
     np.savez(data, x=x, y=y)
     port = _free_port()
     env = dict(os.environ)
+    env["NODE_WORKER_CHUNKS"] = "1" if chunks else "0"
     env.setdefault("OMP_NUM_THREADS", "2")
     procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(world), str(port), str(data),
                                str(tmp_path), repr(float(eps)), str(min_points), str(mode),
@@ -149,3 +151,20 @@ def test_merge_double_components():
     assert par[40] == -1 and par[0] == -1
     ops.merge_reset(a, b, par)
     assert bool((par == -1).all())
+
+
+@pytest.mark.parametrize("world,mode,bad", [(2, 0, 0), (3, 1, 12), (4, 0, 0)])
+def test_node_chunks_all_to_all_equals_single_fit(tmp_path, world, mode, bad):
+    """Host-to-slab path (NodeJob.from_chunk + chunk_labels): each rank starts from its chunk of
+    the input only; one all_to_all routes points to their slabs, one routes the labels back to
+    the chunk owners.  The chunks' labels, concatenated, equal one fit of the whole set."""
+    n = 30_000
+    x, y = _data(n, seed=world * 3 + mode, bad=bad)
+    eps = 60.0 * np.sqrt(n / 1e6)
+    cl, fl, seen, ks, parts = run_ranks(tmp_path, x, y, world, eps, 10, mode, chunks=True)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, eps, 10, mode)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+    assert max(int(pt["n_slab"][0]) for pt in parts) < 0.8 * n
