@@ -568,9 +568,16 @@ int32_t dbscan_csv_write(const char* path, const double* x, const double* y,
 
 int32_t dbscan_format_double(double v, char* buf) {
     if (!buf) return DBSCAN_EARG;
-    const int k = dbscan::java_double_string_c(v, buf);
-    buf[k] = 0;
-    return k;
+    return dbscan::jdk8_double_string(v, buf);
+}
+
+int64_t dbscan_scala_range_count(double start, double end, double step, int32_t inclusive) {
+    int64_t r = DBSCAN_EARG;
+    const int32_t rc = guarded(nullptr, [&]() -> int32_t {
+        r = dbscan::scala_range_count(start, end, step, inclusive != 0);
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? r : rc;
 }
 
 int32_t dbscan_slab_fit_device(dbscan_handle* h, const double* d_x, const double* d_y,

@@ -6,11 +6,10 @@
 //           but never read); each field parsed as java.lang.Double.parseDouble
 //   output  DBSCANSample.scala:35
 //             labeledPoints.map(p => s"${p.x},${p.y},${p.cluster}")
-//           with java.lang.Double.toString for x and y.
+//           with java.lang.Double.toString for x and y, as the reference's runtime (JDK 7/8)
+//           prints it (jdk8_double_string, javanum.hip).
 // Files are memory-mapped and parsed by host threads over newline-aligned byte ranges (count,
-// then parse at the counted offsets).  Double.toString's digits are the shortest that round
-// trip (the JDK >= 19 algorithm; JDK 8 occasionally printed one more digit): the text output is
-// parity unpinned at that level, the values are exact.
+// then parse at the counted offsets).
 #include "../../include/dbscan_hip.h"
 #include "internal.h"
 
@@ -74,72 +73,6 @@ bool parse_java_double(const char* b, const char* e, double* out) {
     }
     *out = neg ? -v : v;
     return true;
-}
-
-// java.lang.Double.toString (JDK 19+ digit selection): shortest round-trip digits; plain
-// notation for 1e-3 <= |d| < 1e7 (at least one fractional digit), else d.dddE[-]n.
-int java_double_string(double d, char* buf) {
-    if (std::isnan(d)) return sprintf(buf, "NaN");
-    if (std::isinf(d)) return sprintf(buf, d > 0 ? "Infinity" : "-Infinity");
-    char* p = buf;
-    if (std::signbit(d)) {
-        *p++ = '-';
-        d = -d;
-    }
-    if (d == 0) {
-        memcpy(p, "0.0", 3);
-        return (int)(p - buf) + 3;
-    }
-    char sci[64];
-    const auto r = std::to_chars(sci, sci + sizeof(sci), d, std::chars_format::scientific);
-    *r.ptr = 0;
-    // sci = D[.DDD]e[+-]XX
-    char digits[32];
-    int nd = 0;
-    const char* q = sci;
-    for (; *q && *q != 'e'; ++q)
-        if (*q != '.') digits[nd++] = *q;
-    int exp10 = atoi(q + 1);
-    while (nd > 1 && digits[nd - 1] == '0') --nd;
-    if (nd == 1) {
-        // Double.toString (JDK 19+): when one digit suffices, the closest decimal of length 1
-        // or 2 that still rounds to d (so 4.9E-324, not 5.0E-324)
-        char two[64];
-        snprintf(two, sizeof(two), "%.1e", d);  // correctly rounded to 2 digits
-        if (strtod(two, nullptr) == d) {
-            nd = 0;
-            for (q = two; *q && *q != 'e'; ++q)
-                if (*q != '.') digits[nd++] = *q;
-            exp10 = atoi(q + 1);
-            while (nd > 1 && digits[nd - 1] == '0') --nd;
-        }
-    }
-    if (d >= 1e-3 && d < 1e7) {
-        if (exp10 >= 0) {
-            for (int i = 0; i <= exp10; ++i) *p++ = i < nd ? digits[i] : '0';
-            *p++ = '.';
-            if (nd > exp10 + 1) {
-                for (int i = exp10 + 1; i < nd; ++i) *p++ = digits[i];
-            } else {
-                *p++ = '0';
-            }
-        } else {
-            *p++ = '0';
-            *p++ = '.';
-            for (int i = 0; i < -exp10 - 1; ++i) *p++ = '0';
-            for (int i = 0; i < nd; ++i) *p++ = digits[i];
-        }
-    } else {
-        *p++ = digits[0];
-        *p++ = '.';
-        if (nd > 1) {
-            for (int i = 1; i < nd; ++i) *p++ = digits[i];
-        } else {
-            *p++ = '0';
-        }
-        p += sprintf(p, "E%d", exp10);
-    }
-    return (int)(p - buf);
 }
 
 struct Mapped {
@@ -275,16 +208,14 @@ void csv_write(const char* path, const double* x, const double* y, const int32_t
             used = 0;
         }
         char* p = buf.data() + used;
-        p += java_double_string(x[i], p);
+        p += jdk8_double_string(x[i], p);
         *p++ = ',';
-        p += java_double_string(y[i], p);
+        p += jdk8_double_string(y[i], p);
         p += sprintf(p, ",%d\n", cluster[i]);
         used = (size_t)(p - buf.data());
     }
     const bool ok = fwrite(buf.data(), 1, used, fp) == used;
     if (fclose(fp) != 0 || !ok) throw ArgError{std::string("write failed: ") + path};
 }
-
-int java_double_string_c(double d, char* buf) { return java_double_string(d, buf); }
 
 }  // namespace dbscan

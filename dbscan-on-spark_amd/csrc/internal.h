@@ -259,7 +259,10 @@ int64_t split_partitions(double mrs, int64_t imin, int64_t jmin, int64_t W, int6
 int64_t csv_read(const char* path, double* x_out, double* y_out, int64_t capacity);
 void csv_write(const char* path, const double* x, const double* y, const int32_t* cluster,
                int64_t n);
-int java_double_string_c(double d, char* buf);
+// javanum.hip: java.lang.Double.toString as JDK 7/8 print it (NUL-terminated, returns the
+// length) and Scala 2.10's NumericRange.count for Double ranges
+int jdk8_double_string(double d, char* buf);
+int64_t scala_range_count(double start, double end, double step, bool inclusive);
 
 // Whole-node fit in one process (node.hip): n_shards slabs over the visible GPUs.
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,

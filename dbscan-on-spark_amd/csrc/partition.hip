@@ -159,15 +159,11 @@ private:
     std::vector<int64_t> sat_;
 };
 
-// Number of elements of the Scala 2.10 Double range `start until end by step` (a NumericRange
-// whose length comes from an exact quotient; elements by repeated addition from start).
+// Number of elements of the Scala 2.10 Double range `start until end by step`
+// (EvenSplitPartitioner.scala:150-152): NumericRange.count, restated exactly in javanum.hip;
+// the elements themselves come by repeated addition from start (NumericRange.foreach).
 int64_t range_len(double start, double end, double step) {
-    if (start == end || (start < end) != (step > 0)) return 0;
-    const long double q = ((long double)end - (long double)start) / (long double)step;
-    const int64_t jumps = (int64_t)q;
-    const long double rem =
-        ((long double)end - (long double)start) - (long double)jumps * (long double)step;
-    return jumps + (rem == 0.0L ? 0 : 1);
+    return scala_range_count(start, end, step, false);
 }
 
 // EvenSplitPartitioner.split (:105-123) + complement (:128-143).  Candidates along one axis:

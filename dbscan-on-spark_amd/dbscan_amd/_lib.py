@@ -48,6 +48,7 @@ SIGNATURES = [
     ("dbscan_csv_read", _i64, [ctypes.c_char_p, _vp, _vp, _i64]),
     ("dbscan_csv_write", _i32, [ctypes.c_char_p, _vp, _vp, _vp, _i64]),
     ("dbscan_format_double", _i32, [_d, ctypes.c_char_p]),
+    ("dbscan_scala_range_count", _i64, [_d, _d, _d, _i32]),
     ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),

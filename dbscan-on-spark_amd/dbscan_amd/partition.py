@@ -59,6 +59,17 @@ def _collect(call, max_parts: int = 1 << 12) -> List[Tuple[DBSCANRectangle, int]
         max_parts = k
 
 
+def scala_range_count(start: float, end: float, step: float, inclusive: bool = False) -> int:
+    """Element count of the Scala 2.10 Double range `start until end by step` (`to` if
+    inclusive): NumericRange.count with DoubleAsIfIntegral, as the EvenSplitPartitioner's
+    candidate splits use it (EvenSplitPartitioner.scala:150-152; csrc/javanum.hip)."""
+    r = _lib.load().dbscan_scala_range_count(float(start), float(end), float(step),
+                                             1 if inclusive else 0)
+    if r < 0:
+        raise ValueError(_lib.load().dbscan_last_error().decode())
+    return int(r)
+
+
 class EvenSplitPartitioner:
     """EvenSplitPartitioner.partition(toSplit, maxPointsPerPartition, minimumRectangleSize)
     (EvenSplitPartitioner.scala:28-35): toSplit is a set of (grid cell, count)."""

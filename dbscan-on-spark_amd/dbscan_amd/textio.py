@@ -4,7 +4,8 @@
                                     textFile(path).map(s => Vectors.dense(s.split(',')
                                     .map(_.toDouble))) -> x = field 0, y = field 1
   write_csv(path, x, y, cluster)    DBSCANSample.scala:35: s"${p.x},${p.y},${p.cluster}"
-  format_double(v)                  java.lang.Double.toString (shortest round-trip digits)
+  format_double(v)                  java.lang.Double.toString as JDK 7/8 print it (the reference's
+                                    runtime; sun.misc.FloatingDecimal's digits)
 """
 from __future__ import annotations
 

@@ -168,12 +168,21 @@ int64_t dbscan_partition_cells(const double* cell_x, const double* cell_y,
  *   otherwise fills up to `capacity` records and returns the count; a malformed record is
  *   DBSCAN_EARG naming its 1-based line.  Memory-mapped, parsed by host threads.
  * dbscan_csv_write: the output of DBSCANSample.scala:35, "x,y,cluster" per point with x and y
- *   in java.lang.Double.toString form (dbscan_format_double; buf >= 32 bytes, returns the
- *   length): shortest round-trip digits, plain for 1e-3 <= |v| < 1e7, else d.dddE[-]n. */
+ *   in java.lang.Double.toString form as the reference's runtime prints it (Spark 2.1.0 on JDK
+ *   7/8, pom.xml:30-37): sun.misc.FloatingDecimal's digits (dbscan_format_double; buf >= 32
+ *   bytes, returns the length) -- usually the shortest round-trip digits, but e.g.
+ *   2.82879384806159E17 prints as 2.82879384806159008E17; plain for 1e-3 <= |v| < 1e7, else
+ *   d.dddE[-]n.
+ * dbscan_scala_range_count: the element count of the Scala 2.10 Double range
+ *   `start until end by step` (inclusive != 0: `to`), NumericRange.count with
+ *   Numeric.DoubleAsIfIntegral (BigDecimal(Double.toString) quot/rem at DECIMAL128): the
+ *   EvenSplitPartitioner's candidate splits (EvenSplitPartitioner.scala:150-152).  Negative on
+ *   the reference's exceptions (step 0, more than Int.MaxValue elements). */
 int64_t dbscan_csv_read(const char* path, double* x_out, double* y_out, int64_t capacity);
 int32_t dbscan_csv_write(const char* path, const double* x, const double* y,
                          const int32_t* cluster, int64_t n);
 int32_t dbscan_format_double(double v, char* buf);
+int64_t dbscan_scala_range_count(double start, double end, double step, int32_t inclusive);
 
 /* Whole-node entry: DBSCAN.train(points, eps, minPoints, ...).labeledPoints
  * (DBSCAN.scala:91-283) for one node, from host arrays, in ONE process.  The points are cut

@@ -43,6 +43,50 @@ def build() -> str:
     return LIB_PATH
 
 
+def scala_range_count(start: float, end: float, step: float, inclusive: bool = False) -> int:
+    """Scala 2.10 NumericRange.count(start, end, step, isInclusive) for Double ranges
+    (`start until end by step`, EvenSplitPartitioner.scala:150-152), restated with Python's
+    decimal module: diff = end - start in double arithmetic; quot = (BigDecimal(diff) /
+    BigDecimal(step)) at DECIMAL128 (34 digits, HALF_EVEN), doubleValue, toLong; rem =
+    BigDecimal remainder (zero iff the decimals divide exactly); BigDecimal(d) is the decimal
+    of Double.toString(d), taken here as the shortest round-trip digits (repr) -- JDK 7/8
+    print longer digits for ~0.3% of doubles (csrc/javanum.hip has that form)."""
+    import decimal
+    from fractions import Fraction
+
+    if step == 0.0:
+        raise ValueError("step cannot be 0.")
+    if start == end:
+        return 1 if inclusive else 0
+    if (start < end) != (step > 0.0):
+        return 0
+    start, end, step = float(start), float(end), float(step)
+    diff = end - start
+    d, s = decimal.Decimal(repr(diff)), decimal.Decimal(repr(step))
+    ctx = decimal.Context(prec=34, rounding=decimal.ROUND_HALF_EVEN)
+    q = float(ctx.divide(d, s))  # float(Decimal) is correctly rounded
+    jumps = int(q) if q == q else 0
+    exact = (Fraction(d) / Fraction(s)).denominator == 1
+    count = jumps + (0 if (not inclusive and exact) else 1)
+    if count > 2 ** 31 - 1 or count < 0:
+        raise ValueError("seqs cannot contain more than Int.MaxValue elements.")
+    return count
+
+
+_RANGE_COUNT_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double)
+
+
+def _range_count_py(a, b, c):
+    try:
+        return scala_range_count(a, b, c)
+    except ValueError:
+        return -1
+
+
+_range_count_cb = _RANGE_COUNT_FN(_range_count_py)
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
@@ -73,6 +117,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_slab_label.argtypes = [dp, dp, vp, i64, ctypes.c_double, vp, vp, vp, vp, vp,
                                         i32, vp, vp]
         L.oracle_slab_label.restype = i32
+        L.oracle_set_range_count.argtypes = [_RANGE_COUNT_FN]
+        L.oracle_set_range_count.restype = None
+        L.oracle_set_range_count(_range_count_cb)
         _lib = L
     return _lib
 

@@ -96,15 +96,17 @@ static int64_t points_in(const grid_t* g, rect_t r) {
     return g->sat[b1 * w + a1] - g->sat[b0 * w + a1] - g->sat[b1 * w + a0] + g->sat[b0 * w + a0];
 }
 
-/* Scala 2.10 `(start until end by step)` over Doubles (EvenSplitPartitioner.scala:150-152). */
+/* Scala 2.10 `(start until end by step)` over Doubles (EvenSplitPartitioner.scala:150-152):
+ * NumericRange.count with Numeric.DoubleAsIfIntegral -- BigDecimal(Double.toString(_)) quot
+ * and rem at DECIMAL128.  Decimal arithmetic is done on the Python side of the oracle (the
+ * `decimal` module: oracle.py scala_range_count) and handed in as a callback, so this
+ * restatement shares no code with the product's (csrc/javanum.hip). */
+typedef int64_t (*range_count_fn)(double start, double end, double step);
+static range_count_fn g_range_count = NULL;
+void oracle_set_range_count(range_count_fn fn) { g_range_count = fn; }
+
 static int64_t range_count(double start, double end, double step) {
-    if (start == end) return 0;
-    if ((start < end) != (step > 0)) return 0;
-    double diff = end - start;
-    long double q = (long double)diff / (long double)step;
-    int64_t jumps = (int64_t)q;
-    long double rem = (long double)diff - (long double)jumps * (long double)step;
-    return jumps + (rem == 0.0L ? 0 : 1);
+    return g_range_count ? g_range_count(start, end, step) : -1;
 }
 
 typedef struct { rect_t r; int64_t c; } rc_t;

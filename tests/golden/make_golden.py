@@ -12,6 +12,11 @@
   (d2 = eps2 +- ulps), duplicates, NaN/inf, eps <= 0, tiny/huge scales, minPoints <= 1,
   and visit-order effects, with the sequential oracle's outputs.  Floats are stored as
   float.hex() strings so they round-trip bit-exactly.
+* jvm_printed_doubles.txt -- every decimal number printed in the reference's source comments
+  (debug output of the author's JVM run, e.g. DBSCAN.scala:73-101's vectors and
+  DBSCANRectangle corners, EvenSplitPartitioner.scala:186-197), one per line with its file:line:
+  java.lang.Double.toString outputs of the reference's runtime, so format_double must print
+  each parsed value back as the same string.  Needs /root/reference (generation only).
 """
 from __future__ import annotations
 
@@ -131,8 +136,31 @@ def cases():
     return out
 
 
+def jvm_printed_doubles():
+    import re
+
+    src = "/root/reference/src/main/scala/org/apache/spark/mllib/clustering/dbscan"
+    seen, out = set(), []
+    for name in sorted(os.listdir(src)):
+        with open(os.path.join(src, name)) as f:
+            for ln, line in enumerate(f, 1):
+                if "//" not in line or "licen" in line.lower():
+                    continue
+                for m in re.finditer(r"(?<![\w.])-?\d+\.\d+(?:E-?\d+)?", line.split("//", 1)[1]):
+                    v = m.group(0)
+                    if v not in seen:
+                        seen.add(v)
+                        out.append(f"{v} {name}:{ln}")
+    with open(os.path.join(HERE, "jvm_printed_doubles.txt"), "w") as f:
+        f.write("# Double.toString outputs printed in the reference's comments (value file:line)\n")
+        f.write("\n".join(out) + "\n")
+    print(f"wrote {len(out)} JVM-printed doubles")
+
+
 def main():
     O.build()
+    if os.path.isdir("/root/reference"):
+        jvm_printed_doubles()
     # labeled_data expected outputs
     x, y, lab = O.load_labeled_csv(os.path.join(HERE, "labeled_data.csv"))
     cn, fn, _ = O.fit_sequential(x, y, EPS_03F, 10, O.NAIVE)

@@ -74,3 +74,79 @@ def test_large_file_parallel_parse(tmp_path):
     rx, ry = read_csv(p)
     np.testing.assert_array_equal(rx, x)
     np.testing.assert_array_equal(ry, y)
+
+
+# ------------------------- JDK 7/8 digits and Scala 2.10 ranges ---------------------------
+@pytest.mark.parametrize("v,s", [
+    # the JDK 19 release note for JDK-4511638: "Double.toString(2e23) now returns 2.0E23,
+    # whereas in earlier releases it returns 1.9999999999999998E23"
+    (2e23, "1.9999999999999998E23"),
+    # the same symmetric-stopping-test path (FloatingDecimal's long branch)
+    (1e23, "9.999999999999999E22"), (8.41e21, "8.409999999999999E21"),
+    # the integer fast path keeps the digits above the half-ulp's "insignificant" ones
+    (2.82879384806159e17, "2.82879384806159008E17"), (2.0 ** 62, "4.6116860184273879E18"),
+    (2.0 ** 63, "9.223372036854776E18"), (1e17, "1.0E17"), (123456789012345680.0,
+                                                              "1.2345678901234568E17")])
+def test_jdk8_double_to_string_digits(v, s):
+    """Spark 2.1.0 / Scala 2.10 run on JDK 7/8 (pom.xml:30-37), whose Double.toString
+    (sun.misc.FloatingDecimal) prints more than the shortest digits for some values."""
+    assert format_double(v) == s
+
+
+def test_jvm_printed_doubles_from_reference_comments():
+    """Every number the reference's own JVM printed into its source comments (golden data,
+    tests/golden/jvm_printed_doubles.txt) is printed back identically."""
+    vals = [l.split()[0] for l in open(f"{GOLDEN}/jvm_printed_doubles.txt") if l[0] != "#"]
+    assert len(vals) > 50
+    for s in vals:
+        assert format_double(float(s)) == s, s
+
+
+def test_jdk8_digits_round_trip_and_only_lengthen():
+    """On random bit patterns: the printed value parses back to the same double, and the JDK
+    7/8 digits are never shorter than the shortest round-trip digits (they equal them for all
+    but a fraction of a percent of doubles)."""
+    rng = np.random.default_rng(5)
+    bits = rng.integers(0, 2 ** 63, 40_000, dtype=np.int64).view(np.float64)
+    longer = 0
+    for v in bits:
+        if not np.isfinite(v):
+            continue
+        s = format_double(float(v))
+        assert float(s) == v
+        sig = lambda t: len(t.lstrip("-").split("E")[0].split("e")[0].replace(".", "").strip("0"))  # noqa
+        assert sig(s) >= sig(repr(float(v)))
+        longer += sig(s) > sig(repr(float(v)))
+    assert longer < 0.01 * bits.size
+
+
+@pytest.mark.parametrize("start,end,step,n", [
+    (0.0, 0.9, 0.3, 3),   # decimal 0.9 / 0.3 = 3 exactly; exact binary division gives 3.0000..4 -> 4
+    (0.0, 0.3, 0.1, 3), (0.6, 2.4, 0.6, 3), (1.0, 1.0, 0.5, 0), (2.0, 1.0, 0.5, 0),
+    (-2.4, 2.4, 0.6000000238418579, 8), (0.1, 0.7, 0.2, 3)])
+def test_scala_double_range_count_known(start, end, step, n):
+    from dbscan_amd.partition import scala_range_count
+
+    assert scala_range_count(start, end, step) == n == O.scala_range_count(start, end, step)
+
+
+def test_scala_double_range_count_vs_oracle():
+    """The product's NumericRange.count (csrc/javanum.hip: bigint decimal division) against
+    the oracle's (Python decimal module) on grid-like and random ranges, until and to."""
+    from dbscan_amd.partition import scala_range_count
+
+    rng = np.random.default_rng(11)
+    for _ in range(3000):
+        mrs = float(2 * rng.choice([0.3, float(np.float32(0.3)), 2.55, 0.001, 1.7, 1e-5]))
+        a, b = sorted(rng.integers(-5000, 5000, 2).tolist())
+        start, end = a * mrs + mrs, b * mrs + rng.choice([0.0, mrs * 1e-9, -mrs * 1e-12])
+        for inc in (False, True):
+            if start == end or (start < end) != (mrs > 0):
+                continue
+            assert scala_range_count(start, end, mrs, inc) == O.scala_range_count(start, end, mrs,
+                                                                                  inc)
+    for _ in range(2000):
+        start, end = rng.normal(size=2) * 10.0 ** rng.integers(-3, 4, 2)
+        step = abs(rng.normal()) * 10.0 ** rng.integers(-3, 1)
+        if end > start and (end - start) / step < 1e6:
+            assert scala_range_count(start, end, step) == O.scala_range_count(start, end, step)
