@@ -87,7 +87,9 @@ def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
 
         torch.cuda.set_device(0)
         h = dbscan_amd.Handle(0)
-        ops = node.HipSlabOps(h)
+        # NODE_WORKER_SHARE_STREAM=0: the handle keeps its own stream (event-ordered)
+        ops = node.HipSlabOps(h, share_stream=os.environ.get("NODE_WORKER_SHARE_STREAM",
+                                                             "1") == "1")
         x, y = x.cuda(), y.cuda()
     else:
         ops = OracleSlabOps()

@@ -1,6 +1,8 @@
 """Node path with the real HIP slab kernels: 2-3 ranks on the one GPU of the test box, gloo
 for the exchange (RCCL needs one GPU per rank; the collectives are the same calls).  The
 union of the ranks' owned labels must equal one fit of the whole data set, bit for bit."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -37,6 +39,60 @@ def test_gpu_node_chunks_equals_single_fit(tmp_path, world, mode):
     np.testing.assert_array_equal(fl, rf)
     np.testing.assert_array_equal(cl, rc)
     assert ks == {rk}
+
+
+@pytest.mark.parametrize("env", [{"DBSCAN_NODE_COMM_STREAM": "1"},
+                                 {"NODE_WORKER_SHARE_STREAM": "0"}],
+                         ids=["comm_stream", "own_stream"])
+def test_gpu_node_stream_variants(tmp_path, env):
+    """The node step's optional stream arrangements: the roots' gather and sort on a stream of
+    their own (DBSCAN_NODE_COMM_STREAM=1), and the handle on its own stream ordered by events
+    (share_stream=False): both bit-exact against one fit."""
+    n = 300_000
+    x, y = gen_blobs(n, noise=0.2, seed=17)
+    cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 2, 2.55, 10, 0, use_gpu=True, timeout=600,
+                                    env_extra=env)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+
+
+def test_set_stream_bind_and_restore():
+    """dbscan_set_stream: a fit on a caller's torch stream, back on the handle's own stream
+    (own = 1), both equal to the oracle; destroying a handle bound to the null stream."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import _lib
+    from dbscan_amd import device as D
+
+    L = _lib.load()
+    x, y = gen_blobs(200_000, noise=0.1, seed=23)
+    ref = O.fit_grid(x, y, 2.55, 10, 0)
+    tx, ty = torch.tensor(x, device="cuda"), torch.tensor(y, device="cuda")
+    h = dbscan_amd.Handle(0)
+    s = torch.cuda.Stream()
+    _lib.check(L.dbscan_set_stream(h.ptr, ctypes.c_void_p(s.cuda_stream), 0))
+    assert h.stream == s.cuda_stream
+    with torch.cuda.stream(s):
+        cl, fl, k = D.fit_tensors(tx, ty, 2.55, 10, 0, h)
+    s.synchronize()
+    assert k == ref[2]
+    np.testing.assert_array_equal(cl.cpu().numpy(), ref[0])
+    _lib.check(L.dbscan_set_stream(h.ptr, None, 1))  # back to the handle's own stream
+    assert h.stream not in (0, s.cuda_stream)
+    cl2, fl2, k2 = D.fit_tensors(tx, ty, 2.55, 10, 0, h)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cl2.cpu().numpy(), ref[0])
+    np.testing.assert_array_equal(fl2.cpu().numpy(), ref[1])
+    h2 = dbscan_amd.Handle(0)
+    _lib.check(L.dbscan_set_stream(h2.ptr, None, 0))  # the null stream
+    D.fit_tensors_async(tx, ty, 2.55, 10, 0, h2, torch.empty_like(cl), torch.empty_like(fl),
+                        None)
+    h2.close()  # waits for the fit on the null stream before freeing its buffers
+    h.close()
 
 
 def test_gpu_node_single_rank(tmp_path):

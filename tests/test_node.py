@@ -28,12 +28,13 @@ def _free_port():
 
 
 def run_ranks(tmp_path, x, y, world, eps, min_points, mode, use_gpu=False, timeout=300,
-              chunks=False):
+              chunks=False, env_extra=None):
     data = tmp_path / "data.npz"
     np.savez(data, x=x, y=y)
     port = _free_port()
     env = dict(os.environ)
     env["NODE_WORKER_CHUNKS"] = "1" if chunks else "0"
+    env.update(env_extra or {})
     env.setdefault("OMP_NUM_THREADS", "2")
     procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(world), str(port), str(data),
                                str(tmp_path), repr(float(eps)), str(min_points), str(mode),
