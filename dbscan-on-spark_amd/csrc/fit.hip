@@ -2824,6 +2824,11 @@ static constexpr int union_w() { return DBSCAN_AB_UNION_W; }
 static constexpr int count_cap() { return DBSCAN_AB_COUNT_CAP; }
 static constexpr bool f32_count() { return DBSCAN_AB_F32 != 0; }
 static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
+// DBSCAN_AB_CAP32: staging capacity of count_tile32 (tiles over it take the big-tile path)
+#ifndef DBSCAN_AB_CAP32
+#define DBSCAN_AB_CAP32 1536
+#endif
+constexpr int kCap32 = DBSCAN_AB_CAP32;
 
 // Archery float32 box, after the rank scan: the one-way core-core pairs decide which component
 // a cluster's expansion claims beyond its own.  Usually there are none (returns nullptr: the
@@ -3045,7 +3050,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz);
             DBSCAN_HIP_CHECK(hipGetLastError());
             if (f32)  // clique grids: small / medium / big tile lists
-                klaunch(prof, "tile_class", tile_class_kernel<1536>,
+                klaunch(prof, "tile_class", tile_class_kernel<kCap32>,
                         dim3((unsigned)std::min<int64_t>(
                             (ntile_bound + kBlock * kClassRounds - 1) / (kBlock * kClassRounds),
                             1024)),
@@ -3092,7 +3097,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         0, s, xy, tstart, tstage, eps2, a.min_points, core, parent,
                         block_cores + 3 * tile_grid, nbr, nbr_k, fa);
                 auto k32 =
-                    union_w() == 5 ? count_tile32_kernel<1536, 5> : count_tile32_kernel<1536, 6>;
+                    union_w() == 5 ? count_tile32_kernel<kCap32, 5> : count_tile32_kernel<kCap32, 6>;
                 klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
                         tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
                         block_cores, nbr, nbr_k, count_ablate(), fa);
