@@ -147,6 +147,19 @@ def load_pmc(stage, n_points, stamp):
     return e, d.get("source")
 
 
+def _limiter(pmc):
+    """What actually bounds the roofline kernel, from its SQ counters (the contract's `bound`
+    names the ceiling it is priced against): the waves' cycle split."""
+    sq = (pmc or {}).get("sq") or {}
+    wc = sq.get("SQ_WAVE_CYCLES")
+    if not wc:
+        return None
+    parked, stalled = sq.get("SQ_WAIT_ANY", 0) / wc, sq.get("SQ_WAIT_INST_ANY", 0) / wc
+    kind = "latency" if parked > 0.5 else ("issue" if stalled > 0.3 else "mixed")
+    return (f"{kind}: {parked:.0%} of wave cycles parked on waitcnt/barriers, {stalled:.0%} "
+            f"issue-stalled, {sq.get('SQ_ACTIVE_INST_ANY', 0) / wc:.0%} issuing (SQ counters)")
+
+
 def cpu_baseline(x, y, eps, min_points, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -294,6 +307,7 @@ def main():
                 "traffic_source": pmc_src,
                 "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
                 "alg_bytes_per_point": ALG_BYTES.get(dom, 0), "points_per_launch": unit_pts,
+                "limiter": _limiter(pmc),
                 "pipeline_frac": round(PIPELINE_ALG_BYTES * pts / (ms_per_step * 1e-3) / 1e9
                                        / HBM_PEAK_GBS, 5)}
         if pmc and pmc.get("valu_insts_per_launch"):
