@@ -1378,6 +1378,8 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
         const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
         return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
     };
+    __shared__ int s_first;  // smallest local quarter holding a core
+    if (i == 0) s_first = 0x7FFFFFFF;
     u.qmap[i] = 0xFFFF;
     u.cmin[i] = ~0ull;
     lds_barrier();
@@ -1410,6 +1412,7 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
             rep = b + first;
             best = fa.perm[rep];
         }
+        if (rep >= 0) atomicMin(&s_first, i);
         fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
         u.lp[i] = i;
         u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) | (uint32_t)jb |
@@ -1420,6 +1423,12 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
     lds_barrier();
     if (ablate != 3) {
         for (int sweep = 0; sweep < 2; ++sweep) {
+            if (sweep == 1) {  // the adjacent pairs joined every core of the tile: no
+                               // distance-2 pair can add an edge inside it
+                const int f = s_first;
+                const bool split = i < nq && (u.lrange[i] >> 31) && lfind(u.lp, i) != lfind(u.lp, f);
+                if (!__syncthreads_or(split)) break;
+            }
             const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
             for (int k = i; k < nq * nofs; k += kBlock) {
                 const int o = k / nq, qi = k - o * nq;
