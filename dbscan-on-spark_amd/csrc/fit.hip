@@ -61,6 +61,32 @@ constexpr int kMaxNbr = 11;  // neighbour lists of non-cores kept while minPoint
 constexpr int32_t kModeArcheryBox = 2;     // DBSCAN_MODE_ARCHERY_F32BOX
 constexpr int64_t kBoxEdgeCap = 1 << 22;   // one-way core-core pairs a box fit can hold
 
+// DBSCAN_AB_STAMPS (timing builds only, never the shipped library): the per-tile kernels' wave 0
+// records the constant-rate clock (100 MHz) at its phase boundaries, per workgroup, read back by
+// dbscan_ab_stamps() (tools/stamps_probe.py).
+#ifndef DBSCAN_AB_STAMPS
+#define DBSCAN_AB_STAMPS 0
+#endif
+#if DBSCAN_AB_STAMPS
+constexpr int kStamps = 12;  // slots per workgroup: 0..9 clock, 10..11 tile sizes
+__device__ long long g_ab_stamps[kTileGrid * kStamps];
+#define AB_STAMP(k)                                                                     \
+    do {                                                                                \
+        if (threadIdx.x == 0) g_ab_stamps[blockIdx.x * kStamps + (k)] = wall_clock64(); \
+    } while (0)
+#define AB_NOTE(k, v)                                                        \
+    do {                                                                     \
+        if (threadIdx.x == 0) g_ab_stamps[blockIdx.x * kStamps + (k)] = (v); \
+    } while (0)
+#else
+#define AB_STAMP(k) \
+    do {            \
+    } while (0)
+#define AB_NOTE(k, v) \
+    do {              \
+    } while (0)
+#endif
+
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
 // two rounded multiplies, one rounded add, <=.  The whole library is built with
 // -ffp-contract=off; the pragma pins it here as well.
@@ -1421,6 +1447,7 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
         u.qmap[lq] = (uint16_t)i;
     }
     lds_barrier();
+    AB_STAMP(5);
     if (ablate != 3) {
         for (int sweep = 0; sweep < 2; ++sweep) {
             if (sweep == 1) {  // the adjacent pairs joined every core of the tile: no
@@ -1449,6 +1476,7 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
                     lunite(u.lp, qi, j);
             }
             lds_barrier();
+            AB_STAMP(6 + sweep);
         }
     }
     int r = -1;
@@ -1457,6 +1485,7 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
         atomicMin(&u.cmin[r], ((unsigned long long)(uint32_t)best << 32) | (uint32_t)rep);
     }
     lds_barrier();
+    AB_STAMP(8);
     if (i < nq) {
         const int crep = r >= 0 ? (int)(uint32_t)(u.cmin[r] & 0xFFFFFFFFull) : -1;
         fa.qg[q0 + i] = make_int4(gx, gy, best, 0);
@@ -1497,12 +1526,15 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
     const auto tile_at = [&](int k) { return k < nt ? fa.tl.medium[k] : ntiles; };
     StageMeta meta = stage_meta(tile_at(blockIdx.x), ntiles, tstage, tstart, fa.tq);
     for (int k = blockIdx.x; k < nt; k += gridDim.x) {
+        AB_STAMP(0);
         const int t = tile_at(k);
         if (threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
         const uint32_t tk = fa.tkey[t];
         const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
         const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
         stage_build32<CAP>(meta, xy, st, buf, g, ox, oy);
+        AB_STAMP(1);
+        AB_NOTE(10, st.total);
         meta = stage_meta(tile_at(k + gridDim.x), ntiles, tstage, tstart, fa.tq);
         const int q0 = st.q0, nq = st.nq;
         int qb = 0, qe = 0;
@@ -1522,7 +1554,9 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                 rowoff[8] = acc;
             }
             __syncthreads();
+            AB_STAMP(2);
             const int own = rowoff[8];
+            AB_NOTE(11, own);
             for (int i = (int)threadIdx.x; i < own; i += kBlock) {
                 int r = 0;
 #pragma unroll
@@ -1586,11 +1620,14 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
             }
+            AB_STAMP(3);
             __syncthreads();
+            AB_STAMP(4);
             fused_tile_union32(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
                                *reinterpret_cast<UnionLds*>(lsts), ablate);
         }
         __syncthreads();
+        AB_STAMP(9);
     }
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
     if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
@@ -3385,3 +3422,18 @@ void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const S
 }
 
 }  // namespace dbscan
+
+#if DBSCAN_AB_STAMPS
+// Timing builds: out = NULL clears the stamps; else copies n <= kTileGrid * kStamps of them.
+extern "C" int dbscan_ab_stamps(long long* out, int n) {
+    using namespace dbscan;
+    const size_t bytes = sizeof(long long) * (size_t)kTileGrid * kStamps;
+    if (!out) {
+        std::vector<long long> z((size_t)kTileGrid * kStamps, 0);
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_ab_stamps), z.data(), bytes) == hipSuccess ? 0 : -1;
+    }
+    const size_t want = sizeof(long long) * (size_t)n;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ab_stamps), want < bytes ? want : bytes) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
