@@ -298,7 +298,7 @@ def main():
         avg_ms = prof[dom]["ms"] / max(1, prof[dom]["launches"])  # live, in the timed region
         pts = stats.get("n", args.points_per_gpu)
         unit_pts = stats.get(CLASS_PTS[dom], pts) if dom in CLASS_PTS else pts
-        alg = ALG_BYTES.get(dom, 0) * unit_pts  # per launch
+        alg = ALG_BYTES.get(dom.split("<")[0], 0) * unit_pts  # per launch
         achieved = alg / (avg_ms * 1e-3) / 1e9
         pmc, pmc_src = load_pmc(dom, pts, src_stamp()) if not node_path else (None, "node path")
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -306,7 +306,8 @@ def main():
                 "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
                 "traffic_source": pmc_src,
                 "kernel": dom, "avg_launch_ms": round(avg_ms, 4),
-                "alg_bytes_per_point": ALG_BYTES.get(dom, 0), "points_per_launch": unit_pts,
+                "alg_bytes_per_point": ALG_BYTES.get(dom.split("<")[0], 0),
+                "points_per_launch": unit_pts,
                 "limiter": _limiter(pmc),
                 "pipeline_frac": round(PIPELINE_ALG_BYTES * pts / (ms_per_step * 1e-3) / 1e9
                                        / HBM_PEAK_GBS, 5)}

@@ -1391,6 +1391,49 @@ __device__ __forceinline__ bool quarters_touch32(const float2* __restrict__ buf,
     return false;
 }
 
+// The 4 adjacent (backward) quarter pairs of core quarter qi, from qi's own lane: the four
+// lookups, and the tests of each pair's first cores, are issued together; a pair whose first
+// cores are not a sure hit takes the full quarters_touch32 test.  lp/lrange/lmask/qmap: the
+// tile's LDS union-find and quarter records (UnionLds / WaveUnion).
+template <class CoreF, class ExactF>
+__device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange,
+                                                 const uint32_t* lmask, const uint16_t* qmap,
+                                                 int qi, const float2* __restrict__ buf,
+                                                 CoreF is_core, F32Cut cut, ExactF exact) {
+    constexpr int kDx[4] = {-1, 0, 1, -1}, kDy[4] = {-1, -1, -1, 0};
+    const uint32_t ri = lrange[qi], am = lmask[qi];
+    const int lq = (int)((ri >> 22) & 255u);
+    const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
+    int jn[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int ux = (lq & 15) + kDx[o], uy = (lq >> 4) + kDy[o];
+        jn[o] = (ux >= 0 && ux <= 15 && uy >= 0) ? (int)qmap[uy * 16 + ux] : 0xFFFF;
+    }
+    uint32_t rj[4], mj[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int jj = jn[o] == 0xFFFF ? qi : jn[o];
+        rj[o] = jn[o] == 0xFFFF ? 0u : lrange[jj];
+        mj[o] = lmask[jj];
+    }
+    const float2 pa = buf[ab + (am ? __ffs(am) - 1 : 0)];
+    bool t[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const float2 pb = buf[(int)(rj[o] & 2047u) + (mj[o] ? __ffs(mj[o]) - 1 : 0)];
+        t[o] = (rj[o] >> 31) && am && mj[o] && f32_d2(pa, pb) <= cut.lo;
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        if ((rj[o] >> 31) && !t[o]) {
+            const int bb = (int)(rj[o] & 2047u), be = bb + (int)((rj[o] >> 11) & 2047u);
+            t[o] = quarters_touch32(buf, ab, ae, am, bb, be, mj[o], is_core, cut, exact);
+        }
+        if (t[o]) lunite(lp, qi, jn[o]);
+    }
+}
+
 // fused_tile_union over the float2 stage (see fused_tile_union for the structure)
 __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
                                    const GridParams& g, const TileStage& st,
@@ -1449,26 +1492,28 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
     lds_barrier();
     AB_STAMP(5);
     if (ablate != 3) {
-        for (int sweep = 0; sweep < 2; ++sweep) {
-            if (sweep == 1) {  // the adjacent pairs joined every core of the tile: no
-                               // distance-2 pair can add an edge inside it
-                const int f = s_first;
-                const bool split = i < nq && (u.lrange[i] >> 31) && lfind(u.lp, i) != lfind(u.lp, f);
-                if (!__syncthreads_or(split)) break;
-            }
-            const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
-            for (int k = i; k < nq * nofs; k += kBlock) {
+        // adjacent quarters (the 4 backward offsets) from each core quarter's own thread
+        if (i < nq && rep >= 0)
+            unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, i, buf, is_core, cut, exact);
+        lds_barrier();
+        AB_STAMP(6);
+        // the adjacent pairs joined every core of the tile: no distance-2 pair can add an edge
+        // inside it
+        const int f = s_first;
+        const bool split = i < nq && rep >= 0 && lfind(u.lp, i) != lfind(u.lp, f);
+        if (__syncthreads_or(split)) {
+            for (int k = i; k < nq * 8; k += kBlock) {
                 const int o = k / nq, qi = k - o * nq;
                 const uint32_t ri = u.lrange[qi];
                 if (!(ri >> 31)) continue;
                 const int lq = (int)((ri >> 22) & 255u);
-                const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+                const int ux = (lq & 15) + kRingDx[4 + o], uy = (lq >> 4) + kRingDy[4 + o];
                 if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
                 const int j = u.qmap[uy * 16 + ux];
                 if (j == 0xFFFF) continue;
                 const uint32_t rj = u.lrange[j];
                 if (!(rj >> 31)) continue;
-                if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                if (lfind(u.lp, qi) == lfind(u.lp, j)) continue;
                 const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
                 const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
                 if (quarters_touch32(buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, cut,
@@ -1476,8 +1521,8 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
                     lunite(u.lp, qi, j);
             }
             lds_barrier();
-            AB_STAMP(6 + sweep);
         }
+        AB_STAMP(7);
     }
     int r = -1;
     if (i < nq && rep >= 0) {
@@ -1848,28 +1893,47 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                 const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
                 return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
             };
-            for (int sweep = 0; sweep < 2; ++sweep) {
-                const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
-                for (int it = lane; it < nq * nofs; it += 64) {
+            for (int qi = lane; qi < nq; qi += 64)
+                if (u.lrange[qi] >> 31)
+                    unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, qi, T.buf, is_core_l, cut,
+                                     exact2);
+            wave_sync();
+            // the adjacent pairs joined every core of the tile: no distance-2 pair can add an
+            // edge inside it
+            int f = 0x7FFFFFFF;
+#pragma unroll
+            for (int pp = kWaveQ / 64 - 1; pp >= 0; --pp)
+                if (lane + pp * 64 < nq && rep[pp] >= 0) f = lane + pp * 64;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, 64));
+            bool split = false;
+#pragma unroll
+            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
+                const int qi = lane + pp * 64;
+                if (qi < nq && rep[pp] >= 0 && lfind(u.lp, qi) != lfind(u.lp, f)) split = true;
+            }
+            if (__ballot(split)) {
+                wave_sync();
+                for (int it = lane; it < nq * 8; it += 64) {
                     const int o = it / nq, qi = it - o * nq;
                     const uint32_t ri = u.lrange[qi];
                     if (!(ri >> 31)) continue;
                     const int lq = (int)((ri >> 22) & 255u);
-                    const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+                    const int ux = (lq & 15) + kRingDx[4 + o], uy = (lq >> 4) + kRingDy[4 + o];
                     if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
                     const int j = u.qmap[uy * 16 + ux];
                     if (j == 0xFFFF) continue;
                     const uint32_t rj = u.lrange[j];
                     if (!(rj >> 31)) continue;
-                    if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                    if (lfind(u.lp, qi) == lfind(u.lp, j)) continue;
                     const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
                     const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
                     if (quarters_touch32(T.buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j],
                                          is_core_l, cut, exact2))
                         lunite(u.lp, qi, j);
                 }
-                wave_sync();
             }
+            wave_sync();
             int rr[kWaveQ / 64];
 #pragma unroll
             for (int pp = 0; pp < kWaveQ / 64; ++pp) {

@@ -599,22 +599,28 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
     int32_t* vpp = val2;
     const auto pass = [&](auto wtag, int shift) {
         constexpr int W = decltype(wtag)::value;
+        // profile names per template instance (the digit widths run differently)
+        const char* up = W == 8 ? "radix_upsweep<8>" : W == 9 ? "radix_upsweep<9>" : "radix_upsweep<7>";
+        const char* of = W == 8 ? "radix_offsets<8>" : W == 9 ? "radix_offsets<9>" : "radix_offsets<7>";
+        const char* dn = W == 8   ? "radix_downsweep<8>"
+                         : W == 9 ? "radix_downsweep<9>"
+                                  : "radix_downsweep<7>";
         {
             StageTimer st(prof, s, "sort_upsweep");
-            klaunch(prof, "radix_upsweep", radix_upsweep_kernel<W>, dim3((unsigned)nb),
+            klaunch(prof, up, radix_upsweep_kernel<W>, dim3((unsigned)nb),
                     dim3(kBlock), 0, s, kin, n, shift, bits_dev, nb, h);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
             StageTimer st(prof, s, "sort_scan");
             uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 512);
-            klaunch(prof, "radix_offsets", radix_offsets_kernel<W>, dim3(kOffBlocks),
+            klaunch(prof, of, radix_offsets_kernel<W>, dim3(kOffBlocks),
                     dim3(kOffThreads), 0, s, (const int32_t*)h, nb, ho, state, scan.epoch,
                     bits_dev, shift);
         }
         {
             StageTimer st(prof, s, "sort_downsweep");
-            klaunch(prof, "radix_downsweep", radix_downsweep_kernel<W>, dim3((unsigned)nb),
+            klaunch(prof, dn, radix_downsweep_kernel<W>, dim3((unsigned)nb),
                     dim3(kBlock), 0, s, kin, (first && iota) ? (const int32_t*)nullptr : vin, kpp,
                     vpp, key3, val3, n, shift, bits_dev, nb, ho, inv);
             DBSCAN_HIP_CHECK(hipGetLastError());

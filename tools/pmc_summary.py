@@ -13,8 +13,8 @@ Writes
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: rocprofv3 reports KB, and on gfx950
 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM); other
 access widths are uncalibrated there, so the figure is an estimate for gather-heavy kernels.
-A stage with several template instances (the radix passes) gets the launch-weighted average
-per launch, which is what bench.py's per-launch timing averages too.
+The radix passes are stages per template instance (radix_downsweep<8> ...), as the library's
+profile names are; a stage with several instances gets the launch-weighted average per launch.
 """
 import csv
 import glob
@@ -53,7 +53,11 @@ def stage_of(sym):
     base = sym.split("<")[0]
     if base in STAGE_OF:
         return STAGE_OF[base]
-    return base[:-len("_kernel")] if base.endswith("_kernel") else None
+    if not base.endswith("_kernel"):
+        return None
+    st = base[:-len("_kernel")]
+    # the radix passes are profiled per template instance (bench.py's names carry the width)
+    return st + sym[len(base):] if st.startswith("radix_") else st
 
 
 def main():
