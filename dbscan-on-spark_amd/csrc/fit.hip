@@ -903,17 +903,17 @@ __device__ __forceinline__ int lfind(int* lp, int x) {
         x = gp;
     }
 }
-__device__ __forceinline__ void lunite(int* lp, int a, int b) {
+__device__ __forceinline__ bool lunite(int* lp, int a, int b) {  // true: this call merged
     for (;;) {
         a = lfind(lp, a);
         b = lfind(lp, b);
-        if (a == b) return;
+        if (a == b) return false;
         if (a < b) {
             const int t = a;
             a = b;
             b = t;
         }
-        if (atomicCAS(&lp[a], a, b) == a) return;
+        if (atomicCAS(&lp[a], a, b) == a) return true;
     }
 }
 
@@ -2300,6 +2300,22 @@ __global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
 // global union-find sees about one operation per component pair per tile side.
 constexpr int kEdgeNodes = 72;
 
+// edge_union's full pair test (the reps were not within eps) and its global union.
+__device__ __forceinline__ bool edge_pair_full(const double2* __restrict__ xy, int4 me, int4 o,
+                                               const uint8_t* __restrict__ core, double eps2) {
+    const auto gcore = [core](int j) { return core[j] != 0; };
+    double px[kQReg], py[kQReg];
+    const int na = load_own(xy, me, 0, px, py);
+    return na >= 0 ? pair_found(px, py, na, xy, o.x, o.y, (uint32_t)o.w, gcore, 0, eps2)
+                   : pair_found_generic(xy, 0, me, o, gcore, eps2);
+}
+__device__ __forceinline__ void edge_unite(int32_t* __restrict__ parent,
+                                           const int32_t* __restrict__ perm, int ca, int cb) {
+    const int ra = uf_find(parent, ca);
+    const int rb = uf_find(parent, cb);
+    if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
+}
+
 template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ ntiles_p,
@@ -2319,7 +2335,6 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
-    const auto gcore = [core](int j) { return core[j] != 0; };
     // one (tile, side) per wave and loop trip: waves never wait for each other
     for (int tw = xcd_block() * (kBlock / 64) + w; tw < 2 * ntiles;
          tw += gridDim.x * (kBlock / 64)) {
@@ -2389,28 +2404,46 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             const int4 me = nqi[w][a];
             const int2 mg = ngq[w][a];
             if (me.z >= 0) {
-                double px[kQReg], py[kQReg];
-                const int na = load_own(xy, me, 0, px, py);
-                // only facing cells within quarter distance 2 along the strip
+                // only facing cells within quarter distance 2 along the strip: three cells, at
+                // most two of each cell's quarters per lane (two lanes per own quarter)
                 const int ua = (side ? mg.x : mg.y) & 15;
-                const int flo = (ua - 2) >> 1, fhi = (ua + 2) >> 1;
+                const int flo = (ua - 2) >> 1;
+                int sb[6], sd[6];
 #pragma unroll
-                for (int sweep = 1; sweep <= 2; ++sweep)
-                    for (int f = flo; f <= fhi; ++f)
-                    for (int b = fnb[w][f + 1] + half; b < fne[w][f + 1]; b += 2) {
+                for (int c = 0; c < 6; ++c) {
+                    const int f = flo + (c >> 1);
+                    const int b = fnb[w][f + 1] + half + 2 * (c & 1);
+                    sb[c] = -1;
+                    sd[c] = 0;
+                    if (b < fne[w][f + 1]) {
                         const int2 og = ngq[w][b];
-                        if (max(abs(og.x - mg.x), abs(og.y - mg.y)) != sweep) continue;
-                        const int4 o = nqi[w][b];
-                        if (o.z < 0) continue;
+                        const int d = max(abs(og.x - mg.x), abs(og.y - mg.y));
+                        if (d <= 2 && nqi[w][b].z >= 0) {
+                            sb[c] = b;
+                            sd[c] = d;
+                        }
+                    }
+                }
+                // each pair's first test: the two quarters' reps (cores), all loads in flight
+                // together; the full test only where the reps are not within eps
+                const double2 pr = xy[me.z];
+                double2 po[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c)
+                    po[c] = sb[c] >= 0 ? xy[nqi[w][sb[c]].z] : make_double2(0.0, 0.0);
+#pragma unroll 1
+                for (int sweep = 1; sweep <= 2; ++sweep)
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        if (sb[c] < 0 || sd[c] != sweep) continue;
+                        const int b = sb[c];
                         if (lfind(lp, a) == lfind(lp, b)) continue;
-                        const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
-                                                            (uint32_t)o.w, gcore, 0, eps2)
-                                               : pair_found_generic(xy, 0, me, o, gcore, eps2);
-                        if (!f) continue;
-                        lunite(lp, a, b);
-                        const int ra = uf_find(parent, ncomp[w][a]);
-                        const int rb = uf_find(parent, ncomp[w][b]);
-                        if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
+                        if (!within_eps(pr.x, pr.y, po[c].x, po[c].y, eps2) &&
+                            !edge_pair_full(xy, me, nqi[w][b], core, eps2))
+                            continue;
+                        // one global union per merge of two LDS sets: a lane that finds its
+                        // pair already joined (another lane's merge) leaves the global sets alone
+                        if (lunite(lp, a, b)) edge_unite(parent, perm, ncomp[w][a], ncomp[w][b]);
                     }
             }
         }

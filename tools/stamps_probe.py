@@ -19,6 +19,8 @@ K_STAMPS, K_GRID = 12, 8192
 PHASES = [("stage (meta + xy loads)", 0, 1), ("rowoff + barrier", 1, 2),
           ("count (wave 0)", 2, 3), ("count barrier", 3, 4), ("union init", 4, 5),
           ("sweep 0", 5, 6), ("sweep 1 + cmin", 6, 8), ("writes + barrier", 8, 9)]
+# KERNEL=edge: a build whose edge_union_kernel stamps instead (slots 0, 1, 2, 9; 10 = nodes)
+EDGE_PHASES = [("strip loads", 0, 1), ("pre-join", 1, 2), ("pair tests + unions", 2, 9)]
 
 
 def main():
@@ -43,14 +45,18 @@ def main():
     assert f(buf.ctypes.data, buf.size) == 0
     s = buf.reshape(K_GRID, K_STAMPS).astype(np.float64)
     live = s[(s[:, 0] > 0) & (s[:, 9] > 0)]
-    s7 = np.where(live[:, 7] > 0, live[:, 7], live[:, 6])
-    live[:, 7] = s7
+    phases = PHASES
+    if os.environ.get("KERNEL") == "edge":
+        phases = EDGE_PHASES
+    else:
+        s7 = np.where(live[:, 7] > 0, live[:, 7], live[:, 6])
+        live[:, 7] = s7
     print(f"tiles stamped: {len(live)}  staged points mean {live[:, 10].mean():.0f}, own mean "
           f"{live[:, 11].mean():.0f}")
     tot = (live[:, 9] - live[:, 0]) / 100.0
     print(f"per tile total: mean {tot.mean():.2f} us  p50 {np.median(tot):.2f}  p90 "
           f"{np.percentile(tot, 90):.2f}")
-    for name, a, b in PHASES:
+    for name, a, b in phases:
         d = (live[:, b] - live[:, a]) / 100.0
         print(f"  {name:26s} mean {d.mean():7.2f} us  p50 {np.median(d):7.2f}  p90 "
               f"{np.percentile(d, 90):7.2f}  share {d.sum() / ((live[:, 9] - live[:, 0]) / 100.0).sum():.2f}")
