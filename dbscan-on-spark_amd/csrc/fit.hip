@@ -519,11 +519,64 @@ __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restri
 enum TileClass { kTileSmall = 0, kTileMedium = 1, kTileBig = 2, kTileNone = 3 };
 constexpr int kSmallCap = 192;
 
+// The small and medium tiles are listed in buckets by stage size, the largest first: the
+// count kernels walk them in that order and workgroups are dispatched in index order, so the
+// longest tiles start first and the last ones dispatched are the shortest (a
+// longest-processing-time order, which shortens the kernels' tails), and the four waves of a
+// count_wave_kernel workgroup get tiles of about the same size.  Each bucket has its own list
+// of capacity cap and its own counter.  Measured (round 2, 10^7 points): four small buckets
+// took count_wave from 0.127 to 0.094 ms; eight medium buckets slowed count_tile32 (0.308 ->
+// 0.316-0.331 ms: within a bucket the tiles lose the list's spatial order), so the medium tiles
+// stay one list in tile order (DBSCAN_AB_MED_BUCKETS: A/B builds).  Small-tile buckets hold
+// stage sizes (kSmallEdge[b + 1], kSmallEdge[b]]; count_wave_kernel runs in instances by lanes
+// per tile (kWaveSplit: 64 lanes above kTinyCap, 32 up to it; with DBSCAN_AB_WAVE_SPLIT=2 also
+// 16 lanes up to 16 points).
+#ifndef DBSCAN_AB_MED_BUCKETS
+#define DBSCAN_AB_MED_BUCKETS 1
+#endif
+constexpr int kMedBuckets = DBSCAN_AB_MED_BUCKETS;
+constexpr int kSmallBuckets = 5;
+#ifndef DBSCAN_AB_WAVE_SPLIT
+#define DBSCAN_AB_WAVE_SPLIT 1
+#endif
+constexpr int kWaveSplit = DBSCAN_AB_WAVE_SPLIT;  // 0: one instance; 1: 64 | 32; 2: 64 | 32 | 16
+#if DBSCAN_AB_WAVE_SPLIT == 2
+__device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 128, 64, 32, 16, 0};
+constexpr int kTinyCap = 64;     // the 32-lane instance: stages in (16, 64]
+constexpr int kTinyBucket0 = 2;  // its first bucket
+#else
+__device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 144, 96, 64, 32, 0};
+constexpr int kTinyCap = 32;     // the 32-lane instance: stages up to 32
+constexpr int kTinyBucket0 = 4;
+#endif
+static_assert(kSmallBuckets + kMedBuckets <= 16, "kStTileBuckets holds 16 counters");
+
 struct TileLists {
-    int32_t* n;      // [3] list lengths (device)
-    int32_t* small;  // occupied tile indices per class
-    int32_t* medium;
-    int32_t* big;
+    int32_t* n;       // [3] list lengths (device): small, medium, big
+    int32_t* small;   // [kSmallBuckets][cap] occupied tile indices
+    int32_t* medium;  // [kMedBuckets][cap]
+    int32_t* big;     // [cap]
+    int32_t* sb;      // [kSmallBuckets] small bucket lengths (device)
+    int32_t* mb;      // [kMedBuckets] medium bucket lengths (device)
+    int32_t cap;      // capacity of each list
+};
+
+// Bucketed list position k of the size-descending order (pre: the buckets' exclusive prefix).
+template <int NB>
+struct BucketWalk {
+    int pre[NB + 1];
+    __device__ __forceinline__ BucketWalk(const int32_t* counts) {
+        pre[0] = 0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) pre[b + 1] = pre[b] + counts[b];
+    }
+    __device__ __forceinline__ int size() const { return pre[NB]; }
+    __device__ __forceinline__ int at(const int32_t* lists, int64_t cap, int k) const {
+        int b = 0;
+#pragma unroll
+        for (int j = 1; j < NB; ++j) b += k >= pre[j] ? 1 : 0;
+        return lists[(int64_t)b * cap + (k - pre[b])];
+    }
 };
 
 constexpr int kClassRounds = 4;  // tile_class_kernel: 64 tiles per lane round, 1024 per block
@@ -537,59 +590,82 @@ __global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __res
                                                             uint8_t* __restrict__ tclass,
                                                             int32_t* __restrict__ class_pts) {
     if (!gp->clique) return;
-    __shared__ int wcnt[3][kBlock / 64];
+    // categories: small bucket b (b = 0 the largest stages), big, medium bucket b
+    constexpr int kCatBig = kSmallBuckets, kCatMed = kSmallBuckets + 1;
+    constexpr int kCat = kCatMed + kMedBuckets;
+    __shared__ int wcnt[kCat][kBlock / 64];
     __shared__ int wpts[3][kBlock / 64];
-    __shared__ int bbase[3];
+    __shared__ int bbase[kCat];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ntiles = *ntiles_p;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (int base = blockIdx.x * kBlock * kClassRounds; base < ntiles;
          base += gridDim.x * kBlock * kClassRounds) {  // block-uniform loop
-        int v[kClassRounds];
-        int cnt[3] = {0, 0, 0}, pts[3] = {0, 0, 0};
+        int v[kClassRounds], cat[kClassRounds];
+        int pts[3] = {0, 0, 0};
 #pragma unroll
         for (int r = 0; r < kClassRounds; ++r) {  // tile = base + (r * 4 + w) * 64 + lane
             const int t = base + (r * (kBlock / 64) + w) * 64 + lane;
             v[r] = kTileNone;
+            cat[r] = -1;
             int own = 0;
             if (t < ntiles) {
                 const int c = tsz[t];
                 v[r] = c <= kSmallCap ? kTileSmall : (c <= CAP ? kTileMedium : kTileBig);
                 tclass[t] = (uint8_t)v[r];
                 own = tstart[t + 1] - tstart[t];
+                if (v[r] == kTileSmall) {
+                    cat[r] = 0;
+#pragma unroll
+                    for (int j = 1; j < kSmallBuckets; ++j) cat[r] += c <= kSmallEdge[j] ? 1 : 0;
+                }
+                else if (v[r] == kTileBig)
+                    cat[r] = kCatBig;
+                else
+                    cat[r] = kCatMed + (kMedBuckets - 1) -
+                             (int)((int64_t)(c - kSmallCap - 1) * kMedBuckets / (CAP - kSmallCap));
             }
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                cnt[k] += __popcll(__ballot(v[r] == k));
-                pts[k] += v[r] == k ? own : 0;
-            }
+            for (int k = 0; k < 3; ++k) pts[k] += v[r] == k ? own : 0;
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k)
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) pts[k] += __shfl_xor(pts[k], o, 64);
-        if (lane < 3) {
-            wcnt[lane][w] = lane == 0 ? cnt[0] : (lane == 1 ? cnt[1] : cnt[2]);
-            wpts[lane][w] = lane == 0 ? pts[0] : (lane == 1 ? pts[1] : pts[2]);
+#pragma unroll
+        for (int k = 0; k < kCat; ++k) {
+            int cnt = 0;
+#pragma unroll
+            for (int r = 0; r < kClassRounds; ++r) cnt += __popcll(__ballot(cat[r] == k));
+            if (lane == 0) wcnt[k][w] = cnt;
         }
+        if (lane < 3) wpts[lane][w] = lane == 0 ? pts[0] : (lane == 1 ? pts[1] : pts[2]);
         __syncthreads();
-        if (threadIdx.x < 3) {  // one atomic per class and workgroup
+        if (threadIdx.x < kCat) {  // one atomic per category and workgroup
             const int k = threadIdx.x;
             const int tot = wcnt[k][0] + wcnt[k][1] + wcnt[k][2] + wcnt[k][3];
-            bbase[k] = tot ? atomicAdd(&tl.n[k], tot) : 0;
+            int32_t* ctr = k < kCatBig ? &tl.sb[k] : (k == kCatBig ? &tl.n[kTileBig] : &tl.mb[k - kCatMed]);
+            bbase[k] = tot ? atomicAdd(ctr, tot) : 0;
+            if (k != kCatBig && tot) atomicAdd(&tl.n[k < kCatBig ? kTileSmall : kTileMedium], tot);
+        }
+        if (threadIdx.x < 3) {
+            const int k = threadIdx.x;
             const int p = wpts[k][0] + wpts[k][1] + wpts[k][2] + wpts[k][3];
             if (p) atomicAdd(&class_pts[k], p);
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < kCat; ++k) {
             int at = bbase[k];
             for (int q = 0; q < w; ++q) at += wcnt[k][q];
-            int32_t* list = k == 0 ? tl.small : (k == 1 ? tl.medium : tl.big);
+            int32_t* list = k < kCatBig ? tl.small + (int64_t)k * tl.cap
+                                        : (k == kCatBig ? tl.big
+                                                        : tl.medium + (int64_t)(k - kCatMed) * tl.cap);
 #pragma unroll
             for (int r = 0; r < kClassRounds; ++r) {
-                const uint64_t m = __ballot(v[r] == k);
-                if (v[r] == k) list[at + __popcll(m & lt)] = base + (r * (kBlock / 64) + w) * 64 + lane;
+                const uint64_t m = __ballot(cat[r] == k);
+                if (cat[r] == k)
+                    list[at + __popcll(m & lt)] = base + (r * (kBlock / 64) + w) * 64 + lane;
                 at += __popcll(m);
             }
         }
@@ -1567,8 +1643,9 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
     const F32Cut cut = f32_cut(g, eps2);
     int mine = 0;
     // the medium tiles (tile_class_kernel): each fits the staging capacity
-    const int nt = fa.tl.n[kTileMedium];
-    const auto tile_at = [&](int k) { return k < nt ? fa.tl.medium[k] : ntiles; };
+    const BucketWalk<kMedBuckets> order(fa.tl.mb);  // largest stages first (tile_class_kernel)
+    const int nt = order.size();
+    const auto tile_at = [&](int k) { return k < nt ? order.at(fa.tl.medium, fa.tl.cap, k) : ntiles; };
     StageMeta meta = stage_meta(tile_at(blockIdx.x), ntiles, tstage, tstart, fa.tq);
     for (int k = blockIdx.x; k < nt; k += gridDim.x) {
         AB_STAMP(0);
@@ -1689,76 +1766,110 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
 // count_tile32_kernel with wave syncs instead of workgroup barriers, so the four waves of a
 // workgroup work on four tiles independently and a tile's latency chain (stage loads, scans,
 // union) never waits for a slower tile.
-constexpr int kWaveQ = kSmallCap;  // quarters of a small tile (each holds >= 1 own point)
-
-struct WaveUnion {  // per wave, aliases the count's neighbour records
-    int lp[kWaveQ];
-    uint32_t lrange[kWaveQ];
-    uint32_t lmask[kWaveQ];
-    unsigned long long cmin[kWaveQ];
+// SEG: lanes per tile.  SEG = 64 is one tile per wave; SEG = 32 (stages of at most kTinyCap
+// points) packs 64 / SEG tiles into a wave, which divides the per-tile instruction stream: a
+// tile that small is bound by that stream (its count is a few candidates), not by its loads.
+// SCAP: the stage capacity; a tile's quarters (each holds >= 1 own point) are at most SCAP.
+template <int SCAP>
+struct WaveUnion {  // per tile, aliases the count's neighbour records
+    int lp[SCAP];
+    uint32_t lrange[SCAP];
+    uint32_t lmask[SCAP];
+    unsigned long long cmin[SCAP];
     uint16_t qmap[kMaxTileQ];
 };
 
-struct WaveTile {
+template <int SCAP>
+struct WaveSeg {  // one tile of a wave
     TileStage st;
     int rowoff[9];
-    uint32_t lcore[kSmallCap / 32 + 1];
-    float2 buf[kSmallCap];
+    uint32_t lcore[SCAP / 32 + 1];
+    float2 buf[SCAP];
+};
+
+template <int SCAP, int NSEG>
+struct WaveTile {
+    WaveSeg<SCAP> sg[NSEG];
     union {
-        uint32_t rec[kMaxNbr * 64];
-        WaveUnion u;
+        uint32_t rec[kMaxNbr * 64];  // the count's neighbour records, one column per lane
+        WaveUnion<SCAP> u[NSEG];
     };
 };
 
-template <int MINW>
+// Walks the small-tile buckets [B0, B0 + NB) (tile_class_kernel), largest stages first.
+template <int MINW, int SEG, int SCAP, int B0, int NB>
 __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, double eps2, int32_t min_points,
     uint8_t* __restrict__ core, int32_t* __restrict__ parent,
     int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, FuseArgs fa) {
-    __shared__ WaveTile wt[kBlock / 64];
+    constexpr int NSEG = 64 / SEG, NQ = SCAP / SEG;
+    static_assert(B0 + NB <= kSmallBuckets && 64 % SEG == 0 && SEG >= 8 && SCAP % SEG == 0,
+                  "small-tile buckets / segments");
+    __shared__ WaveTile<SCAP, NSEG> wt[kBlock / 64];
     __shared__ int wcores[kBlock / 64];
     const GridParams g = *fa.gp;
     const int lane = __lane_id(), w = threadIdx.x >> 6;
-    WaveTile& T = wt[w];
+    const int sgi = lane / SEG, sl = lane - sgi * SEG;  // the lane's tile and its lane in it
+    const uint64_t smask = SEG == 64 ? ~0ull : (((1ull << SEG) - 1) << (sgi * SEG));
+    WaveSeg<SCAP>& T = wt[w].sg[sgi];
     TileStage& st = T.st;
-    WaveUnion& u = T.u;
+    WaveUnion<SCAP>& u = wt[w].u[sgi];
     int mine = 0;
     if (g.clique) {
         const F32Cut cut = f32_cut(g, eps2);
-        const int nt = fa.tl.n[kTileSmall];
-        for (int k = blockIdx.x * (kBlock / 64) + w; k < nt; k += gridDim.x * (kBlock / 64)) {
-            const int t = fa.tl.small[k];
-            // stage table: extended cells lane and lane + 64, scanned across the wave
-            const int2 m0 = tstage[(int64_t)t * 100 + lane];
-            const int2 m1 = lane < 36 ? tstage[(int64_t)t * 100 + 64 + lane] : make_int2(0, 0);
-            const uint32_t tk = fa.tkey[t];
-            const int q0 = fa.tq[(int64_t)t * kTslot], nq = fa.tq[(int64_t)t * kTslot + 64] - q0;
-            int i0 = m0.y, i1 = m1.y;
+        const BucketWalk<NB> order(fa.tl.sb + B0);  // largest stages first
+        const int32_t* lists = fa.tl.small + (int64_t)B0 * fa.tl.cap;
+        const int nt = order.size();
+        const int ngroups = (nt + NSEG - 1) / NSEG;
+        for (int kg = blockIdx.x * (kBlock / 64) + w; kg < ngroups;
+             kg += gridDim.x * (kBlock / 64)) {
+            // a segment without a tile runs the same steps over an empty stage
+            const int k = kg * NSEG + sgi;
+            const bool live = k < nt;
+            const int t = live ? order.at(lists, fa.tl.cap, k) : 0;
+            // stage table: extended cells sl, sl + SEG, ..., scanned across the segment
+            constexpr int kRounds = (100 + SEG - 1) / SEG;
+            int2 m[kRounds];
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v0 = __shfl_up(i0, o, 64), v1 = __shfl_up(i1, o, 64);
-                if (lane >= o) {
-                    i0 += v0;
-                    i1 += v1;
+            for (int r = 0; r < kRounds; ++r) {
+                const int e = r * SEG + sl;
+                m[r] = (live && e < 100) ? tstage[(int64_t)t * 100 + e] : make_int2(0, 0);
+            }
+            const uint32_t tk = live ? fa.tkey[t] : 0u;
+            const int q0 = live ? fa.tq[(int64_t)t * kTslot] : 0;
+            const int nq = live ? fa.tq[(int64_t)t * kTslot + 64] - q0 : 0;
+            int incl[kRounds];
+#pragma unroll
+            for (int r = 0; r < kRounds; ++r) incl[r] = m[r].y;
+#pragma unroll
+            for (int o = 1; o < SEG; o <<= 1) {
+#pragma unroll
+                for (int r = 0; r < kRounds; ++r) {
+                    const int v = __shfl_up(incl[r], o, SEG);
+                    if (sl >= o) incl[r] += v;
                 }
             }
-            const int tot0 = __shfl(i0, 63, 64), total = tot0 + __shfl(i1, 63, 64);
-            st.cb[lane] = m0.x;
-            st.off[lane] = i0 - m0.y;
-            if (lane < 36) {
-                st.cb[64 + lane] = m1.x;
-                st.off[64 + lane] = tot0 + i1 - m1.y;
+            int carry = 0;
+#pragma unroll
+            for (int r = 0; r < kRounds; ++r) {
+                const int e = r * SEG + sl;
+                if (e < 100) {
+                    st.cb[e] = m[r].x;
+                    st.off[e] = carry + incl[r] - m[r].y;
+                }
+                carry += __shfl(incl[r], SEG - 1, SEG);
             }
-            if (lane == 0) st.off[100] = total;
-            if (lane < kSmallCap / 32 + 1) T.lcore[lane] = 0u;
+            const int total = carry;
+            if (sl == 0) st.off[100] = total;
+            if (sl < SCAP / 32 + 1) T.lcore[sl] = 0u;
             wave_sync();
             {
                 const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
                 const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
 #pragma unroll
-                for (int uu = 0; uu < kSmallCap / 64; ++uu) {
-                    const int e = lane + uu * 64;
+                for (int uu = 0; uu < SCAP / SEG; ++uu) {
+                    const int e = sl + uu * SEG;
                     if (e < total) {
                         int c = 0;
 #pragma unroll
@@ -1770,20 +1881,20 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                     }
                 }
             }
-            if (lane < 8) {  // own points per tile row, prefix over the rows
-                const int rs = st.off[(lane + 1) * 10 + 9] - st.off[(lane + 1) * 10 + 1];
-                int incl = rs;
+            if (sl < 8) {  // own points per tile row, prefix over the rows
+                const int rs = st.off[(sl + 1) * 10 + 9] - st.off[(sl + 1) * 10 + 1];
+                int rincl = rs;
 #pragma unroll
                 for (int o = 1; o < 8; o <<= 1) {
-                    const int v = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += v;
+                    const int v = __shfl_up(rincl, o, SEG);
+                    if (sl >= o) rincl += v;
                 }
-                T.rowoff[lane] = incl - rs;
-                if (lane == 7) T.rowoff[8] = incl;
+                T.rowoff[sl] = rincl - rs;
+                if (sl == 7) T.rowoff[8] = rincl;
             }
             wave_sync();
             const int own = T.rowoff[8];
-            for (int i = lane; i < own; i += 64) {
+            for (int i = sl; i < own; i += SEG) {
                 int r = 0;
 #pragma unroll
                 for (int sh = 4; sh > 0; sh >>= 1)
@@ -1803,7 +1914,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                         const double2 a = xy[p], o = xy[stage_slot(st, q)];
                         return within_eps(a.x, a.y, o.x, o.y, eps2);
                     };
-                    uint32_t* lst = T.rec + lane;
+                    uint32_t* lst = wt[w].rec + lane;
                     int cnt = 0, nrec = 0;
                     bool done = scan_count32<true, 64>(T.buf, rg.cs, rg.ce, me, cut, min_points,
                                                        cnt, lst, nrec, nbr_k, 0, exact);
@@ -1828,8 +1939,8 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                             const uint32_t v = lst[rr * 64];
                             const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
                             const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
-                            for (uint32_t m = v >> 16; m; m &= m - 1) {
-                                const int qq = q + __ffs(m) - 1;
+                            for (uint32_t mm = v >> 16; mm; mm &= mm - 1) {
+                                const int qq = q + __ffs(mm) - 1;
                                 const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
                                               (qq >= st.off[k0 + 2] ? 1 : 0);
                                 const int sq = st.cb[c] + (qq - st.off[c]);
@@ -1845,14 +1956,14 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                 mine += is_core ? 1 : 0;
             }
             wave_sync();
-            // quarter records + union over the tile's quarters (fused_tile_union32, per wave)
-            for (int idx = lane; idx < kMaxTileQ; idx += 64) u.qmap[idx] = 0xFFFF;
-            for (int idx = lane; idx < kWaveQ; idx += 64) u.cmin[idx] = ~0ull;
+            // quarter records + union over the tile's quarters (fused_tile_union32, per tile)
+            for (int idx = sl; idx < kMaxTileQ; idx += SEG) u.qmap[idx] = 0xFFFF;
+            for (int idx = sl; idx < SCAP; idx += SEG) u.cmin[idx] = ~0ull;
             wave_sync();
-            int rep[kWaveQ / 64], best[kWaveQ / 64];
+            int rep[NQ], best[NQ];
 #pragma unroll
-            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
-                const int qi = lane + pp * 64;
+            for (int pp = 0; pp < NQ; ++pp) {
+                const int qi = sl + pp * SEG;
                 rep[pp] = -1;
                 best[pp] = 0x7FFFFFFF;
                 if (qi < nq) {
@@ -1893,7 +2004,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                 const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
                 return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
             };
-            for (int qi = lane; qi < nq; qi += 64)
+            for (int qi = sl; qi < nq; qi += SEG)
                 if (u.lrange[qi] >> 31)
                     unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, qi, T.buf, is_core_l, cut,
                                      exact2);
@@ -1902,19 +2013,19 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             // edge inside it
             int f = 0x7FFFFFFF;
 #pragma unroll
-            for (int pp = kWaveQ / 64 - 1; pp >= 0; --pp)
-                if (lane + pp * 64 < nq && rep[pp] >= 0) f = lane + pp * 64;
+            for (int pp = NQ - 1; pp >= 0; --pp)
+                if (sl + pp * SEG < nq && rep[pp] >= 0) f = sl + pp * SEG;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, 64));
+            for (int o = SEG / 2; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, SEG));
             bool split = false;
 #pragma unroll
-            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
-                const int qi = lane + pp * 64;
+            for (int pp = 0; pp < NQ; ++pp) {
+                const int qi = sl + pp * SEG;
                 if (qi < nq && rep[pp] >= 0 && lfind(u.lp, qi) != lfind(u.lp, f)) split = true;
             }
-            if (__ballot(split)) {
+            if (__ballot(split) & smask) {
                 wave_sync();
-                for (int it = lane; it < nq * 8; it += 64) {
+                for (int it = sl; it < nq * 8; it += SEG) {
                     const int o = it / nq, qi = it - o * nq;
                     const uint32_t ri = u.lrange[qi];
                     if (!(ri >> 31)) continue;
@@ -1934,10 +2045,10 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                 }
             }
             wave_sync();
-            int rr[kWaveQ / 64];
+            int rr[NQ];
 #pragma unroll
-            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
-                const int qi = lane + pp * 64;
+            for (int pp = 0; pp < NQ; ++pp) {
+                const int qi = sl + pp * SEG;
                 rr[pp] = -1;
                 if (qi < nq && rep[pp] >= 0) {
                     rr[pp] = lfind(u.lp, qi);
@@ -1947,8 +2058,8 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             }
             wave_sync();
 #pragma unroll
-            for (int pp = 0; pp < kWaveQ / 64; ++pp) {
-                const int qi = lane + pp * 64;
+            for (int pp = 0; pp < NQ; ++pp) {
+                const int qi = sl + pp * SEG;
                 if (qi < nq) {
                     const int crep =
                         rr[pp] >= 0 ? (int)(uint32_t)(u.cmin[rr[pp]] & 0xFFFFFFFFull) : -1;
@@ -2947,6 +3058,11 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 //   8 spills and is slower, tools/union_w_sweep.sh, r05); 5 and 7 for measurements.
 // DBSCAN_AB_F32=0: count clique grids with the fp64 staging.
 // DBSCAN_AB_FUSE=0: run quarter_init and tile_union as their own kernels.
+// DBSCAN_AB_TINY_W: waves per SIMD of the packed count_wave instances.
+#ifndef DBSCAN_AB_TINY_W
+#define DBSCAN_AB_TINY_W 5
+#endif
+static constexpr int kTinyWaves = DBSCAN_AB_TINY_W;
 #ifndef DBSCAN_AB_COUNT_ABLATE
 #define DBSCAN_AB_COUNT_ABLATE 0
 #endif
@@ -3136,8 +3252,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     TileLists tl{};
     uint8_t* tclass = nullptr;
     if (f32) {
-        int32_t* lists = static_cast<int32_t*>(ws.bigt.ensure(3 * ntile_bound * sizeof(int32_t)));
-        tl = TileLists{&st[kStTileLists], lists, lists + ntile_bound, lists + 2 * ntile_bound};
+        int32_t* lists = static_cast<int32_t*>(
+            ws.bigt.ensure((1 + kSmallBuckets + kMedBuckets) * ntile_bound * sizeof(int32_t)));
+        tl = TileLists{&st[kStTileLists],
+                       lists + ntile_bound,
+                       lists + (1 + kSmallBuckets) * ntile_bound,
+                       lists,
+                       &st[kStTileBuckets],
+                       &st[kStTileBuckets + kSmallBuckets],
+                       (int32_t)ntile_bound};
         tclass = static_cast<uint8_t*>(ws.tclass.ensure(ntile_bound));
     }
     int32_t* tsz = static_cast<int32_t*>(ws.tsz.ensure(ntile_bound * sizeof(int32_t)));
@@ -3214,7 +3337,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
     // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
-        ws.blockcnt.ensure(2 * ((size_t)4 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
+        ws.blockcnt.ensure(2 * ((size_t)6 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
@@ -3236,9 +3359,37 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 // clique grids by tile stage size: small tiles one wave each (count_wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
                 // big_union); other grids: count (fp64)
-                klaunch(prof, "count_wave", count_wave_kernel<5>, dim3(tile_grid), dim3(kBlock),
-                        0, s, xy, tstart, tstage, eps2, a.min_points, core, parent,
-                        block_cores + 3 * tile_grid, nbr, nbr_k, fa);
+                // small tiles: 64 lanes per tile over kTinyCap points, then tiles packed 2 (and
+                // 4) to a wave
+                {
+                    int32_t* bc = block_cores + 3 * tile_grid;
+                    if constexpr (kWaveSplit == 0)
+                        klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kSmallBuckets>,
+                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                                a.min_points, core, parent, bc, nbr, nbr_k, fa);
+                    else
+                        klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0>,
+                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                                a.min_points, core, parent, bc, nbr, nbr_k, fa);
+                    if constexpr (kWaveSplit == 1)
+                        klaunch(prof, "count_tiny",
+                                count_wave_kernel<kTinyWaves, 32, 32, kTinyBucket0, 1>,
+                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                                a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
+                    if constexpr (kWaveSplit == 2) {
+                        klaunch(prof, "count_tiny",
+                                count_wave_kernel<kTinyWaves, 32, 64, kTinyBucket0, 2>,
+                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                                a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
+                        klaunch(prof, "count_tiny16",
+                                count_wave_kernel<kTinyWaves, 16, 16, kTinyBucket0 + 2, 1>,
+                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                                a.min_points, core, parent, bc + 2 * tile_grid, nbr, nbr_k, fa);
+                    }
+                    if (kWaveSplit < 2)
+                        DBSCAN_HIP_CHECK(hipMemsetAsync(bc + (kWaveSplit + 1) * tile_grid, 0,
+                                                        (2 - kWaveSplit) * tile_grid * sizeof(int32_t), s));
+                }
                 auto k32 =
                     union_w() == 5 ? count_tile32_kernel<kCap32, 5> : count_tile32_kernel<kCap32, 6>;
                 klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
@@ -3260,7 +3411,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
-        const int64_t nmain = (f32 ? 4 : 1) * (int64_t)tile_grid;
+        const int64_t nmain = (f32 ? 6 : 1) * (int64_t)tile_grid;
         klaunch(prof, "count_rest", count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
                            a.min_points, core, parent, block_cores + nmain);
         DBSCAN_HIP_CHECK(hipGetLastError());
@@ -3417,7 +3568,8 @@ FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
     if (ws.fit_n == 0) return stats;
     GridParams g;
     memcpy(&g, buf + 8, sizeof(g));
-    int32_t v[kStCount];
+    int32_t v[kStTileBuckets];  // (the stats copy holds the states before the buckets)
+    static_assert(16 * sizeof(double) + sizeof(v) <= kFitStatsDoubles * sizeof(double), "stats copy too short");
     memcpy(v, buf + 16, sizeof(v));
     if (v[kStError]) throw ArgError{"cannot size the eps grid"};
     stats.nf = v[kStNf];

@@ -52,7 +52,8 @@ enum FitState {
     kStTileLists = 9,  // [3] clique-grid tiles per count path: small, medium, big
     kStClassPts = 12,  // [3] their own points (what each count kernel processes)
     kStBoxEdges = 15,  // archery float32 box: one-way core-core pairs recorded
-    kStCount = 16
+    kStTileBuckets = 16,  // [<= 16] small, medium tiles per stage-size bucket (tile_class_kernel)
+    kStCount = 32
 };
 
 #define DBSCAN_HIP_CHECK(expr)                                                              \

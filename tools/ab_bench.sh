@@ -15,7 +15,8 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 k = d["kernels_ms_per_step"]
 top = ", ".join(f"{a}={b:.3f}" for a, b in list(k.items())[:8])
-print(f"{sys.argv[1]:10s} {d['ms_per_step']:.4f} ms  k={d['config']['clusters']}  {top}")
+cnt = "+".join(f"{k.get(a, 0):.3f}" for a in ("count32", "count_wave", "count_tiny", "count_tiny16", "big_count"))
+print(f"{sys.argv[1]:10s} {d['ms_per_step']:.4f} ms  k={d['config']['clusters']}  count {cnt}  {top}")
 PY
   done
 done
