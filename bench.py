@@ -57,6 +57,7 @@ SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 ALG_BYTES = {
     "bbox_partial": 16, "bin": 20, "radix_upsweep": 4, "radix_downsweep": 16, "inverse": 8,
     "scatter_xy": 36, "heads_reduce": 4, "heads_down": 16, "count": 21, "count_wave": 21,
+    "count_tiny": 21,
     "count32": 21, "big_count": 21, "edge_union": 0, "quarter_root": 0, "final": 13,
     "label_sorted": 13, "permute_out": 13,
 }

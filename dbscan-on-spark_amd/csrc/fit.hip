@@ -588,7 +588,8 @@ __global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __res
                                                             const GridParams* __restrict__ gp,
                                                             TileLists tl,
                                                             uint8_t* __restrict__ tclass,
-                                                            int32_t* __restrict__ class_pts) {
+                                                            int32_t* __restrict__ class_pts,
+                                                            uint8_t* __restrict__ tcore) {
     if (!gp->clique) return;
     // categories: small bucket b (b = 0 the largest stages), big, medium bucket b
     constexpr int kCatBig = kSmallBuckets, kCatMed = kSmallBuckets + 1;
@@ -613,6 +614,7 @@ __global__ __launch_bounds__(kBlock) void tile_class_kernel(const int32_t* __res
                 const int c = tsz[t];
                 v[r] = c <= kSmallCap ? kTileSmall : (c <= CAP ? kTileMedium : kTileBig);
                 tclass[t] = (uint8_t)v[r];
+                if (v[r] == kTileBig) tcore[t] = 3;  // (big_union's tiles: not tracked)
                 own = tstart[t + 1] - tstart[t];
                 if (v[r] == kTileSmall) {
                     cat[r] = 0;
@@ -1015,6 +1017,8 @@ struct FuseArgs {
     int4* qinfo;             // out: (begin, end, rep, core mask) per quarter
     int4* qg;                // out: (quarter-grid x, y, min visit index of its cores, 0)
     int32_t* qcomp;          // out: tile component rep per quarter (-1: no cores)
+    uint8_t* tcore;          // out (f32): per tile, bit 0 its east cell column holds a core,
+                             // bit 1 its south cell row does (edge_union skips the other sides)
 };
 
 struct UnionLds {  // aliases the count's neighbour-list staging (the two never overlap in time)
@@ -1511,7 +1515,8 @@ __device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange
 }
 
 // fused_tile_union over the float2 stage (see fused_tile_union for the structure)
-__device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
+__device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t key,
+                                   const FuseArgs& fa,
                                    const GridParams& g, const TileStage& st,
                                    const float2* __restrict__ buf,
                                    const uint32_t* __restrict__ lcore,
@@ -1524,7 +1529,11 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
         return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
     };
     __shared__ int s_first;  // smallest local quarter holding a core
-    if (i == 0) s_first = 0x7FFFFFFF;
+    __shared__ int s_tflags;  // the tile's edge strips holding cores (FuseArgs::tcore)
+    if (i == 0) {
+        s_first = 0x7FFFFFFF;
+        s_tflags = 0;
+    }
     u.qmap[i] = 0xFFFF;
     u.cmin[i] = ~0ull;
     lds_barrier();
@@ -1557,7 +1566,12 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
             rep = b + first;
             best = fa.perm[rep];
         }
-        if (rep >= 0) atomicMin(&s_first, i);
+        if (rep >= 0) {
+            atomicMin(&s_first, i);
+            // east cell column: local quarter x 14, 15; south cell row: local quarter y 14, 15
+            const int tf = ((gx & 15) >= 14 ? 1 : 0) | ((gy & 15) >= 14 ? 2 : 0);
+            if (tf) atomicOr(&s_tflags, tf);
+        }
         fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
         u.lp[i] = i;
         u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) | (uint32_t)jb |
@@ -1566,6 +1580,7 @@ __device__ void fused_tile_union32(int q0, int nq, int b, int e, uint32_t key, c
         u.qmap[lq] = (uint16_t)i;
     }
     lds_barrier();
+    if (i == 0) fa.tcore[t] = (uint8_t)s_tflags;
     AB_STAMP(5);
     if (ablate != 3) {
         // adjacent quarters (the 4 backward offsets) from each core quarter's own thread
@@ -1745,7 +1760,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
             AB_STAMP(3);
             __syncthreads();
             AB_STAMP(4);
-            fused_tile_union32(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
+            fused_tile_union32(t, q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
                                *reinterpret_cast<UnionLds*>(lsts), ablate);
         }
         __syncthreads();
@@ -1894,6 +1909,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             }
             wave_sync();
             const int own = T.rowoff[8];
+            int tflags = 0;
             for (int i = sl; i < own; i += SEG) {
                 int r = 0;
 #pragma unroll
@@ -1952,8 +1968,13 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                 }
                 if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
                 if (is_core) atomicOr(&T.lcore[j >> 5], 1u << (j & 31));
+                if (is_core) tflags |= (ex == 7 ? 1 : 0) | (r == 7 ? 2 : 0);
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
+            }
+            {
+                const uint64_t b0 = __ballot(tflags & 1) & smask, b1 = __ballot(tflags & 2) & smask;
+                if (live && sl == 0) fa.tcore[t] = (uint8_t)((b0 ? 1 : 0) | (b1 ? 2 : 0));
             }
             wave_sync();
             // quarter records + union over the tile's quarters (fused_tile_union32, per tile)
@@ -2088,9 +2109,10 @@ constexpr int kBigChunks = 8;
 template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart, double eps2,
-    int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ block_cores,
-    int32_t* __restrict__ nbr, int nbr_k, FuseArgs fa) {
+    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
+    const int32_t* __restrict__ qidx, double eps2, int32_t min_points,
+    uint8_t* __restrict__ core, int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr,
+    int nbr_k, FuseArgs fa) {
     __shared__ int wcores[kBlock / 64];
     __shared__ TileStage st;  // (unused by the global-memory count)
     int mine = 0;
@@ -2101,8 +2123,11 @@ __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
             const int te = tstart[t + 1];
             for (int p = tstart[t] + c * kBlock + (int)threadIdx.x; p < te;
                  p += kBigChunks * kBlock) {
+                // a quarter cell is a clique on these grids: one holding minPoints points makes
+                // each of them core without a count (a third of the big tiles' points at 10^7)
+                const int q = qidx[p];
                 const bool is_core =
-                    (min_points <= 0 ||
+                    (min_points <= 0 || fa.qstart[q + 1] - fa.qstart[q] >= min_points ||
                      count_point<false>(st, nullptr, xy, cell, seg, 0, 0, p, eps2, min_points,
                                         nullptr, nbr, nbr_k)) &&
                     !(fa.zs && fa.zs[p] == 2);  // slab halo: candidate only
@@ -2434,7 +2459,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const int4* __restrict__ qinfo, const int4* __restrict__ qg,
     const int32_t* __restrict__ qcomp, double eps2, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    const GridParams* __restrict__ gp) {
+    const GridParams* __restrict__ gp, const uint8_t* __restrict__ tcore) {
     if (!gp->clique) return;
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
     __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
@@ -2453,6 +2478,8 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
         int nA = 0, ntot = 0;
         {
             const int4 nb = tnb[t];
+            // an own strip without cores has no pair to test (tcore: the count kernels')
+            if (tcore && !((tcore[t] >> side) & 1)) continue;
             const int occB = side ? nb.y : nb.x, occC = side ? nb.w : nb.z;
             const int k = lane & 7;
             int occ = -1, l = 0;
@@ -3251,6 +3278,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         (!box && a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
     TileLists tl{};
     uint8_t* tclass = nullptr;
+    uint8_t* tcore = nullptr;  // f32: per tile, its edge strips hold cores (count kernels)
     if (f32) {
         int32_t* lists = static_cast<int32_t*>(
             ws.bigt.ensure((1 + kSmallBuckets + kMedBuckets) * ntile_bound * sizeof(int32_t)));
@@ -3262,6 +3290,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                        &st[kStTileBuckets + kSmallBuckets],
                        (int32_t)ntile_bound};
         tclass = static_cast<uint8_t*>(ws.tclass.ensure(ntile_bound));
+        tcore = static_cast<uint8_t*>(ws.tcore.ensure(ntile_bound));
     }
     int32_t* tsz = static_cast<int32_t*>(ws.tsz.ensure(ntile_bound * sizeof(int32_t)));
 
@@ -3321,7 +3350,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                             (ntile_bound + kBlock * kClassRounds - 1) / (kBlock * kClassRounds),
                             1024)),
                         dim3(kBlock), 0, s, tsz, tstart, &st[kStTiles], gp, tl, tclass,
-                        &st[kStClassPts]);
+                        &st[kStClassPts], tcore);
         }
         {
             StageTimer t(prof, s, "segs");
@@ -3350,7 +3379,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 case 1024: kern = count_tile_kernel<1024, 5, false>; break;
                 default: break;
             }
-            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp};
+            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp,
+                              tcore};
             if (box) {
                 klaunch(prof, "box_count", box_count_kernel, dim3(tile_grid), dim3(kBlock), 0, s,
                         xy, cell, seg, nf_p, a.eps, eps2, a.min_points, core, parent,
@@ -3396,7 +3426,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
                         block_cores, nbr, nbr_k, count_ablate(), fa);
                 klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,
-                        s, xy, cell, seg, tstart, eps2, a.min_points, core,
+                        s, xy, cell, seg, tstart, qidx, eps2, a.min_points, core,
                         block_cores + tile_grid, nbr, nbr_k, fa);
                 klaunch(prof, "big_union", big_union_kernel, dim3(2048), dim3(kBlock), 0, s, xy,
                         (const uint8_t*)core, eps2, parent, fa, count_ablate());
@@ -3443,7 +3473,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             if (union_w() == 5) eu = edge_union_kernel<5>;
             if (union_w() == 7) eu = edge_union_kernel<7>;
             klaunch(prof, "edge_union", eu, dim3(tile_grid), dim3(kBlock), 0, s, xy,
-                    &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp);
+                    &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
+                    (const uint8_t*)tcore);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");

@@ -151,7 +151,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots, box_edges, box_map;
+        key3, perm3, spacked, lroots, box_edges, box_map, tcore;
     ScanState scan;
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
@@ -164,7 +164,7 @@ struct Workspace {
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
-                          &box_edges, &box_map})
+                          &box_edges, &box_map, &tcore})
             b->release();
     }
 };
