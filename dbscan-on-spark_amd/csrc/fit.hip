@@ -2590,11 +2590,14 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
 }
 
 // After all unions: every quarter rep points straight at its root, so the per-point walk in
-// final_kernel is core -> rep -> root.
-__global__ __launch_bounds__(kBlock) void quarter_root_kernel(const int4* __restrict__ qinfo,
-                                                              const int32_t* __restrict__ nq_p,
-                                                              const GridParams* __restrict__ gp,
-                                                              int32_t* __restrict__ parent) {
+// final_kernel is core -> rep -> root.  qlab (direct fits): also the root's visit index per
+// quarter, and the root flag (every root is a quarter rep: the rep of exactly one quarter), so
+// that final_kernel's grid cores only read their quarter's qlab.
+__global__ __launch_bounds__(kBlock) void quarter_root_kernel(
+    const int4* __restrict__ qinfo, const int32_t* __restrict__ nq_p,
+    const GridParams* __restrict__ gp, int32_t* __restrict__ parent,
+    const int32_t* __restrict__ perm, int32_t* __restrict__ qlab,
+    unsigned long long* __restrict__ root_bits) {
     if (!gp->clique) return;
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= *nq_p) return;
@@ -2603,6 +2606,11 @@ __global__ __launch_bounds__(kBlock) void quarter_root_kernel(const int4* __rest
     int r = rep;
     for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
     parent[rep] = r;
+    if (qlab) {
+        const int32_t o = perm[r];
+        qlab[q] = o;
+        if (r == rep) atomicOr(root_bits + (o >> 6), 1ull << (o & 63));
+    }
 }
 
 // qidx/qinfo (fused union: core parents were never written): a grid core's walk starts at its
@@ -2616,7 +2624,8 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t*
                                                        const int4* __restrict__ qinfo,
                                                        int32_t* __restrict__ lab,
                                                        unsigned long long* __restrict__ root_bits,
-                                                       int32_t* __restrict__ root_out) {
+                                                       int32_t* __restrict__ root_out,
+                                                       const int32_t* __restrict__ qlab) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     if (!core[p]) {
@@ -2625,6 +2634,10 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t*
     }
     int r = (int)p;
     const int64_t nf = *nf_p;
+    if (qlab && gp->clique && p < nf) {  // quarter_root_kernel resolved the quarter's root
+        lab[p] = qlab[qidx[p]];
+        return;
+    }
     if (qidx && gp->clique && nf > 0) {
         // Branch-free on purpose: the divergent form `p < nf ? qinfo[qidx[p]].z : p` was
         // miscompiled (ROCm 7.2 clang, gfx950: the else value was never moved into place for
@@ -3451,6 +3464,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
                                core);
     }
+    // direct fits with fused quarter unions: quarter_root_kernel flags the roots (root bits)
+    uint64_t* qlab_bits =
+        (!a.zone && fuse && mode == kGridEps && !box)
+            ? static_cast<uint64_t*>(ws.is_root.ensure(((n + 63) / 64) * sizeof(uint64_t)))
+            : nullptr;
     if (mode == kGridEps && !box) {  // quarter-cell unions (no-ops unless the grid made them cliques)
         if (!fuse) {
             StageTimer t(prof, s, "quarter_init");
@@ -3478,8 +3496,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
+        // direct fits (fused quarter unions): the roots' visit indices per quarter (into the
+        // dead qcomp) and the root flags, for final_kernel
+        if (qlab_bits) DBSCAN_HIP_CHECK(hipMemsetAsync(qlab_bits, 0, ((n + 63) / 64) * sizeof(uint64_t), s));
         klaunch(prof, "quarter_root", quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
-                           &st[kStQuarters], gp, parent);
+                &st[kStQuarters], gp, parent, perm, qlab_bits ? qcomp : (int32_t*)nullptr,
+                reinterpret_cast<unsigned long long*>(qlab_bits));
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
@@ -3501,10 +3523,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         int32_t* word_rank = static_cast<int32_t*>(ws.rank.ensure(nw * sizeof(int32_t)));
         {
             StageTimer t(prof, s, "final");
-            DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
+            if (!qlab_bits) DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
-                               reinterpret_cast<unsigned long long*>(root_bits), (int32_t*)nullptr);
+                               reinterpret_cast<unsigned long long*>(root_bits), (int32_t*)nullptr,
+                               qlab_bits ? (const int32_t*)qcomp : (const int32_t*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {
@@ -3539,7 +3562,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             if (lean) DBSCAN_HIP_CHECK(hipMemsetAsync(a.root_out, 0xFF, n * sizeof(int32_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
-                               (unsigned long long*)nullptr, lean ? a.root_out : (int32_t*)nullptr);
+                               (unsigned long long*)nullptr, lean ? a.root_out : (int32_t*)nullptr,
+                               (const int32_t*)nullptr);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         {

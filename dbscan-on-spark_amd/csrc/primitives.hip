@@ -481,9 +481,7 @@ __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __re
                                                               int64_t n, double* partial) {
     __shared__ double sm[kWaves][5];
     double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY, cnt = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kBlock) {
-        const double a = x[i], b = y[i];
+    const auto take = [&](double a, double b) {
         if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
             xmin = fmin(xmin, a);
             xmax = fmax(xmax, a);
@@ -491,6 +489,29 @@ __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __re
             ymax = fmax(ymax, b);
             cnt += 1.0;
         }
+    };
+    const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x, stride = (int64_t)gridDim.x * kBlock;
+    if ((((uintptr_t)x | (uintptr_t)y) & 15u) == 0) {
+        // 16-B loads, two pairs in flight per thread and trip (the plain form read 4.7 TB/s)
+        const double2* x2 = reinterpret_cast<const double2*>(x);
+        const double2* y2 = reinterpret_cast<const double2*>(y);
+        const int64_t n2 = n >> 1;
+        int64_t i = gt;
+        for (; i + stride < n2; i += 2 * stride) {
+            const double2 a0 = x2[i], b0 = y2[i], a1 = x2[i + stride], b1 = y2[i + stride];
+            take(a0.x, b0.x);
+            take(a0.y, b0.y);
+            take(a1.x, b1.x);
+            take(a1.y, b1.y);
+        }
+        if (i < n2) {
+            const double2 a0 = x2[i], b0 = y2[i];
+            take(a0.x, b0.x);
+            take(a0.y, b0.y);
+        }
+        if ((n & 1) && gt == 0) take(x[n - 1], y[n - 1]);
+    } else {
+        for (int64_t i = gt; i < n; i += stride) take(x[i], y[i]);
     }
     xmin = wave_min(xmin);
     xmax = wave_max(xmax);
