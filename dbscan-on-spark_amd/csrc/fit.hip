@@ -3413,7 +3413,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     // per-tile kernels: grid stride over occupied tiles (their count stays on the device)
     const unsigned tile_grid = (unsigned)std::min<int64_t>(ntile_bound, kTileGrid);
-    const unsigned rest_grid = std::min(nblk(n), 1024u);  // slots [nf, n): outside the grid
+    // slots [nf, n): outside the grid (usually none: a small grid, since every block's count
+    // enters the core scan)
+    const unsigned rest_grid = std::min(nblk(n), 256u);
     // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
     // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
@@ -3552,7 +3554,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                     dim3(kBlock), 0, s, xy, cell, seg, nf_p, a.eps, eps2, perm, core, parent,
                     edges, &st[kStBoxEdges], (int32_t)kBoxEdgeCap);
         } else {
-            klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 4096u)), dim3(kBlock), 0,
+            // (a no-op on clique grids: a grid that just fills the GPU once)
+            klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 2048u)), dim3(kBlock), 0,
                     s, xy, cell, seg, nf_p, gp, eps2, perm, core, parent);
         }
         DBSCAN_HIP_CHECK(hipGetLastError());

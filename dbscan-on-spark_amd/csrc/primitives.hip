@@ -202,10 +202,25 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
     for (int d = threadIdx.x; d < kWaves * RB; d += kBlock) (&h[0][0])[d] = 0;
     __syncthreads();
     const int64_t base = (int64_t)blockIdx.x * kRTile;
+    if (base + kRTile <= n) {  // a full tile: 16-B key loads, all in flight together
+        static_assert(kRItems % 4 == 0, "whole uint4s per thread");
+        const uint4* k4 = reinterpret_cast<const uint4*>(key + base);
+        uint4 v[kRItems / 4];
+#pragma unroll
+        for (int r = 0; r < kRItems / 4; ++r) v[r] = k4[r * kBlock + threadIdx.x];
+#pragma unroll
+        for (int r = 0; r < kRItems / 4; ++r) {
+            atomicAdd(&h[w][(v[r].x >> shift) & (RB - 1u)], 1u);
+            atomicAdd(&h[w][(v[r].y >> shift) & (RB - 1u)], 1u);
+            atomicAdd(&h[w][(v[r].z >> shift) & (RB - 1u)], 1u);
+            atomicAdd(&h[w][(v[r].w >> shift) & (RB - 1u)], 1u);
+        }
+    } else {
 #pragma unroll 4
-    for (int r = 0; r < kRItems; ++r) {
-        const int64_t i = base + r * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[w][(key[i] >> shift) & (RB - 1u)], 1u);
+        for (int r = 0; r < kRItems; ++r) {
+            const int64_t i = base + r * kBlock + threadIdx.x;
+            if (i < n) atomicAdd(&h[w][(key[i] >> shift) & (RB - 1u)], 1u);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < RB; d += kBlock) {
