@@ -567,7 +567,8 @@ constexpr int kSmallCap = 192;
 // 0.316-0.331 ms: within a bucket the tiles lose the list's spatial order), so the medium tiles
 // stay one list in tile order (DBSCAN_AB_MED_BUCKETS: A/B builds).  Small-tile buckets hold
 // stage sizes (kSmallEdge[b + 1], kSmallEdge[b]]; count_wave_kernel runs in instances by lanes
-// per tile (kWaveSplit: 64 lanes above kTinyCap, 32 up to it; with DBSCAN_AB_WAVE_SPLIT=2 also
+// per tile (kWaveSplit: 64 lanes above kTinyCap, 32 up to it; DBSCAN_AB_WAVE_SPLIT=3: 32 lanes up
+// to 64 points, measured even (10^7 0.092 -> 0.096 ms, config 3 share 0.254 -> 0.242); =2 also
 // 16 lanes up to 16 points).
 #ifndef DBSCAN_AB_MED_BUCKETS
 #define DBSCAN_AB_MED_BUCKETS 1
@@ -582,6 +583,10 @@ constexpr int kWaveSplit = DBSCAN_AB_WAVE_SPLIT;  // 0: one instance; 1: 64 | 32
 __device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 128, 64, 32, 16, 0};
 constexpr int kTinyCap = 64;     // the 32-lane instance: stages in (16, 64]
 constexpr int kTinyBucket0 = 2;  // its first bucket
+#elif DBSCAN_AB_WAVE_SPLIT == 3
+__device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 144, 96, 64, 32, 0};
+constexpr int kTinyCap = 64;     // the 32-lane instance: stages up to 64
+constexpr int kTinyBucket0 = 3;
 #else
 __device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 144, 96, 64, 32, 0};
 constexpr int kTinyCap = 32;     // the 32-lane instance: stages up to 32
@@ -3454,9 +3459,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0>,
                                 dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                                 a.min_points, core, parent, bc, nbr, nbr_k, fa);
-                    if constexpr (kWaveSplit == 1)
+                    if constexpr (kWaveSplit == 1 || kWaveSplit == 3)
                         klaunch(prof, "count_tiny",
-                                count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0, 1>,
+                                count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0,
+                                                  kSmallBuckets - kTinyBucket0>,
                                 dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                                 a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
                     if constexpr (kWaveSplit == 2) {
@@ -3469,9 +3475,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                 dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                                 a.min_points, core, parent, bc + 2 * tile_grid, nbr, nbr_k, fa);
                     }
-                    if (kWaveSplit < 2)
-                        DBSCAN_HIP_CHECK(hipMemsetAsync(bc + (kWaveSplit + 1) * tile_grid, 0,
-                                                        (2 - kWaveSplit) * tile_grid * sizeof(int32_t), s));
+                    if constexpr (kWaveSplit != 2) {
+                        constexpr int used = kWaveSplit == 0 ? 1 : 2;
+                        DBSCAN_HIP_CHECK(hipMemsetAsync(bc + used * tile_grid, 0,
+                                                        (3 - used) * tile_grid * sizeof(int32_t), s));
+                    }
                 }
                 auto k32 =
                     union_w() == 5 ? count_tile32_kernel<kCap32, 5> : count_tile32_kernel<kCap32, 6>;
