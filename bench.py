@@ -359,7 +359,13 @@ def main():
                         f"{args.dense}, seed={args.seed}) -- BASELINE config 3 (10^8 points, "
                         f"20% noise, 8 GPUs) exactly at N = 8")
         else:
-            workload = (f"config 2: G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
+            # which BASELINE config this single fit is (or is the per-GPU share of)
+            shape = (n_total, args.noise, args.dense, args.seed)
+            name = {(10_000_000, 0.0, 1.0, 1): "config 2",
+                    (12_500_000, 0.2, 1.0, 2): "config 3's per-GPU share",
+                    (50_000_000, 0.0, 8.0, 3): "config 4",
+                    (125_000_000, 0.2, 1.0, 4): "config 5's per-GPU share"}.get(shape, "custom")
+            workload = (f"{name}: G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
                         f"dense={args.dense}, seed={args.seed})")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "points/s", "n_gpus": world,

@@ -53,6 +53,9 @@ def stage_of(sym):
     base = sym.split("<")[0]
     if base in STAGE_OF:
         return STAGE_OF[base]
+    if base == "count_wave_kernel":  # instances by lanes per tile: the library's profile names
+        seg = int(sym[len(base) + 1:-1].split(",")[1])
+        return {64: "count_wave", 32: "count_tiny", 16: "count_tiny16"}[seg]
     if not base.endswith("_kernel"):
         return None
     st = base[:-len("_kernel")]
