@@ -121,15 +121,20 @@ class Comm:
 
     def __init__(self, dist=None):
         self.dist = dist
+        # force: run the collectives at one rank too (tests: RCCL's calls on a one-GPU box)
+        self.force = False
         if dist is not None and dist.is_initialized():
             self.world, self.rank = dist.get_world_size(), dist.get_rank()
             self.host = dist.get_backend() == "gloo"
         else:
             self.dist, self.world, self.rank, self.host = None, 1, 0, True
 
+    def _local(self) -> bool:  # one rank and no forced collectives: nothing to exchange
+        return self.world == 1 and not (self.force and self.dist is not None)
+
     def sizes(self, k: int) -> List[int]:
         """Every rank's k, in rank order."""
-        if self.world == 1:
+        if self._local():
             return [k]
         n = torch.tensor([k], dtype=torch.int64,
                          device="cpu" if self.host else torch.device("cuda",
@@ -140,7 +145,7 @@ class Comm:
 
     def allgather_varlen(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate every rank's t along its last dim, in rank order."""
-        if self.world == 1:
+        if self._local():
             return t
         return self.allgather_fixed(t, self.sizes(t.shape[-1]))
 
@@ -148,7 +153,7 @@ class Comm:
         """t: rows grouped by destination rank (send_counts[d] rows to rank d).  Returns the
         rows every rank sent here, in source-rank order: one all_to_all_single of the counts,
         one of the rows (RCCL over xGMI for 'nccl')."""
-        if self.world == 1:
+        if self._local():
             return t
         dev = t.device
         cdev = "cpu" if self.host else t.device
@@ -163,7 +168,7 @@ class Comm:
 
     def allgather_fixed(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
         """allgather_varlen when every rank's length is already known (no size exchange)."""
-        if self.world == 1:
+        if self._local():
             return t
         dev = t.device
         tt = t.cpu() if self.host else t.contiguous()

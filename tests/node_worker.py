@@ -77,7 +77,15 @@ class OracleSlabOps:
 def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # NODE_WORKER_BACKEND=nccl (one rank per GPU: RCCL refuses two ranks on one GPU) with
+    # NODE_WORKER_FORCE_COLLECTIVES=1 runs RCCL's collectives even at world size 1
+    backend = os.environ.get("NODE_WORKER_BACKEND", "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     from dbscan_amd import node
 
     d = np.load(data_path)
@@ -94,6 +102,7 @@ def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
     else:
         ops = OracleSlabOps()
     comm = node.Comm(dist)
+    comm.force = os.environ.get("NODE_WORKER_FORCE_COLLECTIVES") == "1"
     if os.environ.get("NODE_WORKER_CHUNKS") == "1":  # host-to-slab path: this rank's chunk only
         bounds = node.NodeJob.chunk_bounds(x.numel(), world)
         c0, c1 = bounds[rank], bounds[rank + 1]

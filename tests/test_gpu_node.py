@@ -95,6 +95,23 @@ def test_set_stream_bind_and_restore():
     h.close()
 
 
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_gpu_node_rccl_world1(tmp_path, chunks):
+    """The node step over RCCL: one rank on the test GPU with the collectives forced (all_gather,
+    all_to_all_single on device tensors, the dtypes the exchange uses), so the nccl calls the
+    driver's multi-GPU runs make are exercised here; bit-exact against one fit."""
+    n = 300_000
+    x, y = gen_blobs(n, noise=0.2, seed=19)
+    env = {"NODE_WORKER_BACKEND": "nccl", "NODE_WORKER_FORCE_COLLECTIVES": "1"}
+    cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, 2.55, 10, 0, use_gpu=True, timeout=300,
+                                    chunks=chunks, env_extra=env)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
+    np.testing.assert_array_equal(cl, rc)
+    np.testing.assert_array_equal(fl, rf)
+    assert ks == {rk}
+
+
 def test_gpu_node_single_rank(tmp_path):
     x, y = gen_blobs(300_000, noise=0.1, seed=77)
     cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, 2.55, 10, 0, use_gpu=True)

@@ -88,6 +88,21 @@ def test_node_single_rank_equals_single_fit(tmp_path):
     np.testing.assert_array_equal(fl, rf)
 
 
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_node_forced_collectives_one_rank(tmp_path, chunks):
+    """Comm.force: the collectives run at one rank too (the GPU suite's RCCL check uses it)."""
+    n = 20_000
+    x, y = _data(n, seed=5)
+    eps = 60.0 * np.sqrt(n / 1e6)
+    cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, eps, 10, 0, chunks=chunks,
+                                    env_extra={"NODE_WORKER_FORCE_COLLECTIVES": "1"})
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, eps, 10, 0)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+
+
 def test_node_cluster_spanning_every_slab(tmp_path):
     """A long horizontal band crosses every cut: the merge must chain local components across
     all ranks (diameter > 2 in the record graph)."""
