@@ -113,13 +113,19 @@ def parse(argv=None):
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every kernel timed (the breakdown)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="rehearse the N > 1 node path on one GPU: a one-rank process group and "
+                         "the node exchange's collectives run anyway (not a measurement)")
     ap.add_argument("--node", action="store_true", help="use the node path even at N = 1")
     return ap.parse_args(argv)
 
 
 def workload_defaults(args, world):
     """Fill the unset workload flags: config 2 at N = 1 (G(10^7, no noise, seed 1)); config 3
-    weak-scaled at N > 1 (1.25*10^7 points per GPU, 20% noise, seed 2: G(10^8) at N = 8)."""
+    weak-scaled at N > 1 (1.25*10^7 points per GPU, 20% noise, seed 2: G(10^8) at N = 8), and
+    for the one-GPU rehearsal of that path (--force-collectives)."""
+    if getattr(args, "force_collectives", False):
+        world = max(world, 2)
     if args.points_per_gpu is None:
         args.points_per_gpu = 12_500_000 if world > 1 else 10_000_000
     if args.noise is None:
@@ -207,7 +213,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    node_path = world > 1 or args.node
+    node_path = world > 1 or args.node or args.force_collectives
     workload_defaults(args, world)
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
@@ -216,8 +222,14 @@ def main():
 
     h = dbscan_amd.Handle(dev)
     dist = None
-    if world > 1:
+    if world > 1 or args.force_collectives:
         import torch.distributed as dist
+
+        if world == 1:  # rehearsal: a process group of one rank (no launcher)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29400 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
 
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -240,7 +252,7 @@ def main():
         from dbscan_amd import node
 
         job = node.NodeJob.synthetic(n_total, args.noise, args.dense, args.seed, args.eps,
-                                     args.min_points, h, dist)
+                                     args.min_points, h, dist, force=args.force_collectives)
 
         def step():
             return job.run()
@@ -475,6 +487,7 @@ def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x
 
     xa, ya = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
     comm = node.Comm(dist)
+    comm.force = args.force_collectives
     bounds = node.NodeJob.chunk_bounds(n_total, comm.world)
     c0, c1 = bounds[comm.rank], bounds[comm.rank + 1]
     # this rank's chunk of the global input in host memory (pageable, as a caller's arrays),

@@ -413,13 +413,14 @@ class NodeJob:
 
     @classmethod
     def synthetic(cls, n_total, noise, dense, seed, eps, min_points, handle, dist,
-                  mode: int = 0) -> "NodeJob":
+                  mode: int = 0, force: bool = False) -> "NodeJob":
         """bench.py setup: every rank generates the same G(n_total) on its GPU (device
-        generator), then keeps its slab."""
+        generator), then keeps its slab.  force: Comm.force (collectives at one rank too)."""
         from . import device as D
 
         x_all, y_all = D.generate_blobs(n_total, noise, dense, seed, handle)
         comm = Comm(dist)
+        comm.force = force
         job = cls.from_global(x_all, y_all, eps, min_points, mode, comm, HipSlabOps(handle))
         del x_all, y_all
         torch.cuda.empty_cache()
