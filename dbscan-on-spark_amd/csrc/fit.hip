@@ -2769,11 +2769,42 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
             }
         };
         if (nbr) {
+            // the whole list, then every neighbour's core flag, then the cores' labs: three
+            // rounds of loads in flight instead of a dependent pair per neighbour (the non-core
+            // lanes are each wave's longest chains)
             const int32_t* l = nbr + p * nbr_k;
-            for (int k = 0; k < nbr_k; ++k) {
-                const int j = l[k];
-                if (j < 0) break;
-                visit(j);
+            int js[kMaxNbr];
+            bool live = true;
+#pragma unroll
+            for (int k = 0; k < kMaxNbr; ++k) {
+                js[k] = -1;
+                if (k < nbr_k) js[k] = l[k];
+            }
+#pragma unroll
+            for (int k = 0; k < kMaxNbr; ++k) {  // -1 ends the list; later entries are stale
+                live = live && js[k] >= 0;
+                if (!live) js[k] = -1;
+            }
+            bool cj[kMaxNbr];
+#pragma unroll
+            for (int k = 0; k < kMaxNbr; ++k) {
+                cj[k] = false;
+                if (js[k] >= 0) cj[k] = core[js[k]] != 0;
+            }
+            int32_t lj[kMaxNbr];
+#pragma unroll
+            for (int k = 0; k < kMaxNbr; ++k) {
+                lj[k] = 0;
+                if (cj[k]) lj[k] = lab[js[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < kMaxNbr; ++k) {
+                if (!cj[k]) continue;
+                const int64_t w = SLAB ? gs_of_root[lj[k]] : (int64_t)lj[k];
+                if (w < m) {
+                    m = w;
+                    mr = lj[k];
+                }
             }
         } else {
             const double2 me = xy[p];
