@@ -391,7 +391,9 @@ def main():
                 "parallelism": ("single GPU, one local fit" if not node_path else
                                 f"x-slabs x{world} with eps halos" +
                                 (f" + {'RCCL' if args.backend == 'nccl' else args.backend} "
-                                 "all-gathers + global union-find" if world > 1 else
+                                 "all-gathers + global union-find" +
+                                 (" (one-rank rehearsal)" if world == 1 else "")
+                                 if world > 1 or args.force_collectives else
                                  " (one slab: no exchange)")),
                 "clusters": k, "core_points": stats.get("core"),
                 "occupied_cells": stats.get("cells"), "occupied_tiles": stats.get("tiles")},
