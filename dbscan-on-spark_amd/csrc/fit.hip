@@ -1444,29 +1444,38 @@ __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy
     return st.ok;
 }
 
-// One LDS range of candidates in batches of 8 (the last batch masked).  Sure hits by F <= lo,
+// One LDS range of candidates in batches of kScanBatch (the last batch masked).  Sure hits by F <= lo,
 // ambiguous ones by the exact fp64 predicate (exact(q) for LDS index q).  REC: each batch with
 // hits is noted as ONE record (first LDS index | range tag << 11 | hit bits << 16) in the
 // thread's column of lst while fewer than nbr_k records exist; a point that ends below
 // minPoints has at most minPoints - 1 hits, so its records are complete.
+// Candidates per batch: 4, the batch's tail clamped and masked once (round 2: against 8 with
+// a per-candidate select, count_wave + count_tiny 0.092 -> 0.087 ms at 10^7, 0.256 -> 0.236
+// on config 3's share; 8 in this form spilled at 80 VGPRs).  DBSCAN_AB_SCAN_BATCH: A/B builds.
+#ifndef DBSCAN_AB_SCAN_BATCH
+#define DBSCAN_AB_SCAN_BATCH 4
+#endif
+constexpr int kScanBatch = DBSCAN_AB_SCAN_BATCH;
 template <bool REC, int STRIDE = kBlock, class ExactF>
 __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
                                              float2 me, F32Cut cut, int min_points, int& cnt,
                                              uint32_t* lst, int& nrec, int nbr_k, int tag,
                                              ExactF exact) {
-    for (int j = b; j < e; j += 8) {
+    for (int j = b; j < e; j += kScanBatch) {
         const int nin = e - j;
-        float2 qq[8];
+        float2 qq[kScanBatch];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) qq[u] = buf[u < nin ? j + u : j];
+        for (int u = 0; u < kScanBatch; ++u) qq[u] = buf[min(j + u, e - 1)];  // tail masked below
         uint32_t hm = 0, am = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kScanBatch; ++u) {
             const float F = f32_d2(me, qq[u]);
-            hm |= (u < nin && F <= cut.lo) ? (1u << u) : 0u;
-            am |= (u < nin && F <= cut.hi) ? (1u << u) : 0u;
+            hm |= F <= cut.lo ? (1u << u) : 0u;
+            am |= F <= cut.hi ? (1u << u) : 0u;
         }
-        am ^= hm;
+        const uint32_t valid = nin >= kScanBatch ? (1u << kScanBatch) - 1u : (1u << nin) - 1u;
+        hm &= valid;
+        am = (am & valid) ^ hm;
         if (__builtin_expect(am != 0, 0)) {
             for (uint32_t m = am; m; m &= m - 1) {
                 const int u = __ffs(m) - 1;
