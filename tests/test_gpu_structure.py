@@ -151,3 +151,20 @@ def test_fp32_records_far_from_origin(dm, handle, offset, eps):
     x = offset + pts[:, 0]
     y = -offset + pts[:, 1]
     _check(dm, handle, x, y, eps, 8)
+
+
+@pytest.mark.parametrize("n_tiles", [1, 2, 3, 5])
+@pytest.mark.parametrize("per_tile", [9, 10, 31, 32, 33, 64, 65, 192, 193])
+def test_small_tile_buckets_and_packing(dm, handle, n_tiles, per_tile):
+    """Isolated tiles of chosen stage sizes, around the small-tile bucket edges (32 | 64 | 96 |
+    144 | 192) and the two-tiles-per-wave packing: an odd number of packed tiles leaves a wave's
+    second segment empty; 9 / 10 points straddle minPoints."""
+    rng = np.random.default_rng(n_tiles * 1000 + per_tile)
+    eps = 1.0
+    xs, ys = [], []
+    for t in range(n_tiles):  # tile centres 40 eps apart: every stage holds its own clump only
+        cx, cy = 40.0 * t + 4.0, 4.0 + 40.0 * (t % 2)
+        xs.append(cx + rng.normal(0, 0.6, per_tile))
+        ys.append(cy + rng.normal(0, 0.6, per_tile))
+    x, y = np.concatenate(xs), np.concatenate(ys)
+    _check(dm, handle, x, y, eps, 10)
