@@ -228,15 +228,6 @@ struct Heads {
     bool c, q, t;
 };
 
-__device__ __forceinline__ Heads heads_at(const uint32_t* __restrict__ key, int64_t p,
-                                          int64_t nf, uint32_t& k) {
-    if (p >= nf) return {false, false, false};
-    k = key[p];
-    if (p == 0) return {true, true, true};
-    const uint32_t km = key[p - 1];
-    return {(k >> 2) != (km >> 2), k != km, (k >> 8) != (km >> 8)};
-}
-
 // heads_reduce: each thread takes kHeadPer consecutive slots (four 16-B key loads, and the key
 // before them): 0.021 -> 0.012 ms per 10^7-point fit.  (heads_down in that form, with 16-B
 // stores of cell/qidx per thread, measured slower, 0.047 -> 0.071 ms, and keeps its rounds.)
@@ -323,10 +314,28 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
     const int w = threadIdx.x >> 6, lane = __lane_id();
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     int oc = offs[blockIdx.x], oq = offs[nb + blockIdx.x], ot = offs[2 * nb + blockIdx.x];
-    for (int r = 0; r < kHeadTile / kBlock; ++r) {
+    // every round's key (and the key before it) loaded up front: the rounds below wait on
+    // their barriers only, not on a load each
+    constexpr int R = kHeadTile / kBlock;
+    uint32_t kr[R], km[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
         const int64_t p = base + r * kBlock + threadIdx.x;
-        uint32_t k = 0;
-        const Heads h = heads_at(key, p, nf, k);
+        kr[r] = kSentinelKey;
+        if (p < nf) kr[r] = key[p];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t p = base + r * kBlock + threadIdx.x;
+        km[r] = __shfl_up(kr[r], 1, 64);
+        if (lane == 0 && p > 0 && p <= nf) km[r] = key[p - 1];
+    }
+    for (int r = 0; r < R; ++r) {
+        const int64_t p = base + r * kBlock + threadIdx.x;
+        const uint32_t k = kr[r], kmr = km[r];
+        const bool in = p < nf, first = p == 0;
+        const Heads h = {in && (first || (k >> 2) != (kmr >> 2)), in && (first || k != kmr),
+                         in && (first || (k >> 8) != (kmr >> 8))};
         const uint64_t bc = __ballot(h.c), bq = __ballot(h.q), bt = __ballot(h.t);
         if (lane == 0) {
             wcnt[r & 1][0][w] = __popcll(bc);
