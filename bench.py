@@ -104,7 +104,9 @@ def parse(argv=None):
     ap.add_argument("--eps", type=float, default=2.55)
     ap.add_argument("--min-points", type=int, default=10)
     ap.add_argument("--noise", type=float, default=None, help="default 0 (N = 1), 0.2 (N > 1)")
-    ap.add_argument("--dense", type=float, default=1.0)
+    ap.add_argument("--dense", type=float, default=None, help="default 1")
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
+                    help="BASELINE config shape (points per GPU, noise, dense, seed)")
     ap.add_argument("--seed", type=int, default=None, help="default 1 (N = 1), 2 (N > 1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: host_threads()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,15 +119,53 @@ def parse(argv=None):
                     help="rehearse the N > 1 node path on one GPU: a one-rank process group and "
                          "the node exchange's collectives run anyway (not a measurement)")
     ap.add_argument("--node", action="store_true", help="use the node path even at N = 1")
+    ap.add_argument("--no-seam", action="store_true",
+                    help="skip the seam leg (partition-sized fits and batches, N = 1)")
+    ap.add_argument("--seam-only", action="store_true", help="only the seam leg (no timed fit)")
     return ap.parse_args(argv)
 
 
+# BASELINE.json configs as G(n, noise, dense, seed) shapes: (points per GPU at
+# the config's own GPU count, noise, dense, seed, GPUs the config names).  --config C runs that
+# shape with the per-GPU share fixed (weak scaling): exactly the config at its own GPU count,
+# its per-GPU share on one GPU.
+CONFIGS = {
+    2: (10_000_000, 0.0, 1.0, 1, 1),
+    3: (12_500_000, 0.2, 1.0, 2, 8),
+    4: (50_000_000, 0.0, 8.0, 3, 1),
+    5: (125_000_000, 0.2, 1.0, 4, 8),
+}
+
+
+def workload_name(n_total, per_gpu, noise, dense, seed, world):
+    """Which BASELINE config this run is (or is the per-GPU share / weak-scaled form of)."""
+    for c, (pg, nz, dn, sd, ngpu) in CONFIGS.items():
+        if (per_gpu, float(noise), float(dense), int(seed)) != (pg, nz, dn, sd):
+            continue
+        if world == ngpu:
+            return f"config {c}"
+        if world == 1:
+            return f"config {c}'s per-GPU share (config {c} is {ngpu} GPUs x {pg})"
+        return (f"config {c} shape weak-scaled to {world} GPUs ({pg} points per GPU; config {c} "
+                f"itself at {ngpu} GPU{'s' if ngpu > 1 else ''})")
+    return "custom"
+
+
 def workload_defaults(args, world):
-    """Fill the unset workload flags: config 2 at N = 1 (G(10^7, no noise, seed 1)); config 3
-    weak-scaled at N > 1 (1.25*10^7 points per GPU, 20% noise, seed 2: G(10^8) at N = 8), and
-    for the one-GPU rehearsal of that path (--force-collectives)."""
+    """Fill the unset workload flags: --config C (BASELINE config C's shape, per-GPU share
+    fixed); else config 2 at N = 1 (G(10^7, no noise, seed 1)) and config 3 weak-scaled at
+    N > 1 (1.25*10^7 points per GPU, 20% noise, seed 2: G(10^8) at N = 8), also for the one-GPU
+    rehearsal of that path (--force-collectives)."""
     if getattr(args, "force_collectives", False):
         world = max(world, 2)
+    if getattr(args, "config", None):
+        pg, nz, dn, sd, _ = CONFIGS[args.config]
+        args.points_per_gpu = args.points_per_gpu or pg
+        args.noise = nz if args.noise is None else args.noise
+        args.dense = dn if args.dense is None else args.dense
+        args.seed = sd if args.seed is None else args.seed
+    if args.dense is None:
+        args.dense = 1.0
     if args.points_per_gpu is None:
         args.points_per_gpu = 12_500_000 if world > 1 else 10_000_000
     if args.noise is None:
@@ -221,6 +261,9 @@ def main():
     from dbscan_amd import device as D
 
     h = dbscan_amd.Handle(dev)
+    if args.seam_only:
+        print(json.dumps({"seam": seam(args, h, args.cpu_threads or host_threads())}), flush=True)
+        return
     dist = None
     if world > 1 or args.force_collectives:
         import torch.distributed as dist
@@ -358,27 +401,25 @@ def main():
         e2e = end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks,
                          x if not node_path else None, y if not node_path else None)
 
+    seam_out = None
+    if world == 1 and not node_path and not args.no_seam:
+        seam_out = seam(args, h, args.cpu_threads or host_threads())
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not node_path:
         sx, sy = x.cpu().numpy(), y.cpu().numpy()
         threads = args.cpu_threads or host_threads()
         cpu = cpu_baseline(sx, sy, args.eps, args.min_points, threads)
 
+    if node_path:
+        job.close()
     if rank == 0:
-        if world > 1 or node_path:
-            workload = (f"config 3 weak-scaled: G({n_total} points = {args.points_per_gpu} per "
-                        f"GPU x {world}, 32 Gaussian blobs, noise={args.noise}, dense="
-                        f"{args.dense}, seed={args.seed}) -- BASELINE config 3 (10^8 points, "
-                        f"20% noise, 8 GPUs) exactly at N = 8")
-        else:
-            # which BASELINE config this single fit is (or is the per-GPU share of)
-            shape = (n_total, args.noise, args.dense, args.seed)
-            name = {(10_000_000, 0.0, 1.0, 1): "config 2",
-                    (12_500_000, 0.2, 1.0, 2): "config 3's per-GPU share",
-                    (50_000_000, 0.0, 8.0, 3): "config 4",
-                    (125_000_000, 0.2, 1.0, 4): "config 5's per-GPU share"}.get(shape, "custom")
-            workload = (f"{name}: G({n_total} points, 32 Gaussian blobs, noise={args.noise}, "
-                        f"dense={args.dense}, seed={args.seed})")
+        name = workload_name(n_total, args.points_per_gpu, args.noise, args.dense, args.seed,
+                             world)
+        workload = (f"{name}: G({n_total} points" +
+                    (f" = {args.points_per_gpu} per GPU x {world}" if world > 1 else "") +
+                    f", 32 Gaussian blobs, noise={args.noise}, dense={args.dense}, "
+                    f"seed={args.seed})")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "points/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -400,6 +441,7 @@ def main():
             "roofline": roof,
             "valu": valu,
             "end_to_end": e2e,
+            "seam": seam_out,
             "cpu_baseline": cpu,
             "kernels_ms_per_step": {k2: round(v, 4) for k2, v in
                                     sorted(kernels.items(), key=lambda kv: -kv[1])},
@@ -410,6 +452,132 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def seam(args, h, threads):
+    """The seam's real call pattern (DBSCAN.scala:150-155: one LocalDBSCANNaive.fit per spatial
+    partition of <= maxPointsPerPartition points + eps halo).
+      per_call   one fit of m points per call, m in 250 / 2k / 8k / 64k: dbscan_fit_h (host
+                 arrays, PCIe included) and dbscan_fit_device (device-resident, synchronous),
+                 median of repeated calls; m <= 8192 runs the one-workgroup kernel (small.hip),
+                 'tiled' is the same call through the tiled pipeline (dbscan_set_small_max 0)
+      train      G(10^7) (config 2) cut by the reference's EvenSplitPartitioner with
+                 maxPointsPerPartition 8192 and duplicated into eps-grown partitions
+                 (DBSCAN.scala:105-137): every partition fitted (a) by one dbscan_fit_h call each
+                 (one executor thread calling the seam per partition), (b) as ONE
+                 dbscan_fit_batch call (host arrays), (c) device-resident
+                 (dbscan_fit_batch_device_async, back to back), against (d) the reference's
+                 LocalDBSCANNaive.fit O(m^2) restated in C on the same partitions, `threads`
+                 host threads, for a bounded sample of partitions."""
+    import numpy as np
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import device as D
+
+    out = {"per_call": {}}
+    eps, mp = args.eps, args.min_points
+    for m in (250, 2000, 8192, 65536):
+        tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
+        hx, hy = tx.cpu().numpy(), ty.cpu().numpy()
+        cl = np.ones(m, np.int32)
+        fl = np.ones(m, np.uint8)
+        dcl = torch.empty(m, dtype=torch.int32, device="cuda")
+        dfl = torch.empty(m, dtype=torch.uint8, device="cuda")
+        row = {}
+        for tag, small in (("", 8192), ("tiled_", 0)):
+            if small == 0 and m > 8192:
+                continue
+            h.set_small_max(small)
+            reps = 30 if m <= 8192 else 10
+            for kind in ("host", "device"):
+                ts = []
+                for i in range(reps + 2):
+                    t0 = time.perf_counter()
+                    if kind == "host":
+                        dbscan_amd.fit_arrays(hx, hy, eps, mp, 0, handle=h, cluster_out=cl,
+                                              flag_out=fl)
+                    else:
+                        D.fit_tensors(tx, ty, eps, mp, 0, h, dcl, dfl)
+                    if i >= 2:
+                        ts.append(time.perf_counter() - t0)
+                row[f"{tag}{kind}_us"] = round(float(np.median(ts)) * 1e6, 1)
+        h.set_small_max(8192)
+        out["per_call"][str(m)] = row
+
+    n = 10_000_000
+    tx, ty = D.generate_blobs(n, 0.0, 1.0, 1, h)
+    x, y = tx.cpu().numpy(), ty.cpu().numpy()
+    del tx, ty
+    parts = dbscan_amd.partition.partition_points(x, y, eps, 8192, h)
+    rects = np.array([r for r, _ in parts])
+    counts = np.array([c for _, c in parts], np.int64)
+    offs, idx = dbscan_amd.duplicate(x, y, rects, eps)
+    px, py = x[idx], y[idx]
+    sizes = np.diff(offs)
+    npart, total = len(sizes), int(offs[-1])
+    cl = np.ones(total, np.int32)
+    fl = np.ones(total, np.uint8)
+    # (a) one seam call per partition, one thread
+    t0 = time.perf_counter()
+    for p in range(npart):
+        a, b = offs[p], offs[p + 1]
+        dbscan_amd.fit_arrays(px[a:b], py[a:b], eps, mp, 0, handle=h, cluster_out=cl[a:b],
+                              flag_out=fl[a:b])
+    t_calls = time.perf_counter() - t0
+    # (b) one batch call, host arrays
+    ts = []
+    for i in range(4):
+        t0 = time.perf_counter()
+        dbscan_amd.fit_batch(px, py, offs, eps, mp, 0, handle=h, cluster_out=cl, flag_out=fl)
+        if i:
+            ts.append(time.perf_counter() - t0)
+    t_batch = float(np.median(ts))
+    # (c) device-resident batches, back to back
+    dx, dy = torch.from_numpy(px).cuda(), torch.from_numpy(py).cuda()
+    dcl = torch.empty(total, dtype=torch.int32, device="cuda")
+    dfl = torch.empty(total, dtype=torch.uint8, device="cuda")
+    dnk = torch.empty(npart, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    D.fit_batch_tensors_async(dx, dy, offs, eps, mp, 0, h, dcl, dfl, dnk)
+    h.sync()
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        D.fit_batch_tensors_async(dx, dy, offs, eps, mp, 0, h, dcl, dfl, dnk)
+    h.sync()
+    t_dev = (time.perf_counter() - t0) / reps
+    same = bool(np.array_equal(dcl.cpu().numpy(), cl) and np.array_equal(dfl.cpu().numpy(), fl))
+    del dx, dy, dcl, dfl
+    torch.cuda.empty_cache()
+    out["train"] = {
+        "workload": (f"G(10^7) config 2 -> EvenSplitPartitioner(maxPointsPerPartition=8192): "
+                     f"{npart} partitions, {total} points with eps halos (max {int(sizes.max())}, "
+                     f"{int((sizes > 8192).sum())} over the one-workgroup capacity)"),
+        "partitions": npart, "points_with_halos": total,
+        "per_partition_calls": {"seconds": round(t_calls, 4),
+                                "us_per_partition": round(t_calls / npart * 1e6, 2)},
+        "batch_host": {"seconds": round(t_batch, 4),
+                       "us_per_partition": round(t_batch / npart * 1e6, 3),
+                       "points_per_s": round(total / t_batch, 1)},
+        "batch_device": {"ms": round(t_dev * 1e3, 4),
+                         "us_per_partition": round(t_dev / npart * 1e6, 3),
+                         "points_per_s": round(total / t_dev, 1), "equals_host_batch": same},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg only
+
+        r = O.ref_fit_partitions_timed(x, y, eps, mp, rects, counts, threads, 8.0)
+        out["train"]["cpu_reference_fits"] = {
+            "threads": threads, "seconds": round(r["seconds"], 3), "partitions": r["parts"],
+            "points_with_halos": r["outer_points"],
+            "us_per_partition": round(r["seconds"] / max(1, r["parts"]) * 1e6, 1),
+            "points_per_s": round(r["outer_points"] / max(r["seconds"], 1e-9), 1),
+            "what": ("LocalDBSCANNaive.fit O(m^2) restated in C (oracle/reference_pipeline.c) on "
+                     "the same partitions, a thread pool of `threads`, stopped after an 8 s "
+                     "budget (a sample of the partitions)")}
+    return out
 
 
 def end_to_end(args, h, dist, world, rank, n_total, node_path, max_over_ranks, x, y):

@@ -180,6 +180,11 @@ struct dbscan_handle {
     dbscan::FitStats stats;
     dbscan::SlabState slab;
     dbscan::DevBuf hx, hy, hcl, hfl;  // staging for the host-array entry points
+    dbscan::DevBuf boffs, hnk;        // batch fits: offsets + small-partition list; counts
+    void* bpinned = nullptr;          // pinned staging of the batch tables (grow-only)
+    size_t bpinned_bytes = 0;
+    hipEvent_t bcopied = nullptr;     // the last batch tables' upload (pinned buffer reusable)
+    int64_t small_max = dbscan::kSmallMaxPoints;  // one-workgroup fits up to this many points
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
@@ -300,6 +305,10 @@ void dbscan_destroy(dbscan_handle* h) {
     h->hy.release();
     h->hcl.release();
     h->hfl.release();
+    h->boffs.release();
+    h->hnk.release();
+    if (h->bpinned) (void)hipHostFree(h->bpinned);
+    if (h->bcopied) (void)hipEventDestroy(h->bcopied);
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->ready) (void)hipEventDestroy(h->ready);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -349,6 +358,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         h->pending = false;  // a newer fit replaces the unread stats of an older one
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
+        a.small_max = h->small_max;
         h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
@@ -383,6 +393,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
         check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag, true);
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
+        a.small_max = h->small_max;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
@@ -414,6 +425,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
+        a.small_max = h->small_max;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
@@ -832,6 +844,167 @@ int32_t dbscan_profile_read(dbscan_handle* h, char* names, int32_t names_cap, do
         ++k;
     }
     return k;
+}
+
+int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int64_t prev = h->small_max;
+    h->small_max = std::min<int64_t>(std::max<int64_t>(max_points, 0), dbscan::kSmallMaxPoints);
+    return prev;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Validates a batch's offsets (n_parts + 1 non-decreasing, >= 0) and returns the total span.
+int64_t batch_span(const int64_t* offsets, int32_t n_parts) {
+    if (n_parts < 0) throw dbscan::ArgError{"n_parts < 0"};
+    if (!offsets) throw dbscan::ArgError{"NULL offsets"};
+    if (offsets[0] < 0) throw dbscan::ArgError{"offsets[0] < 0"};
+    for (int32_t p = 0; p < n_parts; ++p)
+        if (offsets[p + 1] < offsets[p]) throw dbscan::ArgError{"offsets must not decrease"};
+    if (offsets[n_parts] > DBSCAN_MAX_POINTS) throw dbscan::ArgError{"too many points"};
+    return offsets[n_parts];
+}
+
+// Enqueues one batch on the handle's stream (device arrays indexed like the offsets, host
+// offsets): the partitions the one-workgroup kernel serves in ONE launch, the others through the
+// tiled pipeline one after another (stream-ordered on the handle's workspace).
+void batch_enqueue(dbscan_handle* h, const double* dx, const double* dy, const int64_t* offs,
+                   int32_t n_parts, double eps, int32_t min_points, int32_t mode, int32_t* dcl,
+                   uint8_t* dfl, int32_t* dnk) {
+    const int64_t cap = std::min<int64_t>(h->small_max, dbscan::kSmallMaxPoints);
+    std::vector<int32_t> small, big;
+    for (int32_t p = 0; p < n_parts; ++p) {
+        const int64_t m = offs[p + 1] - offs[p];
+        if (m <= cap && dbscan::small_fit_eligible(m, eps, mode)) small.push_back(p);
+        else big.push_back(p);
+    }
+    if (!small.empty()) {
+        const size_t need = (size_t)(n_parts + 1) * sizeof(int64_t) + small.size() * sizeof(int32_t);
+        if (!h->bcopied) DBSCAN_HIP_CHECK(hipEventCreateWithFlags(&h->bcopied, hipEventDisableTiming));
+        else DBSCAN_HIP_CHECK(hipEventSynchronize(h->bcopied));  // the pinned tables are free
+        if (h->bpinned_bytes < need) {
+            if (h->bpinned) (void)hipHostFree(h->bpinned);
+            h->bpinned = nullptr;
+            h->bpinned_bytes = 0;
+            DBSCAN_HIP_CHECK(hipHostMalloc(&h->bpinned, need + need / 2, hipHostMallocDefault));
+            h->bpinned_bytes = need + need / 2;
+        }
+        char* pin = static_cast<char*>(h->bpinned);
+        memcpy(pin, offs, (size_t)(n_parts + 1) * sizeof(int64_t));
+        memcpy(pin + (size_t)(n_parts + 1) * sizeof(int64_t), small.data(),
+               small.size() * sizeof(int32_t));
+        char* dev = static_cast<char*>(h->boffs.ensure(need));
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(dev, pin, need, hipMemcpyHostToDevice, h->stream));
+        DBSCAN_HIP_CHECK(hipEventRecord(h->bcopied, h->stream));
+        dbscan::enqueue_small_fits(
+            h->stream, &h->prof, dx, dy, reinterpret_cast<const int64_t*>(dev),
+            reinterpret_cast<const int32_t*>(dev + (size_t)(n_parts + 1) * sizeof(int64_t)),
+            (int32_t)small.size(), 0, eps, min_points, mode, dcl, dfl, dnk, nullptr, nullptr);
+    }
+    h->pending = false;
+    for (int32_t p : big) {
+        const int64_t o = offs[p], m = offs[p + 1] - o;
+        dbscan::FitArgs a{dx + o, dy + o, nullptr, m, eps, min_points, mode, dcl + o, dfl + o,
+                          nullptr, nullptr};
+        a.small_max = 0;
+        dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+        dbscan::write_nclusters(h->stream, h->ws, dnk + p);
+        h->pending = true;
+    }
+    if (!h->pending) {
+        h->stats = dbscan::FitStats();
+        h->stats.n = offs[n_parts] - offs[0];
+    }
+    h->prepared = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t dbscan_fit_batch_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                      const int64_t* offsets, int32_t n_parts, double eps,
+                                      int32_t min_points, int32_t mode, int32_t* d_cluster,
+                                      uint8_t* d_flag, int32_t* d_n_clusters) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        const int64_t span = batch_span(offsets, n_parts);
+        check_fit_args(span, eps, mode, d_x, d_y, d_cluster, d_flag, true);
+        if (n_parts > 0 && !d_n_clusters) throw dbscan::ArgError{"NULL n_clusters array"};
+        if (h->pending && h->prof.pending.size() > 4096) settle(h);
+        batch_enqueue(h, d_x, d_y, offsets, n_parts, eps, min_points, mode, d_cluster, d_flag,
+                      d_n_clusters);
+        return DBSCAN_OK;
+    });
+}
+
+int32_t dbscan_fit_batch(dbscan_handle* h, const double* x, const double* y,
+                         const int64_t* offsets, int32_t n_parts, double eps, int32_t min_points,
+                         int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                         int32_t* n_clusters_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        settle(h);
+        const int64_t span = batch_span(offsets, n_parts);
+        check_fit_args(span, eps, mode, x, y, cluster_out, flag_out, true);
+        if (n_parts > 0 && !n_clusters_out) throw dbscan::ArgError{"NULL n_clusters_out"};
+        if (n_parts == 0) return DBSCAN_OK;
+        const int64_t o0 = offsets[0], n = span - o0;
+        std::vector<int64_t> rel((size_t)n_parts + 1);
+        for (int32_t p = 0; p <= n_parts; ++p) rel[(size_t)p] = offsets[p] - o0;
+        const size_t nn = (size_t)std::max<int64_t>(n, 1);
+        double* dx = static_cast<double*>(h->hx.ensure(nn * sizeof(double)));
+        double* dy = static_cast<double*>(h->hy.ensure(nn * sizeof(double)));
+        int32_t* dcl = static_cast<int32_t*>(h->hcl.ensure(nn * sizeof(int32_t)));
+        uint8_t* dfl = static_cast<uint8_t*>(h->hfl.ensure(nn));
+        int32_t* dnk = static_cast<int32_t*>(h->hnk.ensure((size_t)n_parts * sizeof(int32_t)));
+        if (n > 0) {
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x + o0, n * sizeof(double), hipMemcpyHostToDevice,
+                                            h->stream));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y + o0, n * sizeof(double), hipMemcpyHostToDevice,
+                                            h->stream));
+        }
+        batch_enqueue(h, dx, dy, rel.data(), n_parts, eps, min_points, mode, dcl, dfl, dnk);
+        if (n > 0) {
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out + o0, dcl, n * sizeof(int32_t),
+                                            hipMemcpyDeviceToHost, h->stream));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(flag_out + o0, dfl, n, hipMemcpyDeviceToHost,
+                                            h->stream));
+        }
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(n_clusters_out, dnk, (size_t)n_parts * sizeof(int32_t),
+                                        hipMemcpyDeviceToHost, h->stream));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        settle(h);
+        h->prof.flush();
+        return DBSCAN_OK;
+    });
+}
+
+int64_t dbscan_duplicate(const double* x, const double* y, int64_t n, const double* rects,
+                         int64_t n_parts, double eps, int64_t* offsets_out, int64_t* index_out,
+                         int64_t capacity) {
+    return guarded64(nullptr, [&]() -> int64_t {
+        if (n < 0 || n_parts < 0 || capacity < 0 || !offsets_out || (n > 0 && (!x || !y)) ||
+            (n_parts > 0 && !rects))
+            throw dbscan::ArgError{"bad duplicate arguments"};
+        return dbscan::duplicate_points(x, y, n, rects, n_parts, eps, offsets_out, index_out,
+                                        capacity);
+    });
 }
 
 int32_t dbscan_generate_blobs_device(dbscan_handle* h, double* d_x, double* d_y, int64_t n,

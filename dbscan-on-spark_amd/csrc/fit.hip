@@ -59,7 +59,7 @@ constexpr int kQReg = 4;          // own-quarter core points kept in registers f
 constexpr int64_t kTileGrid = 8192;  // workgroups of the per-tile kernels (grid stride)
 constexpr int kMaxNbr = 11;  // neighbour lists of non-cores kept while minPoints - 1 <= this
 constexpr int32_t kModeArcheryBox = 2;     // DBSCAN_MODE_ARCHERY_F32BOX
-constexpr int64_t kBoxEdgeCap = 1 << 22;   // one-way core-core pairs a box fit can hold
+constexpr int64_t kBoxEdgeCap = 1 << 20;   // initial capacity for one-way core pairs (grows)
 
 // DBSCAN_AB_STAMPS (timing builds only, never the shipped library): the per-tile kernels' wave 0
 // records the constant-rate clock (100 MHz) at its phase boundaries, per workgroup, read back by
@@ -2920,15 +2920,12 @@ __global__ __launch_bounds__(kBlock) void box_count_kernel(
     }
 }
 
-// Core-core pairs: both directions -> union (once, from the larger slot); one direction only
-// -> the directed pair (source slot, target slot) is recorded by its source, up to `cap`
-// (the count keeps growing past it, so an overflow is detected on the host).
+// Core-core pairs that hold in both directions -> union (once, from the larger slot).
 __global__ __launch_bounds__(kBlock) void box_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, double eps, double eps2,
     const int32_t* __restrict__ perm, const uint8_t* __restrict__ core,
-    int32_t* __restrict__ parent, int2* __restrict__ edges, int32_t* __restrict__ n_edges,
-    int32_t cap) {
+    int32_t* __restrict__ parent) {
     const int64_t nf = *nf_p;
     for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
          p += (int64_t)gridDim.x * kBlock) {
@@ -2937,18 +2934,40 @@ __global__ __launch_bounds__(kBlock) void box_union_kernel(
         const Seg s = load_seg(seg, cell[p]);
         int rp = uf_find(parent, (int)p);
         for_candidates(s, [&](int j) {
-            if (j == (int)p || !core[j]) return true;
+            if (j >= (int)p || !core[j]) return true;
             const double2 q = xy[j];
             if (!within_eps(me.x, me.y, q.x, q.y, eps2)) return true;
-            const bool fwd = in_f32_box(me.x, me.y, q.x, q.y, eps);  // q in N(p)
-            const bool bwd = in_f32_box(q.x, q.y, me.x, me.y, eps);  // p in N(q)
-            if (fwd && bwd) {
-                if (j < (int)p) {
-                    const int rj = uf_find(parent, j);
-                    if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
-                }
-            } else if (fwd) {
-                const int k = atomicAdd(n_edges, 1);
+            if (in_f32_box(me.x, me.y, q.x, q.y, eps) && in_f32_box(q.x, q.y, me.x, me.y, eps)) {
+                const int rj = uf_find(parent, j);
+                if (rj != rp) rp = uf_unite_roots(parent, perm, rp, rj);
+            }
+            return true;
+        });
+    }
+}
+
+// After the components are final (lab = s(K) of every core): the one-way core-core pairs
+// (q in N(p), p not in N(q)) whose two ends lie in DIFFERENT components -- the only ones that
+// carry information -- recorded as (source slot, target slot) while fewer than `cap` exist.
+// The 64-bit count keeps growing past cap, so the host can size the buffer and run this again.
+__global__ __launch_bounds__(kBlock) void box_pairs_kernel(
+    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
+    const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, double eps, double eps2,
+    const uint8_t* __restrict__ core, const int32_t* __restrict__ lab, int2* __restrict__ edges,
+    unsigned long long* __restrict__ n_edges, unsigned long long cap) {
+    const int64_t nf = *nf_p;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
+         p += (int64_t)gridDim.x * kBlock) {
+        if (!core[p]) continue;
+        const double2 me = xy[p];
+        const Seg s = load_seg(seg, cell[p]);
+        const int32_t lp = lab[p];
+        for_candidates(s, [&](int j) {
+            if (j == (int)p || !core[j] || lab[j] == lp) return true;
+            const double2 q = xy[j];
+            if (!within_eps(me.x, me.y, q.x, q.y, eps2)) return true;
+            if (in_f32_box(me.x, me.y, q.x, q.y, eps) && !in_f32_box(q.x, q.y, me.x, me.y, eps)) {
+                const unsigned long long k = atomicAdd(n_edges, 1ull);
                 if (k < cap) edges[k] = make_int2((int)p, j);
             }
             return true;
@@ -3227,18 +3246,39 @@ constexpr int kCap32 = DBSCAN_AB_CAP32;
 // graph: components in s order; an unclaimed one opens the next cluster, which then claims every
 // unclaimed component reachable over one-way pairs (LocalDBSCANArchery.scala:45-63, 82-110).
 // The only host synchronization of a fit, and only in this mode.
-static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* st, const int32_t* lab,
-                                 const uint64_t* root_bits, const int32_t* word_rank) {
+static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* st,
+                                        const int32_t* lab, const uint64_t* root_bits,
+                                        const int32_t* word_rank, const double2* xy,
+                                        const int32_t* cell, const Seg* seg,
+                                        const int32_t* nf_p, int64_t n, double eps, double eps2,
+                                        const uint8_t* core) {
+    int64_t cap = std::max<int64_t>(kBoxEdgeCap, (int64_t)(ws.box_edges.bytes / (2 * sizeof(int2))));
+    unsigned long long m = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        char* buf = static_cast<char*>(ws.box_edges.ensure(2 * cap * sizeof(int2) + 64));
+        auto* cnt = reinterpret_cast<unsigned long long*>(buf);
+        int2* edges = reinterpret_cast<int2*>(buf + 64);
+        DBSCAN_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(*cnt), s));
+        hipLaunchKernelGGL(box_pairs_kernel, dim3(std::min(nblk(n), 4096u)), dim3(kBlock), 0, s,
+                           xy, cell, seg, nf_p, eps, eps2, core, lab, edges, cnt,
+                           (unsigned long long)cap);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(&m, cnt, sizeof(m), hipMemcpyDeviceToHost, s));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        if (m <= (unsigned long long)cap) break;
+        if (m > (unsigned long long)INT32_MAX)
+            throw ArgError{"archery float32 box: more than 2^31 one-way core pairs"};
+        cap = (int64_t)m;  // one more pass records every pair (the count is exact)
+    }
     int32_t hst[kStCount];
     DBSCAN_HIP_CHECK(hipMemcpyAsync(hst, st, sizeof(hst), hipMemcpyDeviceToHost, s));
     DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-    const int64_t m = hst[kStBoxEdges], k = hst[kStClusters];
+    const int64_t k = hst[kStClusters];
     if (m == 0) return nullptr;
-    if (m > kBoxEdgeCap)
-        throw ArgError{"archery float32 box: more one-way core pairs than the library holds"};
-    int2* edges = static_cast<int2*>(ws.box_edges.p);
-    int2* ranks = edges + kBoxEdgeCap;
-    hipLaunchKernelGGL(box_edge_ranks_kernel, dim3(nblk(m)), dim3(kBlock), 0, s, edges,
+    char* buf = static_cast<char*>(ws.box_edges.p);
+    int2* edges = reinterpret_cast<int2*>(buf + 64);
+    int2* ranks = edges + cap;
+    hipLaunchKernelGGL(box_edge_ranks_kernel, dim3(nblk((int64_t)m)), dim3(kBlock), 0, s, edges,
                        (int32_t)m, lab, root_bits, word_rank, ranks);
     DBSCAN_HIP_CHECK(hipGetLastError());
     std::vector<int2> e((size_t)m);
@@ -3310,6 +3350,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         return;
     }
     const int32_t* nf_p = &st[kStNf];
+    // partition-sized full fits (the seam's usual call, DBSCAN.scala:150-155): one launch,
+    // one workgroup, everything in LDS (small.hip)
+    if (!a.zone && n <= std::min<int64_t>(a.small_max, kSmallMaxPoints) &&
+        small_fit_eligible(n, a.eps, a.mode)) {
+        StageTimer t(prof, s, "small_fit");
+        enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
+                           a.mode, a.cluster, a.flag, nullptr, gp, st);
+        return;
+    }
 
     uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
     uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
@@ -3606,10 +3655,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
         StageTimer t(prof, s, "union");
         if (box) {
-            int2* edges = static_cast<int2*>(ws.box_edges.ensure(2 * kBoxEdgeCap * sizeof(int2)));
             klaunch(prof, "box_union", box_union_kernel, dim3(std::min(nblk(n), 4096u)),
-                    dim3(kBlock), 0, s, xy, cell, seg, nf_p, a.eps, eps2, perm, core, parent,
-                    edges, &st[kStBoxEdges], (int32_t)kBoxEdgeCap);
+                    dim3(kBlock), 0, s, xy, cell, seg, nf_p, a.eps, eps2, perm, core, parent);
         } else {
             // (a no-op on clique grids: a grid that just fills the GPU once)
             klaunch(prof, "union", union_kernel, dim3(std::min(nblk(n), 2048u)), dim3(kBlock), 0,
@@ -3636,7 +3683,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         if (box) {
             StageTimer t(prof, s, "output");
-            const int32_t* cmap = resolve_box_pairs(s, ws, st, lab, root_bits, word_rank);
+            const int32_t* cmap = resolve_box_pairs(s, ws, st, lab, root_bits, word_rank, xy,
+                                                    cell, seg, nf_p, n, a.eps, eps2, core);
             uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
             klaunch(prof, "box_label", box_label_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                     cell, seg, nf_p, n, a.eps, eps2, core, lab, root_bits, word_rank, cmap,

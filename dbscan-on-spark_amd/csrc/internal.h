@@ -37,6 +37,8 @@ namespace dbscan {
 constexpr uint32_t kSentinelKey = 0xFFFFFFFFu;
 constexpr int kBlock = 256;
 constexpr int64_t kMaxGridTiles = int64_t(1) << 23;  // 8x8-cell tiles per grid (u32 keys)
+// Partitions of at most this many points are fitted by ONE workgroup in LDS (small.hip)
+constexpr int64_t kSmallMaxPoints = 8192;
 
 // Device-side fit state (ints after the grid in the handle's misc buffer), written by kernels
 // and read back by the host only when it synchronizes.
@@ -201,6 +203,9 @@ struct FitArgs {
     // permutation of the per-point roots to slab order)
     const int64_t* shared_idx = nullptr;
     int64_t n_shared = 0;
+    // full fits of n <= small_max points (and a mode / eps the one-workgroup kernel serves) run
+    // small.hip's single-launch fit; 0 keeps every fit on the tiled pipeline
+    int64_t small_max = kSmallMaxPoints;
 };
 
 // What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).
@@ -281,6 +286,24 @@ void enqueue_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uin
                               const int64_t* gid, const int32_t* root, const int32_t* parent,
                               int64_t* gs_of_root, int64_t* own_roots, int32_t* total_dst,
                               int32_t* lroots);
+
+// ---- one-workgroup fits (small.hip) ----
+// Can small_fit_kernel fit n points with this eps / mode (finite eps*eps, Naive or Archery)?
+bool small_fit_eligible(int64_t n, double eps, int32_t mode);
+// d_offs == nullptr: one fit of single_n points (x, y, cluster, flag from index 0), its cluster
+// count and statistics into st / gp (the handle's fit state).  Else one workgroup per listed
+// partition: d_list[i] indexes d_offs (partition p = points [d_offs[p], d_offs[p+1]), each of
+// <= kSmallMaxPoints), cluster counts into d_nclusters[p].
+void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const double* y,
+                        const int64_t* d_offs, const int32_t* d_list, int32_t nlist,
+                        int64_t single_n, double eps, int32_t min_points, int32_t mode,
+                        int32_t* cluster, uint8_t* flag, int32_t* d_nclusters, GridParams* gp,
+                        int32_t* st);
+// DBSCAN.scala:116-137 on the host: the points every partition's outer rectangle (main grown
+// by eps, inclusive) holds, in input order (partition.hip)
+int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,
+                         int64_t n_parts, double eps, int64_t* offsets_out, int64_t* index_out,
+                         int64_t capacity);
 
 // ---- primitives (primitives.hip) ----
 // Exclusive scan of int32 values produced by `mode`:

@@ -482,6 +482,9 @@ int64_t scala_range_count(double start, double end, double step, bool inclusive)
     const bool upward = start < end, pos_step = step > 0.0;
     if (upward != pos_step) return 0;
     const double diff = end - start;  // Numeric.DoubleIsConflicted.minus (Double arithmetic)
+    // BigDecimal(Double.toString(v)) throws NumberFormatException for "Infinity" / "NaN"
+    if (!std::isfinite(diff) || !std::isfinite(step))
+        throw ArgError{"NumericRange: BigDecimal of a non-finite Double (NumberFormatException)"};
     Big D, S;
     int a, b;
     bool nd, ns;
@@ -521,12 +524,13 @@ int64_t scala_range_count(double start, double end, double step, bool inclusive)
     if (c > 0 || (c == 0 && qv.odd())) qv = Big::add(qv, Big(1));
     const std::string s = qv.decimal() + "e" + std::to_string(-t);
     const double qd = strtod(s.c_str(), nullptr);
-    int64_t jumps;
-    if (std::isnan(qd)) jumps = 0;
-    else if (qd >= 9.2233720368547758e18) jumps = INT64_MAX;
-    else jumps = (int64_t)qd;  // Double.toLong: truncation
+    // Double.toLong truncates; any count past Int.MaxValue throws in the reference (Java's
+    // long overflow of jumps + 1 included), so check before adding
+    if (!(qd < 2147483648.0))
+        throw ArgError{"NumericRange: seqs cannot contain more than Int.MaxValue elements."};
+    const int64_t jumps = qd > 0 ? (int64_t)qd : 0;
     const int64_t count = jumps + ((!inclusive && exact) ? 0 : 1);
-    if (count > INT32_MAX || count < 0)
+    if (count > INT32_MAX)
         throw ArgError{"NumericRange: seqs cannot contain more than Int.MaxValue elements."};
     return count;
 }

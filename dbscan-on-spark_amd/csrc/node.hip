@@ -5,8 +5,11 @@
 //                          -> n_shards x-slabs at count quantiles snapped to the 2*eps grid,
 //                             each with its 2-zone halo (node.py: make_cuts, zones)
 //   DBSCAN.scala:150-155   LocalDBSCANNaive.fit per partition
-//                          -> dbscan_slab_fit_device per shard, one host thread and one handle
-//                             (HIP stream) per shard, shard s on device s % device_count
+//                          -> dbscan_slab_fit_device per shard, shard s on device
+//                             s % device_count, one host thread and one handle (HIP stream) per
+//                             device; shards sharing a device run one after another on its
+//                             handle and are re-fitted before their label (one workspace per
+//                             device, so 8 shards of 10^9 points fit one GPU's HBM)
 //   DBSCAN.scala:158-222   band points, findAdjacencies, DBSCANGraph, global ids
 //                          -> records (gid of a shared core, gid of its local root) merged by a
 //                             host union-find (the records are a thin band: O(1e5) at 1e8 pts),
@@ -74,7 +77,6 @@ struct Shard {
     std::vector<int64_t> gs;      // global s(K) per local root
     std::vector<int32_t> cluster;
     std::vector<uint8_t> flag;
-    dbscan_handle* h = nullptr;
     std::string err;
     int32_t rc = DBSCAN_OK;
 };
@@ -105,57 +107,76 @@ uint8_t zone_of(double x, int r, int world, const std::vector<double>& cuts, dou
     return z;
 }
 
-// Phase 1 of one shard on its own handle/device: upload, slab fit, root back to the host.
-void shard_fit(Shard& s, int device, double eps, int32_t min_points) {
-    s.h = dbscan_create(device);
-    if (!s.h) {
-        s.rc = DBSCAN_EHIP;
-        s.err = dbscan_last_error();
-        return;
+// Uploads a shard and runs its slab fit on handle h (device buffers returned in *dev, freed by
+// the caller).  Phase 1 reads the roots back; phase 2 re-fits on a handle that held other
+// shards meanwhile (the fit is deterministic) and then labels.
+struct ShardDev {
+    double *x = nullptr, *y = nullptr;
+    uint8_t *zone = nullptr, *core = nullptr;
+    int32_t* root = nullptr;
+    void release() {
+        for (void* p : {(void*)x, (void*)y, (void*)zone, (void*)core, (void*)root}) (void)hipFree(p);
+        *this = ShardDev();
     }
+};
+
+bool shard_upload_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points,
+                      ShardDev* d) {
     const int64_t m = (int64_t)s.gid.size();
-    s.root.assign(m, -1);
-    if (m == 0) return;
-    double *dx = nullptr, *dy = nullptr;
-    uint8_t *dz = nullptr, *dcore = nullptr;
-    int32_t* droot = nullptr;
     auto fail = [&](hipError_t e, const char* what) {
         s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
         s.err = std::string(what) + ": " + hipGetErrorString(e);
+        return false;
     };
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&dx, m * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&dy, m * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&dz, m);
-    if (e == hipSuccess) e = hipMalloc(&dcore, m);
-    if (e == hipSuccess) e = hipMalloc(&droot, m * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMemcpy(dx, s.x.data(), m * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dy, s.y.data(), m * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dz, s.zone.data(), m, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        fail(e, "shard upload");
-    } else {
-        s.rc = dbscan_slab_fit_device(s.h, dx, dy, dz, m, eps, min_points, dcore, droot);
-        if (s.rc != DBSCAN_OK) {
-            s.err = dbscan_last_error();
-        } else {
-            e = hipMemcpy(s.root.data(), droot, m * sizeof(int32_t), hipMemcpyDeviceToHost);
-            if (e != hipSuccess) fail(e, "shard download");
-        }
+    if (e == hipSuccess) e = hipMalloc(&d->x, m * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&d->y, m * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&d->zone, m);
+    if (e == hipSuccess) e = hipMalloc(&d->core, m);
+    if (e == hipSuccess) e = hipMalloc(&d->root, m * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemcpy(d->x, s.x.data(), m * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d->y, s.y.data(), m * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d->zone, s.zone.data(), m, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(e, "shard upload");
+    s.rc = dbscan_slab_fit_device(h, d->x, d->y, d->zone, m, eps, min_points, d->core, d->root);
+    if (s.rc != DBSCAN_OK) {
+        s.err = dbscan_last_error();
+        return false;
     }
-    (void)hipFree(dx);
-    (void)hipFree(dy);
-    (void)hipFree(dz);
-    (void)hipFree(dcore);
-    (void)hipFree(droot);
+    return true;
 }
 
-// Phase 2: labels of the shard's zone-0 points from the merged component ids.
-void shard_label(Shard& s, int device, const std::vector<int64_t>& all_roots, int32_t mode) {
+// Phase 1 of one shard: slab fit, roots back to the host.
+void shard_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points) {
+    const int64_t m = (int64_t)s.gid.size();
+    s.root.assign(m, -1);
+    if (m == 0) return;
+    ShardDev d;
+    if (shard_upload_fit(s, h, device, eps, min_points, &d)) {
+        const hipError_t e =
+            hipMemcpy(s.root.data(), d.root, m * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            s.rc = DBSCAN_EHIP;
+            s.err = std::string("shard download: ") + hipGetErrorString(e);
+        }
+    }
+    d.release();
+}
+
+// Phase 2: labels of the shard's zone-0 points from the merged component ids.  refit: the
+// handle's last slab fit was another shard's (shards sharing a device run one after another on
+// one handle, so a device holds one workspace, not one per shard).
+void shard_label(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points,
+                 const std::vector<int64_t>& all_roots, int32_t mode, bool refit) {
     const int64_t m = (int64_t)s.gid.size();
     s.cluster.assign(m, 0);
     s.flag.assign(m, DBSCAN_FLAG_NOT_FLAGGED);
     if (m == 0) return;
+    ShardDev fitd;
+    if (refit && !shard_upload_fit(s, h, device, eps, min_points, &fitd)) {
+        fitd.release();
+        return;
+    }
     uint8_t *dz = nullptr, *dfl = nullptr;
     int64_t *dgid = nullptr, *dgs = nullptr, *droots = nullptr;
     int32_t* dcl = nullptr;
@@ -178,7 +199,7 @@ void shard_label(Shard& s, int device, const std::vector<int64_t>& all_roots, in
         s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
         s.err = std::string("shard label upload: ") + hipGetErrorString(e);
     } else {
-        s.rc = dbscan_slab_label_device(s.h, dz, dgid, dgs, droots, nr, mode, dcl, dfl);
+        s.rc = dbscan_slab_label_device(h, dz, dgid, dgs, droots, nr, mode, dcl, dfl);
         if (s.rc != DBSCAN_OK) {
             s.err = dbscan_last_error();
         } else {
@@ -192,6 +213,7 @@ void shard_label(Shard& s, int device, const std::vector<int64_t>& all_roots, in
     }
     for (void* p : {(void*)dz, (void*)dfl, (void*)dgid, (void*)dgs, (void*)droots, (void*)dcl})
         (void)hipFree(p);
+    fitd.release();
 }
 
 // Min-root union-find over global visit indices (host; the records are few).
@@ -252,6 +274,13 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
     const int world = (int)cuts.size() + 1;
     const double R = reach(eps);
     std::vector<Shard> sh(world);
+    for (auto& s : sh) {  // (a slab holds ~n/world points plus its halos)
+        const size_t guess = (size_t)(n / world + n / (8 * world) + 16);
+        s.gid.reserve(guess);
+        s.x.reserve(guess);
+        s.y.reserve(guess);
+        s.zone.reserve(guess);
+    }
     for (int64_t i = 0; i < n; ++i) {  // slab plan: points in increasing global visit order
         // only the owner and shards whose halo can reach x need a look: scan neighbours of the
         // owner until both directions fall out of reach
@@ -276,12 +305,29 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             }
         }
     }
-    {
-        std::vector<std::thread> th;
-        for (int r = 0; r < world; ++r)
-            th.emplace_back(shard_fit, std::ref(sh[r]), r % ndev, eps, min_points);
-        for (auto& t : th) t.join();
+    // one host thread and one handle per device; the shards of a device run one after another
+    // on its handle (one workspace per device: 8 shards of a 10^9-point job on one GPU)
+    const int nworkers = std::min(world, ndev);
+    std::vector<dbscan_handle*> hs(nworkers, nullptr);
+    for (int w = 0; w < nworkers; ++w) {
+        hs[w] = dbscan_create(w);
+        if (!hs[w]) {
+            *err = dbscan_last_error();
+            for (auto* h : hs)
+                if (h) dbscan_destroy(h);
+            return DBSCAN_EHIP;
+        }
     }
+    const bool shared_dev = world > nworkers;
+    auto each_device = [&](auto&& f) {
+        std::vector<std::thread> th;
+        for (int w = 0; w < nworkers; ++w)
+            th.emplace_back([&, w]() {
+                for (int r = w; r < world; r += nworkers) f(r, w);
+            });
+        for (auto& t : th) t.join();
+    };
+    each_device([&](int r, int w) { shard_fit(sh[r], hs[w], w, eps, min_points); });
     int32_t rc = DBSCAN_OK;
     for (auto& s : sh)
         if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
@@ -305,12 +351,12 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                     s.gs[p] = gs;
                     if (s.zone[p] == 0 && gs == g) all_roots.push_back(g);
                 }
+            std::vector<int32_t>().swap(s.root);
         }
         std::sort(all_roots.begin(), all_roots.end());
-        std::vector<std::thread> th;
-        for (int r = 0; r < world; ++r)
-            th.emplace_back(shard_label, std::ref(sh[r]), r % ndev, std::cref(all_roots), mode);
-        for (auto& t : th) t.join();
+        each_device([&](int r, int w) {
+            shard_label(sh[r], hs[w], w, eps, min_points, all_roots, mode, shared_dev);
+        });
         for (auto& s : sh)
             if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
                 rc = s.rc;
@@ -326,8 +372,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                 }
         *n_clusters_out = (int64_t)all_roots.size();
     }
-    for (auto& s : sh)
-        if (s.h) dbscan_destroy(s.h);
+    for (auto* h : hs) dbscan_destroy(h);
     return rc;
 }
 

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 namespace dbscan {
@@ -309,6 +310,113 @@ int64_t partition_cells(const double* cell_x, const double* cell_y, const int64_
     const int64_t r = split_partitions(mrs, imin, jmin, W, H, h, max_points, out);
     if (r < 0) throw ArgError{"dbscan_partition_cells: rectangle is not a proper sub-rectangle"};
     return r;
+}
+
+// DBSCAN.scala:116-137: localMargins = (p.shrink(eps), p, p.shrink(-eps)) and
+//   duplicated = for (point, ((inner, main, outer), id)) if outer.contains(point) yield (id, point)
+// i.e. every point goes to every partition whose outer rectangle (main grown by eps, the
+// reference's own fp arithmetic: x + (-eps), x2 - (-eps)) contains it, borders included
+// (DBSCANRectangle.scala:35-37).  Each partition's points come out in input order (the order
+// groupByKey hands a partition to LocalDBSCANNaive.fit).  Host threads over chunks of the input;
+// a bucket grid over the outer rectangles replaces the reference's scan of every partition per
+// point (the same decisions).  Returns the total; fills offsets_out[n_parts + 1] and, when
+// index_out is given and capacity >= total, index_out.
+int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,
+                         int64_t n_parts, double eps, int64_t* offsets_out, int64_t* index_out,
+                         int64_t capacity) {
+    struct Box {
+        double x, y, x2, y2;
+    };
+    std::vector<Box> outer((size_t)n_parts);
+    bool finite = true;
+    double bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
+    for (int64_t p = 0; p < n_parts; ++p) {
+        const double* r = rects + 4 * p;
+        Box b{r[0] + (-eps), r[1] + (-eps), r[2] - (-eps), r[3] - (-eps)};  // shrink(-eps)
+        outer[(size_t)p] = b;
+        finite = finite && std::isfinite(b.x) && std::isfinite(b.y) && std::isfinite(b.x2) &&
+                 std::isfinite(b.y2);
+        bx0 = std::min(bx0, b.x);
+        bx1 = std::max(bx1, b.x2);
+        by0 = std::min(by0, b.y);
+        by1 = std::max(by1, b.y2);
+    }
+    // bucket grid: bucket(v) = floor((v - b0) * ib), clamped; monotone in v, so a point inside
+    // a box lies in one of the buckets the box registered in
+    int G = 1;
+    if (finite && n_parts > 0) {
+        G = (int)std::min<double>(4096.0, 2.0 * std::ceil(std::sqrt((double)n_parts)) + 1.0);
+        if (!(bx1 > bx0) || !(by1 > by0) || !std::isfinite(bx1 - bx0) || !std::isfinite(by1 - by0))
+            G = 1;
+    }
+    const double ibx = G > 1 ? G / (bx1 - bx0) : 0.0, iby = G > 1 ? G / (by1 - by0) : 0.0;
+    auto bucket = [&](double v, double b0, double ib) -> int {
+        if (G == 1) return 0;
+        const double t = std::floor((v - b0) * ib);
+        if (!(t > 0)) return 0;  // (NaN too)
+        return t >= G - 1 ? G - 1 : (int)t;
+    };
+    std::vector<int32_t> head((size_t)G * G + 1, 0), lst;
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<int32_t> fill;
+        if (pass == 1) {
+            for (size_t k = 1; k < head.size(); ++k) head[k] += head[k - 1];
+            lst.resize((size_t)head.back());
+            fill.assign(head.begin(), head.end() - 1);
+        }
+        for (int64_t p = 0; p < n_parts; ++p) {
+            const Box& b = outer[(size_t)p];
+            const int i0 = bucket(b.x, bx0, ibx), i1 = bucket(b.x2, bx0, ibx);
+            const int j0 = bucket(b.y, by0, iby), j1 = bucket(b.y2, by0, iby);
+            for (int j = j0; j <= j1; ++j)
+                for (int i = i0; i <= i1; ++i) {
+                    const size_t c = (size_t)j * G + i;
+                    if (pass == 0) ++head[c + 1];
+                    else lst[(size_t)fill[c]++] = (int32_t)p;
+                }
+        }
+    }
+    int T = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / 65536));
+    const unsigned hc = std::thread::hardware_concurrency();
+    if (hc > 0) T = std::min<int>(T, (int)hc);
+    const int64_t chunk = (n + T - 1) / std::max(T, 1);
+    std::vector<std::vector<int64_t>> cnt((size_t)T, std::vector<int64_t>((size_t)n_parts, 0));
+    auto visit = [&](int t, bool write, std::vector<int64_t>* pos) {
+        const int64_t a = t * chunk, e = std::min<int64_t>(n, a + chunk);
+        for (int64_t i = a; i < e; ++i) {
+            const double px = x[i], py = y[i];
+            const size_t c = (size_t)bucket(py, by0, iby) * G + bucket(px, bx0, ibx);
+            for (int32_t k = head[c]; k < head[c + 1]; ++k) {
+                const int32_t p = lst[(size_t)k];
+                const Box& b = outer[(size_t)p];
+                if (b.x <= px && px <= b.x2 && b.y <= py && py <= b.y2) {  // contains
+                    if (write) index_out[(*pos)[(size_t)p]++] = i;
+                    else ++cnt[(size_t)t][(size_t)p];
+                }
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back(visit, t, false, nullptr);
+        for (auto& h : th) h.join();
+    }
+    int64_t total = 0;
+    std::vector<std::vector<int64_t>> pos((size_t)T, std::vector<int64_t>((size_t)n_parts, 0));
+    for (int64_t p = 0; p < n_parts; ++p) {
+        offsets_out[p] = total;
+        for (int t = 0; t < T; ++t) {
+            pos[(size_t)t][(size_t)p] = total;
+            total += cnt[(size_t)t][(size_t)p];
+        }
+    }
+    offsets_out[n_parts] = total;
+    if (index_out && capacity >= total) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back(visit, t, true, &pos[(size_t)t]);
+        for (auto& h : th) h.join();
+    }
+    return total;
 }
 
 }  // namespace dbscan

@@ -1,0 +1,525 @@
+// small.hip -- the local fit of one partition held entirely in ONE workgroup's LDS, for the
+// partition sizes DBSCAN.train hands the seam, and its batched form.
+//
+// DBSCAN.scala:150-155 calls `new LocalDBSCANNaive(eps, minPoints).fit(points)` once per spatial
+// partition: at most maxPointsPerPartition points (EvenSplitPartitioner.scala:44-209) plus the
+// eps halo (DBSCAN.scala:116-137) -- hundreds to ~10^4 points.  The tiled pipeline of fit.hip is
+// ~45 launches whose fixed cost dominates at that size; here one workgroup of 1024 threads does
+// the whole fit of a partition of <= kSmallMaxPoints points in one launch, and a batch of an
+// executor's partitions is one launch with one workgroup per partition (dbscan_fit_batch).
+//
+// Same closed form as fit.hip (LocalDBSCANNaive.scala:37-118,
+// LocalDBSCANArchery.scala:103-106), same fp64 predicate (DBSCANPoint.scala:26-30), same results
+// bit for bit, partition-local cluster ids 1..k in the order the reference opens them:
+//   load    x, y of the partition (fp64, coalesced) into registers; bbox of the finite points
+//   grid    cells of side >= eps (the 3x3 stencil holds every accepted pair, DESIGN.md "grid
+//           soundness"), the side doubled along the longer axis until the dense cell table fits
+//           kSmCells entries
+//   sort    counting sort by cell in LDS (histogram with LDS atomics, scan, scatter); each slot
+//           keeps an fp32 record of its coordinates (units of the base cell side, origin at the
+//           bbox centre) and (visit index << 16 | cell)
+//   count   each slot scans the 3 row ranges of its stencil, early exit at minPoints; the fp32
+//           pre-filter decides far from the threshold (band sized from the records' magnitude,
+//           below), the exact fp64 predicate on the global coordinates inside the band
+//   union   union-find in LDS over core-core pairs, each unordered pair once; the root with the
+//           larger visit index is hooked under the smaller, so a root IS s(K)
+//   number  roots flagged by visit index, popcount scan: cluster id = 1 + roots before s(K)
+//   label   cores: their root's id; non-cores: min s(K) over core neighbours + the Naive /
+//           Archery rule; written in input order
+// The order of the slots inside a cell depends on LDS atomics; nothing above depends on it.
+//
+// fp32 pre-filter bound.  u = fl64((v*0.5 - c*0.5) * (2/h0)) is the coordinate in units of the
+// base side h0 (= eps-ish), |u| <= Rr; r = fl32(u), |r - u| <= 2^-24 Rr; the fp64 steps add a
+// common scale error (relative ~2^-51) that only matters far below the band.  For a pair near
+// the threshold (|du| <= ~1 per axis) dx_f = fl32(r_q - r_p) is within E = 2^-23 (Rr + 1) of
+// the exact scaled difference, so F = fl32(dx_f^2 + dy_f^2) (one fused step or two roundings)
+// is within 4E + 2E^2 + 2^-22 e2 of d^2/h0^2, e2 = eps2/h0^2.  With M = 2^-20 (Rr + 4) +
+// 2^-20 e2 (> twice that): F <= rd(e2 - M) => the reference's fp64 d2 <= eps2 holds;
+// F > ru(e2 + M) => it does not; otherwise the fp64 predicate runs on the two points' global
+// coordinates.  Rr > 2^20 (absurd extents against eps) turns the pre-filter off: every
+// candidate takes the exact path.
+#include "../../include/dbscan_hip.h"
+#include "internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace dbscan {
+namespace {
+
+constexpr int kSmT = 1024;                  // threads per workgroup
+constexpr int kSmW = kSmT / 64;             // waves per workgroup
+constexpr int kSmN = (int)kSmallMaxPoints;  // points a workgroup holds
+constexpr int kSmPer = kSmN / kSmT;         // points per thread in the load phase
+constexpr int kSmCells = 8192;              // dense cell table entries
+constexpr int kSmCellPer = kSmCells / kSmT;
+constexpr uint32_t kNoCell = 0xFFFFu;
+static_assert(kSmN % kSmT == 0 && kSmCells % kSmT == 0, "whole rounds per thread");
+static_assert(kSmN <= 65536 && kSmCells < 65535, "16-bit visit indices, cells and cell starts");
+
+// DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77 (no FMA: -ffp-contract=off and
+// the pragma)
+__device__ __forceinline__ bool sm_within(double px, double py, double ox, double oy,
+                                          double eps2) {
+#pragma clang fp contract(off)
+    const double dx = ox - px;
+    const double dy = oy - py;
+    const double a = dx * dx;
+    const double b = dy * dy;
+    return (a + b) <= eps2;
+}
+
+__device__ __forceinline__ float sm_d2(float2 a, float2 b) {
+    const float dx = b.x - a.x, dy = b.y - a.y;
+    return __builtin_fmaf(dx, dx, dy * dy);
+}
+
+struct SmGrid {
+    double xmin2, ymin2, invx, invy;  // cell = floor((v*0.5 - vmin*0.5) * inv), as make_grid
+    double cx2, cy2, invs;            // record = fl32((v*0.5 - c*0.5) * invs)
+    float lo, hi;                     // F <= lo: neighbour; F > hi: not; else exact fp64
+    int nx, ny, ncells, nf, exact_only, bad;
+};
+
+// Workgroup exclusive scan of one int per thread; *total = the sum.  ws: kSmW + 1 ints.
+__device__ int sm_excl_scan(int v, int* ws, int* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        const int s = lane < kSmW ? ws[lane] : 0;
+        int si = s;
+#pragma unroll
+        for (int o = 1; o < kSmW; o <<= 1) {
+            const int u = __shfl_up(si, o, 64);
+            if (lane >= o) si += u;
+        }
+        if (lane < kSmW) ws[lane] = si - s;
+        if (lane == kSmW - 1) ws[kSmW] = si;
+    }
+    __syncthreads();
+    const int r = ws[w] + incl - v;
+    *total = ws[kSmW];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Union-find over slots in LDS.  Parents always have a strictly smaller visit index than their
+// children (roots are hooked larger-under-smaller), so there are no cycles and path halving
+// only ever shortcuts to an ancestor.
+__device__ __forceinline__ int sm_ld(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int sm_find(int* par, int x) {
+    while (true) {
+        const int p = sm_ld(par + x);
+        if (p == x) return x;
+        const int g = sm_ld(par + p);
+        if (g != p) __hip_atomic_store(par + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        x = g;
+    }
+}
+__device__ void sm_unite(int* par, const uint32_t* info, int a, int b) {
+    while (true) {
+        a = sm_find(par, a);
+        b = sm_find(par, b);
+        if (a == b) return;
+        if ((info[a] >> 16) < (info[b] >> 16)) {  // a: the root with the larger visit index
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(par + a, a, b) == a) return;
+    }
+}
+
+// The grid of one partition (one thread).  Sides as make_grid (fit.hip): >= R*(1+2^-16) with
+// R = max(|eps|*(1+2^-40), 2^-500); doubled along the axis with more cells until nx*ny fits.
+__device__ void sm_make_grid(double xmin, double xmax, double ymin, double ymax, int nf,
+                             double eps, double eps2, SmGrid* g) {
+    g->nf = nf;
+    g->bad = 0;
+    g->exact_only = 0;
+    g->nx = g->ny = g->ncells = 1;
+    if (nf == 0) return;
+    double R = fabs(eps) * (1.0 + 0x1p-40);
+    if (R < 0x1p-500) R = 0x1p-500;
+    const double h0 = R * (1.0 + 0x1p-16);
+    double hx = h0, hy = h0;
+    auto cells = [](double vmax, double vmin, double h) {
+        return floor((vmax * 0.5 - vmin * 0.5) * (2.0 / h)) + 1.0;
+    };
+    bool ok = false;
+    double cx = 1, cy = 1;
+    for (int it = 0; it < 4096; ++it) {
+        cx = cells(xmax, xmin, hx);
+        cy = cells(ymax, ymin, hy);
+        if (cx * cy <= (double)kSmCells) {
+            ok = true;
+            break;
+        }
+        if (cx >= cy) hx *= 2.0; else hy *= 2.0;
+    }
+    if (!ok) {
+        g->bad = 1;
+        return;
+    }
+    g->nx = (int)cx;
+    g->ny = (int)cy;
+    g->ncells = g->nx * g->ny;
+    g->xmin2 = xmin * 0.5;
+    g->ymin2 = ymin * 0.5;
+    g->invx = 2.0 / hx;
+    g->invy = 2.0 / hy;
+    // fp32 records around the bbox centre, in units of h0
+    g->cx2 = xmin * 0.5 + (xmax * 0.5 - xmin * 0.5) * 0.5;
+    g->cy2 = ymin * 0.5 + (ymax * 0.5 - ymin * 0.5) * 0.5;
+    g->invs = 2.0 / h0;
+    const double rr = fmax((xmax * 0.5 - xmin * 0.5), (ymax * 0.5 - ymin * 0.5)) * g->invs * 0.5 +
+                      1.0;
+    const double e2 = eps2 * (0.5 * g->invs) * (0.5 * g->invs);
+    if (!(rr <= 0x1p20) || !(e2 <= 0x1p20)) {
+        g->exact_only = 1;
+        g->lo = 0.f;
+        g->hi = 0.f;
+        return;
+    }
+    const double M = (rr + 4.0) * 0x1p-20 + e2 * 0x1p-20;
+    g->lo = __double2float_rd(e2 - M);
+    g->hi = __double2float_ru(e2 + M);
+}
+
+// One partition per workgroup.  offs == nullptr: one partition [0, single_n) (blockIdx 0);
+// else partition list[blockIdx.x] = points [offs[p], offs[p+1]).  nclusters[p] (or st) gets its
+// cluster count.  st/gp (single fits only): the handle's fit statistics.
+__global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, const int64_t* __restrict__ offs,
+    const int32_t* __restrict__ list, int64_t single_n, double eps, double eps2, int min_points,
+    int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
+    int32_t* __restrict__ nclusters, GridParams* __restrict__ gp, int32_t* __restrict__ st) {
+    __shared__ float2 rec[kSmN];           // fp32 records by slot
+    __shared__ uint32_t info[kSmN];        // visit index << 16 | cell (kNoCell: outside the grid)
+    __shared__ int par[kSmN];              // sort cursors, then union-find parents (slots)
+    __shared__ uint16_t cst[kSmCells + 2];  // first slot of every cell; cst[ncells] = nf
+    __shared__ uint8_t core[kSmN];
+    __shared__ uint32_t rbits[kSmN / 32];  // roots by visit index
+    __shared__ int wrank[kSmN / 32];       // roots before each word
+    __shared__ double red[5][kSmW];
+    __shared__ int wsc[kSmW + 1];
+    __shared__ int nonfin;
+    __shared__ SmGrid G;
+
+    const int tid = threadIdx.x;
+    int64_t off = 0, m64 = single_n;
+    int part = 0;
+    if (offs) {
+        part = list[blockIdx.x];
+        off = offs[part];
+        m64 = offs[part + 1] - off;
+    }
+    const int m = (int)m64;  // the host routes only m <= kSmN here
+    const double* px = x + off;
+    const double* py = y + off;
+
+    // ---- load + bbox ----
+    double vx[kSmPer], vy[kSmPer];
+    double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, nfin = 0;
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const int i = tid + k * kSmT;
+        vx[k] = 0;
+        vy[k] = 0;
+        if (i < m) {
+            vx[k] = px[i];
+            vy[k] = py[i];
+            if (isfinite(vx[k]) && isfinite(vy[k])) {
+                mnx = fmin(mnx, vx[k]);
+                mxx = fmax(mxx, vx[k]);
+                mny = fmin(mny, vy[k]);
+                mxy = fmax(mxy, vy[k]);
+                nfin += 1;
+            }
+        }
+    }
+    if (tid < kSmN / 32) rbits[tid] = 0;
+    if (tid == 0) nonfin = 0;
+    {
+        const int lane = tid & 63, w = tid >> 6;
+        mnx = wave_min(mnx);
+        mxx = wave_max(mxx);
+        mny = wave_min(mny);
+        mxy = wave_max(mxy);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nfin += __shfl_xor(nfin, o, 64);
+        if (lane == 0) {
+            red[0][w] = mnx;
+            red[1][w] = mxx;
+            red[2][w] = mny;
+            red[3][w] = mxy;
+            red[4][w] = nfin;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 1; k < kSmW; ++k) {
+                red[0][0] = fmin(red[0][0], red[0][k]);
+                red[1][0] = fmax(red[1][0], red[1][k]);
+                red[2][0] = fmin(red[2][0], red[2][k]);
+                red[3][0] = fmax(red[3][0], red[3][k]);
+                red[4][0] += red[4][k];
+            }
+            sm_make_grid(red[0][0], red[1][0], red[2][0], red[3][0], (int)red[4][0], eps, eps2,
+                         &G);
+        }
+        __syncthreads();
+    }
+    const int nf = G.nf;
+    const int nx = G.nx, ny = G.ny, ncells = G.ncells;
+    if (G.bad) {  // (unreachable for finite bboxes: 4096 doublings span every double extent)
+        if (tid == 0 && st) st[kStError] = 1;
+        return;
+    }
+
+    // ---- counting sort by cell ----
+    for (int c = tid; c < ncells; c += kSmT) par[c] = 0;
+    __syncthreads();
+    int mycell[kSmPer];
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const int i = tid + k * kSmT;
+        mycell[k] = -1;
+        if (i < m && isfinite(vx[k]) && isfinite(vy[k])) {
+            int cx = (int)floor((vx[k] * 0.5 - G.xmin2) * G.invx);
+            int cy = (int)floor((vy[k] * 0.5 - G.ymin2) * G.invy);
+            cx = min(max(cx, 0), nx - 1);
+            cy = min(max(cy, 0), ny - 1);
+            mycell[k] = cy * nx + cx;
+            atomicAdd(&par[mycell[k]], 1);
+        }
+    }
+    __syncthreads();
+    int occupied = 0;
+    {
+        int cnt[kSmCellPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kSmCellPer; ++k) {
+            const int c = tid * kSmCellPer + k;
+            cnt[k] = c < ncells ? par[c] : 0;
+            sum += cnt[k];
+            occupied += cnt[k] > 0 ? 1 : 0;
+        }
+        int tot = 0;
+        int run = sm_excl_scan(sum, wsc, &tot);
+#pragma unroll
+        for (int k = 0; k < kSmCellPer; ++k) {
+            const int c = tid * kSmCellPer + k;
+            if (c < ncells) {
+                par[c] = run;
+                cst[c] = (uint16_t)run;
+            }
+            run += cnt[k];
+        }
+        if (tid == 0) cst[ncells] = (uint16_t)nf;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const int i = tid + k * kSmT;
+        if (i >= m) continue;
+        if (mycell[k] >= 0) {
+            const int s = atomicAdd(&par[mycell[k]], 1);
+            rec[s] = make_float2((float)((vx[k] * 0.5 - G.cx2) * G.invs),
+                                 (float)((vy[k] * 0.5 - G.cy2) * G.invs));
+            info[s] = ((uint32_t)i << 16) | (uint32_t)mycell[k];
+        } else {
+            const int s = nf + atomicAdd(&nonfin, 1);
+            info[s] = ((uint32_t)i << 16) | kNoCell;
+        }
+    }
+    __syncthreads();
+
+    // ---- stencil walk helpers ----
+    const float lo = G.lo, hi = G.hi;
+    const bool exact_only = G.exact_only != 0;
+    // neighbour test of slots p (record me) and q
+    auto pair = [&](int p, float2 me, int q) -> bool {
+        if (!exact_only) {
+            const float F = sm_d2(me, rec[q]);
+            if (F <= lo) return true;
+            if (F > hi) return false;
+        }
+        const int vp = (int)(info[p] >> 16), vq = (int)(info[q] >> 16);
+        return sm_within(px[vp], py[vp], px[vq], py[vq], eps2);
+    };
+    // f(q) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own row first);
+    // f returns false to stop
+    auto for_stencil = [&](int p, int qmin, auto&& f) {
+        const int c = (int)(info[p] & 0xFFFFu);
+        const int cy = c / nx, cx = c - cy * nx;
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+            if (r < 0 || r >= ny) continue;
+            const int e = cst[r * nx + x1 + 1];
+            for (int q = max((int)cst[r * nx + x0], qmin); q < e; ++q)
+                if (!f(q)) return;
+        }
+    };
+
+    // ---- count: core <=> |N(p)| >= minPoints (LocalDBSCANNaive.scala:52-56,99-101) ----
+    int ncore_local = 0;
+    for (int p = tid; p < m; p += kSmT) {
+        bool c = min_points <= 0;
+        if (!c && p < nf) {
+            const float2 me = rec[p];
+            int cnt = 0;
+            for_stencil(p, 0, [&](int q) {
+                cnt += pair(p, me, q) ? 1 : 0;
+                return cnt < min_points;
+            });
+            c = cnt >= min_points;
+        }
+        core[p] = c ? 1 : 0;
+        par[p] = p;
+        ncore_local += c ? 1 : 0;
+    }
+    __syncthreads();
+
+    // ---- union over core-core pairs (each unordered pair once: q > p) ----
+    for (int p = tid; p < nf; p += kSmT) {
+        if (!core[p]) continue;
+        const float2 me = rec[p];
+        for_stencil(p, p + 1, [&](int q) {
+            if (core[q] && pair(p, me, q)) sm_unite(par, info, p, q);
+            return true;
+        });
+    }
+    __syncthreads();
+
+    // ---- roots: s(K) flagged by visit index; then every core points at its root ----
+    // (read-only walks first, writes after a barrier: a path-halving find racing with the
+    // compression could leave a pointer one ancestor short of the root)
+    int myroot[kSmPer];
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const int p = tid + k * kSmT;
+        myroot[k] = -1;
+        if (p < m && core[p]) {
+            int r = p;
+            for (int u = par[r]; u != r; u = par[r]) r = u;
+            myroot[k] = r;
+            if (r == p) {
+                const uint32_t v = info[p] >> 16;
+                atomicOr(&rbits[v >> 5], 1u << (v & 31u));
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k)
+        if (myroot[k] >= 0) par[tid + k * kSmT] = myroot[k];
+    int nclust = 0;
+    {
+        const int v = tid < kSmN / 32 ? __popc(rbits[tid]) : 0;
+        const int r = sm_excl_scan(v, wsc, &nclust);  // (its barriers also order the compression)
+        if (tid < kSmN / 32) wrank[tid] = r;
+    }
+    __syncthreads();
+    auto cluster_of = [&](uint32_t s) -> int {  // 1 + roots with a smaller visit index
+        return wrank[s >> 5] + __popc(rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
+    };
+
+    // ---- labels (LocalDBSCANNaive.scala:89-106; Archery re-claim :103-106) ----
+    int32_t* cl_out = cluster + off;
+    uint8_t* fl_out = flag + off;
+    for (int p = tid; p < m; p += kSmT) {
+        const uint32_t v = info[p] >> 16;
+        int cid = 0;
+        uint8_t f = DBSCAN_FLAG_NOISE;
+        if (core[p]) {
+            cid = cluster_of(info[par[p]] >> 16);
+            f = DBSCAN_FLAG_CORE;
+        } else if (p < nf) {
+            const float2 me = rec[p];
+            uint32_t best = 0xFFFFFFFFu;
+            for_stencil(p, 0, [&](int q) {
+                if (core[q]) {
+                    const uint32_t s = info[par[q]] >> 16;
+                    if (s < best && pair(p, me, q)) best = s;
+                }
+                return true;
+            });
+            if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
+                cid = cluster_of(best);
+                f = DBSCAN_FLAG_BORDER;
+            }
+        }
+        cl_out[v] = cid;
+        fl_out[v] = f;
+    }
+
+    // ---- counts and statistics ----
+    {
+        int tot = 0;
+        (void)sm_excl_scan(ncore_local, wsc, &tot);
+        int occ = 0;
+        (void)sm_excl_scan(occupied, wsc, &occ);
+        if (tid == 0) {
+            if (nclusters) nclusters[part] = nclust;
+            if (st) {
+                st[kStNf] = nf;
+                st[kStCore] = tot;
+                st[kStClusters] = nclust;
+                st[kStCells] = nf > 0 ? occ : 0;
+                st[kStTiles] = 0;
+                st[kStBits] = 0;
+            }
+            if (gp) {
+                GridParams g{G.xmin2, G.ymin2, G.invx, G.invy, (uint32_t)nx, (uint32_t)ny, 1u, 1u,
+                             0};
+                *gp = g;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+bool small_fit_eligible(int64_t n, double eps, int32_t mode) {
+    const double eps2 = eps * eps;
+    return n >= 0 && n <= kSmallMaxPoints && std::isfinite(eps2) &&
+           (mode == DBSCAN_MODE_NAIVE || mode == DBSCAN_MODE_ARCHERY);
+}
+
+void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const double* y,
+                        const int64_t* d_offs, const int32_t* d_list, int32_t nlist,
+                        int64_t single_n, double eps, int32_t min_points, int32_t mode,
+                        int32_t* cluster, uint8_t* flag, int32_t* d_nclusters, GridParams* gp,
+                        int32_t* st) {
+    const unsigned grid = d_offs ? (unsigned)nlist : 1u;
+    if (grid == 0) return;
+    klaunch(prof, "small_fit", small_fit_kernel, dim3(grid), dim3(kSmT), 0, s, x, y, d_offs,
+            d_list, single_n, eps, eps * eps, (int)min_points, (int)mode, cluster, flag,
+            d_nclusters, gp, st);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dbscan

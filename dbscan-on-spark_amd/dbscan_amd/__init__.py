@@ -6,6 +6,6 @@ in include/dbscan_hip.h); this package is the host-side mirror of the reference 
 """
 from ._lib import (DBSCANError, Handle, MODE_ARCHERY, MODE_ARCHERY_F32BOX, MODE_NAIVE, LIB_PATH, load)  # noqa: F401
 from .local import (DBSCANLabeledPoint, DBSCANPoint, Flag, LocalDBSCANArchery,  # noqa: F401
-                    LocalDBSCANNaive, Unknown, fit_arrays, train_node)
+                    LocalDBSCANNaive, Unknown, duplicate, fit_arrays, fit_batch, train_node)
 from .partition import DBSCANRectangle, EvenSplitPartitioner  # noqa: F401
 from .train import DBSCAN  # noqa: F401

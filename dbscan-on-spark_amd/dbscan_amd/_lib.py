@@ -63,7 +63,13 @@ SIGNATURES = [
      [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     ("dbscan_slab_label_finish_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
+    ("dbscan_set_small_max", _i64, [_vp, _i64]),
+    ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_fit_batch_device_async", _i32,
+     [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_duplicate", _i64, [_vp, _vp, _i64, _vp, _i64, _d, _vp, _vp, _i64]),
 ]
+SMALL_MAX_POINTS = 8192  # DBSCAN_SMALL_MAX_POINTS
 
 _lib = None
 _lock = threading.Lock()
@@ -142,6 +148,14 @@ class Handle:
     @property
     def stream(self) -> int:
         return int(load().dbscan_stream(self._h) or 0)
+
+    def set_small_max(self, max_points: int) -> int:
+        """Fits of <= max_points points run the one-workgroup kernel (small.hip); 0 sends every
+        fit through the tiled pipeline.  Returns the previous value."""
+        r = load().dbscan_set_small_max(self._h, int(max_points))
+        if r < 0:
+            check(int(r))
+        return int(r)
 
     def stats(self) -> dict:
         buf = (ctypes.c_int64 * 14)()

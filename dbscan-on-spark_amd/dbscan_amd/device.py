@@ -53,6 +53,25 @@ def fit_tensors_async(x: torch.Tensor, y: torch.Tensor, eps: float, min_points: 
                                                    _p(flag), nk))
 
 
+def fit_batch_tensors_async(x: torch.Tensor, y: torch.Tensor, offsets, eps: float,
+                            min_points: int, mode: int, handle: _lib.Handle,
+                            cluster: torch.Tensor, flag: torch.Tensor,
+                            n_clusters: torch.Tensor) -> None:
+    """Enqueue a batch of partition fits (dbscan_fit_batch_device_async): partition p is
+    x[offsets[p]:offsets[p+1]] (offsets: host int64 array); n_clusters: int32 device tensor of
+    n_parts entries.  handle.sync() before reading the outputs."""
+    import numpy as np
+
+    offs = np.ascontiguousarray(offsets, dtype=np.int64)
+    assert x.is_cuda and y.is_cuda and x.dtype == torch.float64 and y.dtype == torch.float64
+    assert cluster.dtype == torch.int32 and flag.dtype == torch.uint8
+    assert n_clusters.dtype == torch.int32 and n_clusters.numel() >= offs.size - 1
+    assert offs[-1] <= x.numel() and x.numel() == y.numel()
+    _lib.check(_lib.load().dbscan_fit_batch_device_async(
+        handle.ptr, _p(x), _p(y), offs.ctypes.data_as(ctypes.c_void_p), offs.size - 1,
+        float(eps), int(min_points), int(mode), _p(cluster), _p(flag), _p(n_clusters)))
+
+
 def generate_blobs(n: int, noise: float, dense: float, seed: int, handle: _lib.Handle,
                    device=None):
     """SURVEY §8d generator on the device (no PCIe): returns (x, y) float64 tensors."""

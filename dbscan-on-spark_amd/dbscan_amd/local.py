@@ -110,6 +110,58 @@ def fit_arrays(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
     return cl, fl, int(k.value)
 
 
+def fit_batch(x, y, offsets, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
+              handle: Optional[_lib.Handle] = None, cluster_out: Optional[np.ndarray] = None,
+              flag_out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Independent local fits of a batch of partitions (dbscan_fit_batch): partition p is
+    x[offsets[p]:offsets[p+1]] (visit order = array order), fitted exactly as fit_arrays would
+    fit it alone.  Returns (cluster int32[n], flag uint8[n], n_clusters int32[n_parts]) with
+    partition-local cluster ids -- DBSCAN.scala:153-154's flatMapValues(fit) over an executor's
+    partitions in one call."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    offs = np.ascontiguousarray(offsets, dtype=np.int64)
+    if x.shape != y.shape or x.ndim != 1 or offs.ndim != 1 or offs.size < 1:
+        raise ValueError("x, y: equal 1-D arrays; offsets: n_parts + 1 values")
+    n = x.size
+    if offs[-1] > n:
+        raise ValueError("offsets exceed the arrays")
+    cl = cluster_out if cluster_out is not None else np.zeros(n, np.int32)
+    fl = flag_out if flag_out is not None else np.zeros(n, np.uint8)
+    nk = np.zeros(max(1, offs.size - 1), np.int32)
+    h = handle or default_handle()
+    vp = ctypes.c_void_p
+    _lib.check(_lib.load().dbscan_fit_batch(
+        h.ptr, x.ctypes.data_as(vp), y.ctypes.data_as(vp), offs.ctypes.data_as(vp),
+        offs.size - 1, float(eps), int(min_points), int(mode), cl.ctypes.data_as(vp),
+        fl.ctypes.data_as(vp), nk.ctypes.data_as(vp)))
+    return cl, fl, nk[:offs.size - 1]
+
+
+def duplicate(x, y, rects, eps: float) -> Tuple[np.ndarray, np.ndarray]:
+    """DBSCAN.scala:116-137: the input indices every partition's outer rectangle (rectangle
+    grown by eps) holds, each partition in input order.  rects: (k, 4) array of (x, y, x2, y2).
+    Returns (offsets int64[k+1], index int64[total])."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    r = np.ascontiguousarray(np.asarray(rects, np.float64).reshape(-1, 4))
+    k = r.shape[0]
+    offs = np.zeros(k + 1, np.int64)
+    L, vp = _lib.load(), ctypes.c_void_p
+    tot = L.dbscan_duplicate(x.ctypes.data_as(vp), y.ctypes.data_as(vp), x.size,
+                             r.ctypes.data_as(vp), k, float(eps), offs.ctypes.data_as(vp), None,
+                             0)
+    if tot < 0:
+        _lib.check(int(tot))
+    idx = np.zeros(max(1, tot), np.int64)
+    tot2 = L.dbscan_duplicate(x.ctypes.data_as(vp), y.ctypes.data_as(vp), x.size,
+                              r.ctypes.data_as(vp), k, float(eps), offs.ctypes.data_as(vp),
+                              idx.ctypes.data_as(vp), idx.size)
+    if tot2 != tot:
+        _lib.check(int(tot2) if tot2 < 0 else _lib.DBSCAN_EARG)
+    return offs, idx[:tot]
+
+
 def train_node(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
                n_shards: int = 0) -> Tuple[np.ndarray, np.ndarray, int]:
     """Whole-node fit of host arrays in one process (dbscan_train_node): n_shards x-slabs over

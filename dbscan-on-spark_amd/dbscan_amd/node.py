@@ -30,6 +30,8 @@ from __future__ import annotations
 import ctypes
 import os
 import math
+import sys
+import warnings
 from typing import List, Optional
 
 import torch
@@ -212,11 +214,23 @@ class HipSlabOps:
             _lib.check(_lib.load().dbscan_set_stream(self.h.ptr, None, 1))
             self._bound = False
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def __del__(self):
+        # Callers close() explicitly (NodeJob.close, the bench, the tests).  A finalizer may run
+        # at interpreter shutdown, after torch has torn down its streams: HIP calls from here are
+        # best-effort only, and never once the interpreter is finalizing or the handle is gone.
+        if not self._bound or sys.is_finalizing() or not getattr(self.h, "_h", None):
+            return
         try:
             self.close()
-        except Exception:
-            pass
+        except Exception as e:  # pragma: no cover - finalizer
+            warnings.warn(f"HipSlabOps finalizer could not unbind the handle's stream: {e}")
 
     def _to_handle(self):
         cur = torch.cuda.current_stream()
@@ -474,6 +488,18 @@ class NodeJob:
         tick("slab_label")
         self.n_clusters = int(all_roots.numel())
         return self.n_clusters
+
+    def close(self) -> None:
+        """Release the slab ops (gives the handle its own stream back)."""
+        if self.ops is not None and hasattr(self.ops, "close"):
+            self.ops.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     def owned(self):
         """(global visit index, cluster, flag) of this rank's owned points."""

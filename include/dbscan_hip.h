@@ -184,6 +184,47 @@ int32_t dbscan_csv_write(const char* path, const double* x, const double* y,
 int32_t dbscan_format_double(double v, char* buf);
 int64_t dbscan_scala_range_count(double start, double end, double step, int32_t inclusive);
 
+/* ---------------------------------------------------------------------------------------
+ * Partition-sized fits: the seam's real call pattern.  DBSCAN.scala:150-155 runs one
+ * LocalDBSCANNaive(eps, minPoints).fit per spatial partition -- at most maxPointsPerPartition
+ * points (EvenSplitPartitioner.scala:44-209) plus the eps halo (DBSCAN.scala:116-137).
+ * Full fits of at most dbscan_set_small_max(h, ...) points (default and ceiling
+ * DBSCAN_SMALL_MAX_POINTS) with a finite eps*eps in mode NAIVE or ARCHERY run ONE kernel in
+ * which one workgroup holds the whole partition in LDS (same results bit for bit as the tiled
+ * pipeline; dbscan_fit / dbscan_fit_h / dbscan_fit_device / dbscan_fit_device_async all route
+ * there).  dbscan_set_small_max returns the previous value (0 sends every fit through the tiled
+ * pipeline). */
+#define DBSCAN_SMALL_MAX_POINTS 8192
+int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
+
+/* A batch of independent local fits -- an executor's partitions -- in one call: partition p is
+ * points [offsets[p], offsets[p+1]) of x, y (host array offsets, n_parts + 1 non-decreasing
+ * values >= 0), each fitted exactly as dbscan_fit would fit it alone: cluster_out / flag_out at
+ * the same indices (partition-local cluster ids 1..k_p, 0 = Noise), k_p in n_clusters_out[p].
+ * Partitions the one-workgroup kernel serves run in ONE launch, one workgroup each; the others
+ * run the tiled pipeline one after another on the handle's stream.  Replaces the per-partition
+ * flatMapValues(LocalDBSCANNaive.fit) of DBSCAN.scala:153-154 for a whole batch.
+ * dbscan_fit_batch: host arrays, synchronous.  dbscan_fit_batch_device_async: device arrays
+ * (n_clusters too; offsets stay a host array), enqueued on the handle's stream; dbscan_sync waits. */
+int32_t dbscan_fit_batch(dbscan_handle* h, const double* x, const double* y,
+                         const int64_t* offsets, int32_t n_parts, double eps, int32_t min_points,
+                         int32_t mode, int32_t* cluster_out, uint8_t* flag_out,
+                         int32_t* n_clusters_out);
+int32_t dbscan_fit_batch_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
+                                      const int64_t* offsets, int32_t n_parts, double eps,
+                                      int32_t min_points, int32_t mode, int32_t* d_cluster,
+                                      uint8_t* d_flag, int32_t* d_n_clusters);
+
+/* DBSCAN.scala:116-137 on the host: every point goes to every partition whose outer rectangle
+ * (the partition's rectangle (x, y, x2, y2) from dbscan_partition, grown by eps with the
+ * reference's arithmetic, shrink(-eps)) contains it, borders included; each partition's points
+ * in input order, as groupByKey hands them to the local fit.  Returns the total number of
+ * (partition, point) records; fills offsets_out[n_parts + 1] and, when index_out is not NULL and
+ * capacity >= the total, index_out (input indices) -- ready for dbscan_fit_batch after a gather. */
+int64_t dbscan_duplicate(const double* x, const double* y, int64_t n, const double* rects,
+                         int64_t n_parts, double eps, int64_t* offsets_out, int64_t* index_out,
+                         int64_t capacity);
+
 /* Whole-node entry: DBSCAN.train(points, eps, minPoints, ...).labeledPoints
  * (DBSCAN.scala:91-283) for one node, from host arrays, in ONE process.  The points are cut
  * into n_shards x-slabs at count quantiles snapped to the 2*eps grid (n_shards <= 0: one per

@@ -12,8 +12,11 @@ sequential fit.
             bench.py --gpus 8 times the same data set, one slab per GPU) + one per-GPU share
             G(1.25*10^7, 0.2, -, 2) as a single fit
   config 4  G(5*10^7, 0, dense=8, 3), one fit: one giant component per dense blob
-  config 5  the per-GPU share at the same density, G(1.25*10^8, 0.2, -, 4), one fit (the
-            10^9-point 8-GPU job itself is not checked against the oracle here)
+  config 5  the per-GPU share at the same density, G(1.25*10^8, 0.2, -, 4), one fit; and the
+            whole 10^9-point job G(10^9, 0.2, -, 4) through dbscan_train_node with 8 x-slabs
+            taking turns on the one test GPU, against the oracle's single fit of all 10^9
+            points, plus a second run with 5 slabs on a permuted visit order (core flags must
+            move with the points)
 
 Size-independent properties ride along: core flags are invariant under a permutation of the
 visit order, and a second fit of the same data is identical (idempotence)."""
@@ -117,3 +120,44 @@ def test_config3_full_size_train_node(dm, handle):
 def test_config5_share(handle):
     """One GPU's share of config 5 at the same density: G(1.25*10^8, 20% noise, seed 4)."""
     _single_fit_vs_oracle(handle, 125_000_000, 0.2, 1.0, 4)
+
+
+@pytest.mark.timeout(1150)
+def test_config5_full_size_train_node(dm, handle):
+    """BASELINE config 5 at full size: G(10^9, 20% uniform noise, seed 4), 16 GB of coordinates.
+    dbscan_train_node cuts it into 8 x-slabs with eps halos (the 8-GPU job's slabs, here taking
+    turns on the one test GPU: one workspace, each slab re-fitted before its label) and merges
+    them exactly; the global labels must equal ONE fit of all 10^9 points by the CPU oracle
+    (oracle_fit_grid on the host cores), bit for bit, cluster numbers included.  Then the same
+    points in a permuted visit order through 5 slabs: core flags are a property of the point set,
+    so they must move with the points (a cut- and order-invariance check at full size)."""
+    import time
+
+    import torch
+
+    n = 1_000_000_000
+    t0 = time.time()
+    tx, ty = _device_data(handle, n, 0.2, 1.0, 4)
+    hx, hy = tx.cpu().numpy(), ty.cpu().numpy()
+    del tx, ty
+    torch.cuda.empty_cache()
+    print(f"\n[config5] generated + copied {n} points in {time.time() - t0:.1f} s", flush=True)
+    t0 = time.time()
+    cl, fl, k = dm.train_node(hx, hy, EPS, MINPTS, 0, 8)
+    print(f"[config5] train_node 8 slabs: {time.time() - t0:.1f} s, {k} clusters, "
+          f"{int((fl == 1).sum())} core", flush=True)
+    t0 = time.time()
+    ref = O.fit_grid(hx, hy, EPS, MINPTS, 0)
+    print(f"[config5] oracle fit_grid: {time.time() - t0:.1f} s", flush=True)
+    _assert_equal(cl, fl, k, ref)
+    del ref, cl
+    core = fl == 1
+    del fl
+    p = np.random.default_rng(4).permutation(n // 8)  # permute 8 interleaved blocks' order
+    perm = (np.arange(8)[None, :] + 8 * p[:, None]).ravel()
+    del p
+    t0 = time.time()
+    cl2, fl2, k2 = dm.train_node(hx[perm], hy[perm], EPS, MINPTS, 0, 5)
+    print(f"[config5] permuted, 5 slabs: {time.time() - t0:.1f} s", flush=True)
+    assert k2 == k
+    np.testing.assert_array_equal(fl2 == 1, core[perm])

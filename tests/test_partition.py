@@ -83,3 +83,32 @@ def test_partition_points_vs_oracle(n, maxpp, noise, seed):
     assert len(got) == len(counts)
     np.testing.assert_array_equal(np.array([c for _, c in got]), counts)
     np.testing.assert_array_equal(np.array([tuple(r) for r, _ in got]), rects)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_duplicate_into_outer_rectangles(seed):
+    """dbscan_duplicate (host code) against a brute-force restatement of DBSCAN.scala:116-137:
+    point i goes to partition p iff outer_p = p.shrink(-eps) contains it (inclusive,
+    DBSCANRectangle.scala:35-37), each partition's points in input order.  Rectangles from the
+    reference's partitioner restated in the oracle; points on the outer borders exactly, NaNs
+    and points outside every rectangle included."""
+    import dbscan_amd
+
+    rng = np.random.default_rng(seed)
+    x, y = gen_blobs(20_000, noise=0.3, seed=seed + 40)
+    eps = 2.55 * (0.5 + seed * 0.3)
+    rects, _ = O.ref_partition(x, y, eps, 700)
+    # points exactly on outer borders, NaNs, and far outside
+    k = rng.integers(0, len(rects), 200)
+    x[:200] = rects[k, 0] + (-eps)
+    y[:200] = rng.uniform(rects[k, 1], rects[k, 3])
+    x[200:300] = rects[k[:100], 2] - (-eps)
+    x[300:310] = np.nan
+    x[310:320] = 1e9
+    offs, idx = dbscan_amd.duplicate(x, y, rects, eps)
+    ox, oy = rects[:, 0] + (-eps), rects[:, 1] + (-eps)
+    ox2, oy2 = rects[:, 2] - (-eps), rects[:, 3] - (-eps)
+    assert len(offs) == len(rects) + 1 and offs[0] == 0
+    for p in range(len(rects)):
+        want = np.flatnonzero((ox[p] <= x) & (x <= ox2[p]) & (oy[p] <= y) & (y <= oy2[p]))
+        np.testing.assert_array_equal(idx[offs[p]:offs[p + 1]], want)
