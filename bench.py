@@ -207,11 +207,40 @@ def _limiter(pmc):
             f"issue-stalled, {sq.get('SQ_ACTIVE_INST_ANY', 0) / wc:.0%} issuing (SQ counters)")
 
 
-def cpu_baseline(x, y, eps, min_points, threads):
+def _affinity() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(x, y, eps, min_points, threads, sample_s=None, h=None):
+    """The reference path on the host cores.  sample_s = None: the whole restated DBSCAN.train
+    (partitioner, halos, per-partition LocalDBSCANNaive.fit O(m^2), merge) over every point, plus
+    the strong comparator.  sample_s = S (N > 1: 10^8+ points): the same per-partition fits on
+    the reference's partitions of the same points, stopped after S seconds; value = the
+    partitions' own points / the time they took (the partitioner and merge are not timed)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import oracle as O  # CPU baseline leg only
+
+    if sample_s is not None:
+        import dbscan_amd
+
+        parts = dbscan_amd.partition.partition_points(x, y, eps, 8192, h)
+        rects = np.array([r for r, _ in parts])
+        counts = np.array([c for _, c in parts], np.int64)
+        r = O.ref_fit_partitions_timed(x, y, eps, min_points, rects, counts, threads, sample_s)
+        return {
+            "value": r["main_points"] / max(r["seconds"], 1e-9), "unit": "points/s",
+            "cores": threads, "kind": "port", "seconds": round(r["seconds"], 3),
+            "sample": (f"bounded sample: LocalDBSCANNaive.fit O(m^2) restated in C "
+                       f"(oracle/reference_pipeline.c) on {r['parts']} of the {len(counts)} "
+                       f"partitions the reference's EvenSplitPartitioner(maxPointsPerPartition="
+                       f"8192) makes of the same {x.size} points ({r['outer_points']} points with "
+                       f"eps halos), {threads} threads, {sample_s:.0f} s budget; value = those "
+                       f"partitions' own points / seconds (partitioner and merge not timed)")}
 
     t0 = time.perf_counter()
     r = O.ref_train(x, y, eps, min_points, 8192, threads)
@@ -406,10 +435,27 @@ def main():
         seam_out = seam(args, h, args.cpu_threads or host_threads())
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not node_path:
-        sx, sy = x.cpu().numpy(), y.cpu().numpy()
-        threads = args.cpu_threads or host_threads()
-        cpu = cpu_baseline(sx, sy, args.eps, args.min_points, threads)
+    if rank == 0 and not args.no_cpu_baseline:
+        if world == 1 and not node_path:
+            sx, sy = x.cpu().numpy(), y.cpu().numpy()
+            threads = args.cpu_threads or host_threads()
+            cpu = cpu_baseline(sx, sy, args.eps, args.min_points, threads)
+        else:
+            # the node's CPU share for this job (the other ranks idle meanwhile): the per-GPU
+            # share times the ranks, capped by this process's affinity; a bounded sample of the
+            # reference's per-partition fits over the same G(n_total)
+            from dbscan_amd import device as D
+
+            threads = args.cpu_threads or min(host_threads() * world, _affinity())
+            gx, gy = D.generate_blobs(n_total, args.noise, args.dense, args.seed, h)
+            sx, sy = gx.cpu().numpy(), gy.cpu().numpy()
+            del gx, gy
+            torch.cuda.empty_cache()
+            cpu = cpu_baseline(sx, sy, args.eps, args.min_points, threads, sample_s=12.0, h=h)
+            del sx, sy
+        if cpu is not None:
+            cpu["nproc"] = os.cpu_count()
+            cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
 
     if node_path:
         job.close()

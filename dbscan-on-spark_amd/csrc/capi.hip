@@ -231,6 +231,25 @@ int32_t guarded(dbscan_handle* h, F&& f) {
     }
 }
 
+// One lock per device over large host<->device copies (>= 2^20 points): see dbscan_fit_h.
+class XferLock {
+  public:
+    XferLock(int device, int64_t n) {
+        static std::mutex mu[64];
+        if (n >= (int64_t(1) << 20)) {
+            m_ = &mu[device & 63];
+            m_->lock();
+        }
+    }
+    ~XferLock() {
+        if (m_) m_->unlock();
+    }
+    bool held() const { return m_ != nullptr; }
+
+  private:
+    std::mutex* m_ = nullptr;
+};
+
 // local = the local-fit entry points, which also take DBSCAN_MODE_ARCHERY_F32BOX (its
 // directed neighbour relation has no slab/merge form)
 void check_fit_args(int64_t n, double eps, int32_t mode, const void* a, const void* b,
@@ -422,16 +441,28 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         double* dy = static_cast<double*>(h->hy.ensure(n * sizeof(double)));
         int32_t* dcl = static_cast<int32_t*>(h->hcl.ensure(n * sizeof(int32_t)));
         uint8_t* dfl = static_cast<uint8_t*>(h->hfl.ensure(n));
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        {
+            // Concurrent handles (Spark local[N] executor threads) take turns on the device's
+            // PCIe link for large copies, so one fit's kernels overlap another's copies instead
+            // of two pageable copies contending (the lock is not held while kernels run)
+            XferLock xl(h->device, n);
+            DBSCAN_HIP_CHECK(
+                hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            DBSCAN_HIP_CHECK(
+                hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+            if (xl.held()) DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        }
         dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
         a.small_max = h->small_max;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
-                                        hipMemcpyDeviceToHost, h->stream));
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(flag_out, dfl, n, hipMemcpyDeviceToHost, h->stream));
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        {
+            XferLock xl(h->device, n);  // (run_fit has waited for the fit)
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(cluster_out, dcl, n * sizeof(int32_t),
+                                            hipMemcpyDeviceToHost, h->stream));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(flag_out, dfl, n, hipMemcpyDeviceToHost, h->stream));
+            DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        }
         h->prof.flush();
         if (n_clusters_out) *n_clusters_out = (int32_t)k;
         return DBSCAN_OK;

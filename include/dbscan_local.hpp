@@ -13,6 +13,7 @@
 // dbscan_last_error().  There is no CPU fallback.
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -90,6 +91,43 @@ inline std::vector<DBSCANLabeledPoint> fit(Handle* h, double eps, int minPoints,
     }
     return out;
 }
+// One fit per partition in one call (dbscan_fit_batch): result p equals fit(parts[p]).
+inline std::vector<std::vector<DBSCANLabeledPoint>> fit_all(
+    Handle* h, double eps, int minPoints, int mode,
+    const std::vector<std::vector<DBSCANPoint>>& parts) {
+    std::vector<int64_t> offs(1, 0);
+    std::vector<double> xs, ys;
+    for (const auto& pt : parts) {
+        for (const auto& p : pt) {
+            xs.push_back(p.x());
+            ys.push_back(p.y());
+        }
+        offs.push_back((int64_t)xs.size());
+    }
+    const size_t n = xs.size();
+    std::vector<int32_t> cl(n), k(parts.size());
+    std::vector<uint8_t> fl(n);
+    std::unique_ptr<Handle> own;
+    if (!h) own.reset(h = new Handle(0));
+    const int rc = dbscan_fit_batch(h->get(), xs.data(), ys.data(), offs.data(),
+                                    (int32_t)parts.size(), eps, minPoints, mode, cl.data(),
+                                    fl.data(), k.data());
+    if (rc != DBSCAN_OK)
+        throw std::runtime_error(std::string("dbscan_fit_batch: ") + dbscan_last_error());
+    std::vector<std::vector<DBSCANLabeledPoint>> out(parts.size());
+    for (size_t g = 0; g < parts.size(); ++g) {
+        out[g].reserve(parts[g].size());
+        for (size_t i = 0; i < parts[g].size(); ++i) {
+            const size_t j = (size_t)offs[g] + i;
+            DBSCANLabeledPoint lp(parts[g][i]);
+            lp.cluster = cl[j];
+            lp.flag = static_cast<Flag>(fl[j]);
+            lp.visited = true;
+            out[g].push_back(std::move(lp));
+        }
+    }
+    return out;
+}
 }  // namespace detail
 
 // new LocalDBSCANNaive(eps, minPoints).fit(points)   (LocalDBSCANNaive.scala:31,37)
@@ -99,6 +137,11 @@ class LocalDBSCANNaive {
         : eps_(eps), minPoints_(minPoints), minDistanceSquared(eps * eps), h_(h) {}
     std::vector<DBSCANLabeledPoint> fit(const std::vector<DBSCANPoint>& points) const {
         return detail::fit(h_, eps_, minPoints_, DBSCAN_MODE_NAIVE, points);
+    }
+    // flatMapValues(fit) over many partitions at once (DBSCAN.scala:153-154, dbscan_fit_batch)
+    std::vector<std::vector<DBSCANLabeledPoint>> fitAll(
+        const std::vector<std::vector<DBSCANPoint>>& partitions) const {
+        return detail::fit_all(h_, eps_, minPoints_, DBSCAN_MODE_NAIVE, partitions);
     }
 
    private:
@@ -138,6 +181,40 @@ struct DBSCANRectangle {
         return x == o.x && y == o.y && x2 == o.x2 && y2 == o.y2;
     }
 };
+
+// DBSCAN.scala:116-137: every point into every partition whose eps-grown rectangle
+// (shrink(-eps), borders included) contains it, each partition in input order -- the input of
+// flatMapValues(fit) / LocalDBSCANNaive::fitAll (dbscan_duplicate).
+inline std::vector<std::vector<DBSCANPoint>> duplicate(
+    const std::vector<DBSCANPoint>& data,
+    const std::vector<std::pair<int, DBSCANRectangle>>& partitions, double eps) {
+    const int64_t n = (int64_t)data.size(), k = (int64_t)partitions.size();
+    std::vector<double> xs((size_t)n), ys((size_t)n), rects((size_t)(4 * k));
+    for (int64_t i = 0; i < n; ++i) {
+        xs[(size_t)i] = data[(size_t)i].x();
+        ys[(size_t)i] = data[(size_t)i].y();
+    }
+    for (int64_t p = 0; p < k; ++p) {
+        const DBSCANRectangle& r = partitions[(size_t)p].second;
+        rects[(size_t)(4 * p)] = r.x;
+        rects[(size_t)(4 * p + 1)] = r.y;
+        rects[(size_t)(4 * p + 2)] = r.x2;
+        rects[(size_t)(4 * p + 3)] = r.y2;
+    }
+    std::vector<int64_t> offs((size_t)k + 1);
+    const int64_t tot = dbscan_duplicate(xs.data(), ys.data(), n, rects.data(), k, eps,
+                                         offs.data(), nullptr, 0);
+    if (tot < 0) throw std::runtime_error(std::string("dbscan_duplicate: ") + dbscan_last_error());
+    std::vector<int64_t> idx((size_t)std::max<int64_t>(tot, 1));
+    if (dbscan_duplicate(xs.data(), ys.data(), n, rects.data(), k, eps, offs.data(), idx.data(),
+                         (int64_t)idx.size()) != tot)
+        throw std::runtime_error(std::string("dbscan_duplicate: ") + dbscan_last_error());
+    std::vector<std::vector<DBSCANPoint>> out((size_t)k);
+    for (int64_t p = 0; p < k; ++p)
+        for (int64_t j = offs[(size_t)p]; j < offs[(size_t)p + 1]; ++j)
+            out[(size_t)p].push_back(data[(size_t)idx[(size_t)j]]);
+    return out;
+}
 
 // DBSCAN.train(data, eps, minPoints, maxPointsPerPartition) (DBSCAN.scala:40-48).
 //   partitions()    the reference's (id, rectangle) list: EvenSplitPartitioner over the 2*eps

@@ -1,4 +1,4 @@
-"""Node path with the real HIP slab kernels: 2-3 ranks on the one GPU of the test box, gloo
+"""Node path with the real HIP slab kernels: 2, 3 and 8 ranks on the one GPU of the test box, gloo
 for the exchange (RCCL needs one GPU per rank; the collectives are the same calls).  The
 union of the ranks' owned labels must equal one fit of the whole data set, bit for bit."""
 import ctypes
@@ -21,6 +21,24 @@ def test_gpu_node_equals_single_fit(tmp_path, world, mode, n):
                                         timeout=600)
     assert np.all(seen == 1)
     rc, rf, rk = O.fit_grid(x, y, eps, 10, mode)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_gpu_node_world8_config3_shape(tmp_path, chunks):
+    """The N = 8 rehearsal of the bench's node path with the HIP slab kernels: 8 ranks (gloo)
+    sharing the one test GPU, 7 cuts, 2*10^6 points of config 3's shape (20% noise), both the
+    global-input and the host-chunk form; bit-exact against one oracle fit."""
+    n = 2_000_000
+    x, y = gen_blobs(n, noise=0.2, seed=2)
+    cl, fl, seen, ks, parts = run_ranks(tmp_path, x, y, 8, 2.55, 10, 0, use_gpu=True,
+                                        timeout=800, chunks=chunks)
+    assert np.all(seen == 1)
+    assert len(parts[0]["cuts"]) == 7
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
     np.testing.assert_array_equal(fl, rf)
     np.testing.assert_array_equal(cl, rc)
     assert ks == {rk}

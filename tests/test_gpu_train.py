@@ -74,6 +74,11 @@ int main(int argc, char** argv) {
     for (const auto& pr : m.partitions())
         std::printf("P %d %.17g %.17g %.17g %.17g\n", pr.first, pr.second.x, pr.second.y,
                     pr.second.x2, pr.second.y2);
+    // the seam's own pattern: duplicate into eps-grown partitions, one batch of local fits
+    auto parts = dbscan::duplicate(pts, m.partitions(), (double)0.3f);
+    auto res = dbscan::LocalDBSCANNaive((double)0.3f, 10).fitAll(parts);
+    for (size_t g = 0; g < res.size(); ++g)
+        for (const auto& p : res[g]) std::printf("Q %zu %d %d\n", g, p.cluster, (int)p.flag);
     return 0;
 }
 ''')
@@ -84,7 +89,7 @@ int main(int argc, char** argv) {
                    check=True)
     out = subprocess.run([str(exe), str(data)], check=True, capture_output=True,
                          text=True).stdout.split("\n")
-    lab_lines = [l.split() for l in out if l and not l.startswith("P")]
+    lab_lines = [l.split() for l in out if l and not l[0] in "PQ"]
     cl = np.array([int(a) for a, _ in lab_lines])
     fl = np.array([int(b) for _, b in lab_lines])
     rc, rf, _ = O.fit_sequential(x, y, EPS_03F, 10, 0)
@@ -93,3 +98,49 @@ int main(int argc, char** argv) {
     parts = [tuple(map(float, l.split()[2:])) for l in out if l.startswith("P")]
     rects, _ = O.ref_partition(x, y, EPS_03F, 250)
     assert parts == [tuple(map(float, r)) for r in rects]
+    import dbscan_amd
+
+    offs, idx = dbscan_amd.duplicate(x, y, rects, EPS_03F)
+    q = np.array([[int(v) for v in l.split()[1:]] for l in out if l.startswith("Q")])
+    assert q.shape[0] == offs[-1] == 1097
+    for g in range(len(rects)):
+        a, b = offs[g], offs[g + 1]
+        rc, rf, _ = O.fit_sequential(x[idx[a:b]], y[idx[a:b]], EPS_03F, 10, 0)
+        assert (q[a:b, 0] == g).all()
+        np.testing.assert_array_equal(q[a:b, 1], rc)
+        np.testing.assert_array_equal(q[a:b, 2], rf)
+
+
+def test_dbscan_sample_file_flow(tmp_path):
+    """DBSCANSample.scala:17-35 end to end from files: sc.textFile(labeled_data.csv) parsed by
+    dbscan_csv_read -> DBSCAN.train(eps = 0.1, minPoints = 3, maxPointsPerPartition = 400) on the
+    GPU -> model.labeledPoints written as "${p.x},${p.y},${p.cluster}" by dbscan_csv_write.
+    Expected text: the csv's own coordinate fields (they are exactly what JDK 7/8's
+    Double.toString prints for those doubles) and the oracle's restated DBSCAN.train
+    (ref_train: the reference's partitioner, halos, per-partition LocalDBSCANNaive and merge)
+    cluster ids, mapped through the one bijection between the two numberings (the reference
+    numbers global clusters in its collect order).  saveAsTextFile's line order follows the
+    Spark partitions, so the lines are compared as a multiset.  Every point appears once in
+    both (the reference's known defects drop no point and split no cluster on this input)."""
+    import dbscan_amd
+    from dbscan_amd import textio
+
+    src = os.path.join(ROOT, "tests", "golden", "labeled_data.csv")
+    x, y = textio.read_csv(src)
+    fields = [l.split(",") for l in open(src).read().splitlines() if l]
+    np.testing.assert_array_equal(x, np.array([float(f[0]) for f in fields]))
+    np.testing.assert_array_equal(y, np.array([float(f[1]) for f in fields]))
+    model = dbscan_amd.DBSCAN.train(np.stack([x, y], 1), eps=0.1, minPoints=3,
+                                    maxPointsPerPartition=400)
+    out = tmp_path / "labeled_data_result.txt"
+    textio.write_csv(out, x, y, model.cluster)
+    got = out.read_text().splitlines()
+    ref = O.ref_train(x, y, 0.1, 3, 400)
+    assert (ref["records"] == 1).all() and len(ref["rects"]) == 2
+    pairs = set(zip(ref["cluster"].tolist(), model.cluster.tolist()))
+    assert len(pairs) == len(set(ref["cluster"].tolist())) == len(set(model.cluster.tolist()))
+    to_ours = dict(pairs)
+    assert to_ours.get(0, 0) == 0  # Noise stays 0
+    want = [f"{f[0]},{f[1]},{to_ours[c]}" for f, c in zip(fields, ref["cluster"].tolist())]
+    assert sorted(got) == sorted(want)
+    assert model.n_clusters == ref["n_clusters"] == 26

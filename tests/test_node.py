@@ -184,3 +184,31 @@ def test_node_chunks_all_to_all_equals_single_fit(tmp_path, world, mode, bad):
     np.testing.assert_array_equal(cl, rc)
     assert ks == {rk}
     assert max(int(pt["n_slab"][0]) for pt in parts) < 0.8 * n
+
+
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_node_world8_rehearsal(tmp_path, chunks):
+    """The N = 8 shape of the bench's node path on CPU (gloo, 8 ranks, 7 cuts): blobs + noise
+    plus a horizontal band that crosses every slab, so the merge chains local components through
+    all 8 ranks; both the global-input and the host-chunk (two all_to_all) forms.  The union of
+    the ranks' owned labels equals one oracle fit of the whole set."""
+    rng = np.random.default_rng(88)
+    n = 48_000
+    x, y = _data(n, seed=88, bad=16)
+    s = np.sqrt(n / 1e6)
+    t = rng.uniform(-1100 * s, 1100 * s, 12_000)
+    x = np.concatenate([x, t])
+    y = np.concatenate([y, rng.normal(0, 0.3, t.size)])
+    p = rng.permutation(x.size)
+    x, y = x[p], y[p]
+    eps = 60.0 * s
+    cl, fl, seen, ks, parts = run_ranks(tmp_path, x, y, 8, eps, 10, 0, chunks=chunks,
+                                        timeout=600)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, eps, 10, 0)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+    assert len(parts[0]["cuts"]) == 7
+    band = np.abs(y) < 1.0
+    assert len(np.unique(rc[band & (rf == 1)])) == 1  # the band is one cluster across the slabs
