@@ -3252,7 +3252,10 @@ static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* s
                                         const int32_t* cell, const Seg* seg,
                                         const int32_t* nf_p, int64_t n, double eps, double eps2,
                                         const uint8_t* core) {
-    int64_t cap = std::max<int64_t>(kBoxEdgeCap, (int64_t)(ws.box_edges.bytes / (2 * sizeof(int2))));
+    // what the buffer already holds (edges + ranks behind a 64-B count): ensure() must not grow it
+    const int64_t held = ws.box_edges.bytes > 64
+                             ? (int64_t)((ws.box_edges.bytes - 64) / (2 * sizeof(int2))) : 0;
+    int64_t cap = std::max<int64_t>(kBoxEdgeCap, held);
     unsigned long long m = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         char* buf = static_cast<char*>(ws.box_edges.ensure(2 * cap * sizeof(int2) + 64));
