@@ -903,44 +903,96 @@ int64_t batch_span(const int64_t* offsets, int32_t n_parts) {
     return offsets[n_parts];
 }
 
+// Batches that span at least this many points (or hold a partition over the one-workgroup
+// capacity) run as ONE tiled fit over per-partition grids (batch.hip); smaller ones as one
+// launch of the one-workgroup kernel (small.hip).
+constexpr int64_t kBatchTiledSpan = 65536;
+
+// Pinned staging of the batch tables (grow-only), free once the last upload from it is done.
+char* batch_pinned(dbscan_handle* h, size_t need) {
+    if (!h->bcopied) DBSCAN_HIP_CHECK(hipEventCreateWithFlags(&h->bcopied, hipEventDisableTiming));
+    else DBSCAN_HIP_CHECK(hipEventSynchronize(h->bcopied));
+    if (h->bpinned_bytes < need) {
+        if (h->bpinned) (void)hipHostFree(h->bpinned);
+        h->bpinned = nullptr;
+        h->bpinned_bytes = 0;
+        DBSCAN_HIP_CHECK(hipHostMalloc(&h->bpinned, need + need / 2, hipHostMallocDefault));
+        h->bpinned_bytes = need + need / 2;
+    }
+    return static_cast<char*>(h->bpinned);
+}
+
 // Enqueues one batch on the handle's stream (device arrays indexed like the offsets, host
-// offsets): the partitions the one-workgroup kernel serves in ONE launch, the others through the
-// tiled pipeline one after another (stream-ordered on the handle's workspace).
+// offsets).  Large batches: one tiled fit over the partitions' own grids (batch.hip; one host
+// synchronization, for the partitions' boxes), the partitions it cannot place fitted one after
+// another.  Small batches: the partitions the one-workgroup kernel serves in ONE launch, the
+// others through the tiled pipeline one after another (stream-ordered on the handle's workspace).
 void batch_enqueue(dbscan_handle* h, const double* dx, const double* dy, const int64_t* offs,
                    int32_t n_parts, double eps, int32_t min_points, int32_t mode, int32_t* dcl,
                    uint8_t* dfl, int32_t* dnk) {
     const int64_t cap = std::min<int64_t>(h->small_max, dbscan::kSmallMaxPoints);
-    std::vector<int32_t> small, big;
-    for (int32_t p = 0; p < n_parts; ++p) {
-        const int64_t m = offs[p + 1] - offs[p];
-        if (m <= cap && dbscan::small_fit_eligible(m, eps, mode)) small.push_back(p);
-        else big.push_back(p);
-    }
-    if (!small.empty()) {
-        const size_t need = (size_t)(n_parts + 1) * sizeof(int64_t) + small.size() * sizeof(int32_t);
-        if (!h->bcopied) DBSCAN_HIP_CHECK(hipEventCreateWithFlags(&h->bcopied, hipEventDisableTiming));
-        else DBSCAN_HIP_CHECK(hipEventSynchronize(h->bcopied));  // the pinned tables are free
-        if (h->bpinned_bytes < need) {
-            if (h->bpinned) (void)hipHostFree(h->bpinned);
-            h->bpinned = nullptr;
-            h->bpinned_bytes = 0;
-            DBSCAN_HIP_CHECK(hipHostMalloc(&h->bpinned, need + need / 2, hipHostMallocDefault));
-            h->bpinned_bytes = need + need / 2;
-        }
-        char* pin = static_cast<char*>(h->bpinned);
-        memcpy(pin, offs, (size_t)(n_parts + 1) * sizeof(int64_t));
-        memcpy(pin + (size_t)(n_parts + 1) * sizeof(int64_t), small.data(),
-               small.size() * sizeof(int32_t));
-        char* dev = static_cast<char*>(h->boffs.ensure(need));
-        DBSCAN_HIP_CHECK(hipMemcpyAsync(dev, pin, need, hipMemcpyHostToDevice, h->stream));
-        DBSCAN_HIP_CHECK(hipEventRecord(h->bcopied, h->stream));
-        dbscan::enqueue_small_fits(
-            h->stream, &h->prof, dx, dy, reinterpret_cast<const int64_t*>(dev),
-            reinterpret_cast<const int32_t*>(dev + (size_t)(n_parts + 1) * sizeof(int64_t)),
-            (int32_t)small.size(), 0, eps, min_points, mode, dcl, dfl, dnk, nullptr, nullptr);
-    }
+    const int64_t o0 = n_parts > 0 ? offs[0] : 0, span = n_parts > 0 ? offs[n_parts] - o0 : 0;
+    bool over = false;
+    for (int32_t p = 0; p < n_parts && !over; ++p) over = offs[p + 1] - offs[p] > cap;
+    const bool tiled = n_parts > 1 && (mode == DBSCAN_MODE_NAIVE || mode == DBSCAN_MODE_ARCHERY) &&
+                       std::isfinite(eps * eps) && (over || span >= kBatchTiledSpan);
+    std::vector<int32_t> alone;
     h->pending = false;
-    for (int32_t p : big) {
+    if (tiled) {
+        const size_t offs_b = (size_t)(n_parts + 1) * sizeof(int64_t);
+        const size_t box_b = (size_t)n_parts * 5 * sizeof(double);
+        const size_t tab_b = (size_t)n_parts * sizeof(dbscan::PartGrid);
+        char* pin = batch_pinned(h, offs_b + box_b + tab_b);
+        int64_t* rel = reinterpret_cast<int64_t*>(pin);
+        double* box = reinterpret_cast<double*>(pin + offs_b);
+        auto* tab = reinterpret_cast<dbscan::PartGrid*>(pin + offs_b + box_b);
+        for (int32_t p = 0; p <= n_parts; ++p) rel[p] = offs[p] - o0;
+        char* dev = static_cast<char*>(h->boffs.ensure(offs_b + tab_b));
+        auto* d_offs = reinterpret_cast<int64_t*>(dev);
+        auto* d_tab = reinterpret_cast<dbscan::PartGrid*>(dev + offs_b);
+        double* d_box = static_cast<double*>(h->ws.pbox.ensure(box_b));
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(d_offs, rel, offs_b, hipMemcpyHostToDevice, h->stream));
+        dbscan::enqueue_batch_bbox(h->stream, dx + o0, dy + o0, d_offs, n_parts, d_box);
+        DBSCAN_HIP_CHECK(hipMemcpyAsync(box, d_box, box_b, hipMemcpyDeviceToHost, h->stream));
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+        dbscan::BatchFit bf;
+        if (dbscan::plan_batch_grid(box, rel, n_parts, eps, tab, &bf, &alone)) {
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(d_tab, tab, tab_b, hipMemcpyHostToDevice, h->stream));
+            bf.g.parts = d_tab;
+            bf.g.poffs = d_offs;
+            bf.nclusters = dnk;
+            dbscan::FitArgs a{dx + o0, dy + o0, nullptr, span, eps, min_points, mode,
+                              dcl + o0, dfl + o0, nullptr, nullptr};
+            a.small_max = 0;
+            a.batch = &bf;
+            dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+            h->pending = true;
+        }
+        DBSCAN_HIP_CHECK(hipEventRecord(h->bcopied, h->stream));
+    } else {
+        std::vector<int32_t> small;
+        for (int32_t p = 0; p < n_parts; ++p) {
+            const int64_t m = offs[p + 1] - offs[p];
+            if (m <= cap && dbscan::small_fit_eligible(m, eps, mode)) small.push_back(p);
+            else alone.push_back(p);
+        }
+        if (!small.empty()) {
+            const size_t need =
+                (size_t)(n_parts + 1) * sizeof(int64_t) + small.size() * sizeof(int32_t);
+            char* pin = batch_pinned(h, need);
+            memcpy(pin, offs, (size_t)(n_parts + 1) * sizeof(int64_t));
+            memcpy(pin + (size_t)(n_parts + 1) * sizeof(int64_t), small.data(),
+                   small.size() * sizeof(int32_t));
+            char* dev = static_cast<char*>(h->boffs.ensure(need));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(dev, pin, need, hipMemcpyHostToDevice, h->stream));
+            DBSCAN_HIP_CHECK(hipEventRecord(h->bcopied, h->stream));
+            dbscan::enqueue_small_fits(
+                h->stream, &h->prof, dx, dy, reinterpret_cast<const int64_t*>(dev),
+                reinterpret_cast<const int32_t*>(dev + (size_t)(n_parts + 1) * sizeof(int64_t)),
+                (int32_t)small.size(), 0, eps, min_points, mode, dcl, dfl, dnk, nullptr, nullptr);
+        }
+    }
+    for (int32_t p : alone) {
         const int64_t o = offs[p], m = offs[p + 1] - o;
         dbscan::FitArgs a{dx + o, dy + o, nullptr, m, eps, min_points, mode, dcl + o, dfl + o,
                           nullptr, nullptr};
@@ -951,7 +1003,7 @@ void batch_enqueue(dbscan_handle* h, const double* dx, const double* dy, const i
     }
     if (!h->pending) {
         h->stats = dbscan::FitStats();
-        h->stats.n = offs[n_parts] - offs[0];
+        h->stats.n = span;
     }
     h->prepared = false;
 }

@@ -137,6 +137,36 @@ __device__ __forceinline__ void for_candidates(const Seg& s, F f) {
             if (!f(j)) return;
 }
 
+// Batched fits: the partition holding batch index i (offs[0] <= i < offs[np]; empty partitions
+// are skipped because their range is empty)
+__device__ __forceinline__ int part_of(const int64_t* __restrict__ offs, int np, int64_t i) {
+    int lo = 0, hi = np;  // offs[lo] <= i < offs[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (offs[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// The origin of a tile's fp32 cell-unit records: the grid origin and the tile's halo corner in
+// cells (batched fits: the tile's partition's local grid; tpart = partition of each tile)
+struct TileOrg {
+    double xmin2, ymin2, ox, oy;
+};
+__device__ __forceinline__ TileOrg tile_org(const GridParams& g, const int32_t* __restrict__ tpart,
+                                            int t, uint32_t tk) {
+    const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
+    TileOrg o{g.xmin2, g.ymin2, (double)(8 * (int64_t)tx - 1), (double)(8 * (int64_t)ty - 1)};
+    if (g.nparts > 0) {
+        const PartGrid P = g.parts[tpart[t]];
+        o.xmin2 = P.xmin2;
+        o.ymin2 = P.ymin2;
+        o.ox -= (double)P.cx0;
+        o.oy -= (double)P.cy0;
+    }
+    return o;
+}
+
 __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ x,
                                                      const double* __restrict__ y, int64_t n,
                                                      const GridParams* __restrict__ gp,
@@ -146,14 +176,29 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
     const GridParams g = *gp;
     const double a = x[i], b = y[i];
     uint32_t k = kSentinelKey;
-    if (__builtin_isfinite(a) && __builtin_isfinite(b)) {
+    // the grid of this point: the fit's own, or (batched fits) its partition's local grid at
+    // that partition's place in the virtual tile grid
+    double xmin2 = g.xmin2, ymin2 = g.ymin2, mx = 2.0 * (double)g.nx - 1.0,
+           my = 2.0 * (double)g.ny - 1.0;
+    uint32_t qx0 = 0, qy0 = 0;
+    bool binned = true;
+    if (g.nparts > 0) {
+        const PartGrid P = g.parts[part_of(g.poffs, g.nparts, i)];
+        xmin2 = P.xmin2;
+        ymin2 = P.ymin2;
+        mx = 2.0 * (double)P.nx - 1.0;
+        my = 2.0 * (double)P.ny - 1.0;
+        qx0 = 2u * (uint32_t)P.cx0;
+        qy0 = 2u * (uint32_t)P.cy0;
+        binned = P.nx > 0;
+    }
+    if (binned && __builtin_isfinite(a) && __builtin_isfinite(b)) {
         // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
-        double fx = floor(2.0 * ((a * 0.5 - g.xmin2) * g.invx));
-        double fy = floor(2.0 * ((b * 0.5 - g.ymin2) * g.invy));
-        const double mx = 2.0 * (double)g.nx - 1.0, my = 2.0 * (double)g.ny - 1.0;
+        double fx = floor(2.0 * ((a * 0.5 - xmin2) * g.invx));
+        double fy = floor(2.0 * ((b * 0.5 - ymin2) * g.invy));
         fx = fx < 0 ? 0 : (fx > mx ? mx : fx);
         fy = fy < 0 ? 0 : (fy > my ? my : fy);
-        const uint32_t qx = (uint32_t)fx, qy = (uint32_t)fy;
+        const uint32_t qx = (uint32_t)fx + qx0, qy = (uint32_t)fy + qy0;
         const uint32_t cx = qx >> 1, cy = qy >> 1;
         const uint32_t tile = (cy >> 3) * g.ntx + (cx >> 3);
         const uint32_t local = ((cy & 7u) << 3) | (cx & 7u);
@@ -192,6 +237,25 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
     if (i >= n) return;
     const int32_t p = inv[i];
     if (p < *nf_p) xy[p] = make_double2(x[i], y[i]);
+}
+
+// Bucketed sort (large fits): perm and the sorted coordinates from the padded band segments,
+// one coalesced pass over the places; every write lands inside the place's band (its segment's
+// slot range), which stays cache-resident while the launch sweeps the bands in order.
+__global__ __launch_bounds__(kBlock) void scatter_bucket_kernel(int64_t np,
+                                                                const int32_t* __restrict__ idx,
+                                                                const int32_t* __restrict__ inv,
+                                                                const double2* __restrict__ xyb,
+                                                                const int32_t* __restrict__ nf_p,
+                                                                int32_t* __restrict__ perm,
+                                                                double2* __restrict__ xy) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    const int32_t i = idx[j];
+    if (i < 0) return;  // a pad
+    const int32_t p = inv[j];
+    perm[p] = i;
+    if (p < *nf_p) xy[p] = xyb[j];
 }
 
 // Slab fits: the zone-2 points (count candidates, never core) marked in sorted order (zs,
@@ -1071,6 +1135,7 @@ struct FuseArgs {
     int32_t* qcomp;          // out: tile component rep per quarter (-1: no cores)
     uint8_t* tcore;          // out (f32): per tile, bit 0 its east cell column holds a core,
                              // bit 1 its south cell row does (edge_union skips the other sides)
+    const int32_t* tpart = nullptr;  // batched fits: partition of each occupied tile
 };
 
 struct UnionLds {  // aliases the count's neighbour-list staging (the two never overlap in time)
@@ -1398,7 +1463,7 @@ __device__ __forceinline__ float f32_d2(float2 a, float2 b) {
 // stage_build with the float2 cell-unit records (origin ox, oy: the tile's halo corner)
 template <int CAP>
 __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy, TileStage& st,
-                              float2* buf, const GridParams& g, double ox, double oy) {
+                              float2* buf, const GridParams& g, const TileOrg& o) {
     const int tid = threadIdx.x;
     if (tid < 100) {
         st.cb[tid] = m.b;
@@ -1444,8 +1509,8 @@ __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy
                 for (int s = 64; s > 0; s >>= 1)
                     if (lo + s < 100 && st.off[lo + s] <= i) lo += s;
                 const double2 v = xy[st.cb[lo] + (i - st.off[lo])];
-                buf[i] = make_float2((float)((v.x * 0.5 - g.xmin2) * g.invx - ox),
-                                     (float)((v.y * 0.5 - g.ymin2) * g.invy - oy));
+                buf[i] = make_float2((float)((v.x * 0.5 - o.xmin2) * g.invx - o.ox),
+                                     (float)((v.y * 0.5 - o.ymin2) * g.invy - o.oy));
             }
         }
     }
@@ -1727,10 +1792,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
         AB_STAMP(0);
         const int t = tile_at(k);
         if (threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
-        const uint32_t tk = fa.tkey[t];
-        const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
-        const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
-        stage_build32<CAP>(meta, xy, st, buf, g, ox, oy);
+        stage_build32<CAP>(meta, xy, st, buf, g, tile_org(g, fa.tpart, t, fa.tkey[t]));
         AB_STAMP(1);
         AB_NOTE(10, st.total);
         meta = stage_meta(tile_at(k + gridDim.x), ntiles, tstage, tstart, fa.tq);
@@ -1941,8 +2003,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             if (sl < SCAP / 32 + 1) T.lcore[sl] = 0u;
             wave_sync();
             {
-                const uint32_t ty = tk / g.ntx, tx = tk - ty * g.ntx;
-                const double ox = (double)(8 * (int64_t)tx - 1), oy = (double)(8 * (int64_t)ty - 1);
+                const TileOrg o = live ? tile_org(g, fa.tpart, t, tk) : TileOrg{0, 0, 0, 0};
 #pragma unroll
                 for (int uu = 0; uu < SCAP / SEG; ++uu) {
                     const int e = sl + uu * SEG;
@@ -1952,8 +2013,8 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                         for (int sh = 64; sh > 0; sh >>= 1)
                             if (c + sh < 100 && st.off[c + sh] <= e) c += sh;
                         const double2 v = xy[st.cb[c] + (e - st.off[c])];
-                        T.buf[e] = make_float2((float)((v.x * 0.5 - g.xmin2) * g.invx - ox),
-                                               (float)((v.y * 0.5 - g.ymin2) * g.invy - oy));
+                        T.buf[e] = make_float2((float)((v.x * 0.5 - o.xmin2) * g.invx - o.ox),
+                                               (float)((v.y * 0.5 - o.ymin2) * g.invy - o.oy));
                     }
                 }
             }
@@ -2859,6 +2920,66 @@ __global__ __launch_bounds__(kBlock) void permute_out_kernel(
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
 
+// Batched fits: clusters numbered per partition (LocalDBSCANNaive.scala:58 counts from 0 in every
+// fit): roots(o) = roots with a visit (batch) index below o, so partition p's ids are the batch
+// ids minus roots(offs[p]).
+__device__ __forceinline__ int32_t roots_before(const uint64_t* __restrict__ root_bits,
+                                                const int32_t* __restrict__ word_rank,
+                                                int64_t o) {
+    return word_rank[o >> 6] + __popcll(root_bits[o >> 6] & ((1ull << (o & 63)) - 1ull));
+}
+
+__global__ __launch_bounds__(kBlock) void permute_out_batch_kernel(
+    int64_t n, const int32_t* __restrict__ inv, const uint32_t* __restrict__ packed,
+    const int64_t* __restrict__ poffs, int np, const uint64_t* __restrict__ root_bits,
+    const int32_t* __restrict__ word_rank, int32_t* __restrict__ cluster_out,
+    uint8_t* __restrict__ flag_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = packed[inv[i]];
+    const int32_t c = (int32_t)(v >> 1);
+    cluster_out[i] = c ? c - roots_before(root_bits, word_rank, poffs[part_of(poffs, np, i)]) : 0;
+    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
+}
+
+// Clusters of every partition of a batch (n = the batch's span; the total is st[kStClusters]).
+__global__ __launch_bounds__(kBlock) void batch_nclusters_kernel(
+    int64_t n, const int64_t* __restrict__ poffs, int np, const uint64_t* __restrict__ root_bits,
+    const int32_t* __restrict__ word_rank, const int32_t* __restrict__ st,
+    int32_t* __restrict__ nclusters) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= np) return;
+    const int64_t a = poffs[p], b = poffs[p + 1];
+    const int32_t ra = a >= n ? st[kStClusters] : roots_before(root_bits, word_rank, a);
+    const int32_t rb = b >= n ? st[kStClusters] : roots_before(root_bits, word_rank, b);
+    nclusters[p] = rb - ra;
+}
+
+// Batched fits: the partition of every occupied tile (all of a tile's points belong to one
+// partition: each partition's grid holds its own tiles), from its first slot's batch index.
+__global__ __launch_bounds__(kBlock) void tile_part_kernel(const int32_t* __restrict__ tstart,
+                                                           const int32_t* __restrict__ ntiles_p,
+                                                           const int32_t* __restrict__ perm,
+                                                           const GridParams* __restrict__ gp,
+                                                           int32_t* __restrict__ tpart) {
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= *ntiles_p) return;
+    tpart[t] = part_of(gp->poffs, gp->nparts, perm[tstart[t]]);
+}
+
+// Bucketed sort: input order through the padded places (pos: input -> place, inv: place ->
+// slot); pos reads are coalesced, the place reads hit each band's running segment.
+__global__ __launch_bounds__(kBlock) void permute_out_bucket_kernel(
+    int64_t n, const int32_t* __restrict__ pos, const int32_t* __restrict__ inv,
+    const uint32_t* __restrict__ packed, int32_t* __restrict__ cluster_out,
+    uint8_t* __restrict__ flag_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = packed[inv[pos[i]]];
+    cluster_out[i] = (int32_t)(v >> 1);
+    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
+}
+
 // ---------------------------------------------------------------------------------------
 // LocalDBSCANArchery with its float32 R-tree search box (DBSCAN_MODE_ARCHERY_F32BOX).
 // The tree stores Point(p.x.toFloat, p.y.toFloat) (LocalDBSCANArchery.scala:38-41) and a
@@ -3167,6 +3288,14 @@ __global__ void grid_kernel(const double* __restrict__ bb, double eps, GridParam
     st[kStBits] = bits;
 }
 
+// Batched fits: the virtual grid planned on the host (plan_batch_grid).
+__global__ void batch_grid_kernel(GridParams g, int32_t nf, int32_t bits,
+                                  GridParams* __restrict__ gp, int32_t* __restrict__ st) {
+    *gp = g;
+    st[kStNf] = nf;
+    st[kStBits] = bits;
+}
+
 // All-pairs (eps*eps = +inf: one cell holding every point) and no-pairs (eps*eps NaN) fits.
 __global__ void grid_fixed_kernel(int32_t nf, GridParams* __restrict__ gp,
                                   int32_t* __restrict__ st) {
@@ -3363,13 +3492,20 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         return;
     }
 
+    // large direct fits sort through the padded bands (bucket_sort: cache-resident random writes)
+    const bool bucketed = !a.zone && !a.batch && mode == kGridEps && n >= kBucketMinPoints &&
+                          n + 256 * 2048 < (int64_t)INT32_MAX;
     uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
     uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
     int32_t* inv = static_cast<int32_t*>(ws.inv.ensure(n * sizeof(int32_t)));
     int32_t* perm = static_cast<int32_t*>(ws.perm.ensure(n * sizeof(int32_t)));
     int32_t* perm2 = static_cast<int32_t*>(ws.perm2.ensure(n * sizeof(int32_t)));
     if (mode == kGridEps) {
-        {
+        if (a.batch) {  // batched fits: the virtual grid of the partitions' local grids
+            klaunch(prof, "grid", batch_grid_kernel, dim3(1), dim3(1), 0, s, a.batch->g,
+                    a.batch->nf, a.batch->bits, gp, st);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        } else {
             StageTimer t(prof, s, "bbox");
             bbox_finite(s, a.x, a.y, n, misc, ws.scan_tmp);
             klaunch(prof, "grid", grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
@@ -3380,10 +3516,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));
-        int32_t* perm3 = static_cast<int32_t*>(ws.perm3.ensure(n * sizeof(int32_t)));
-        radix_sort_pairs(s, key, perm, key2, perm2, key3, perm3, n, &st[kStBits], ws.hist,
-                         ws.scan, prof, inv, /*iota=*/true);
+        if (bucketed) {  // large fits: MSD band split, then LSD inside the bands
+            bucket_sort(s, a.x, a.y, key, n, &st[kStBits], ws.bucket, ws.hist, ws.scan, prof);
+            key = ws.bucket.key_fin;  // (perm: written by scatter_bucket_kernel below)
+        } else {
+            uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));
+            int32_t* perm3 = static_cast<int32_t*>(ws.perm3.ensure(n * sizeof(int32_t)));
+            radix_sort_pairs(s, key, perm, key2, perm2, key3, perm3, n, &st[kStBits], ws.hist,
+                             ws.scan, prof, inv, /*iota=*/true);
+        }
     } else {
         StageTimer t(prof, s, "bin");
         // all pairs: one cell holding every point, the predicate decides (incl. non-finite)
@@ -3450,13 +3591,19 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         tcore = static_cast<uint8_t*>(ws.tcore.ensure(ntile_bound));
     }
     int32_t* tsz = static_cast<int32_t*>(ws.tsz.ensure(ntile_bound * sizeof(int32_t)));
+    int32_t* tpart =
+        a.batch ? static_cast<int32_t*>(ws.tpart.ensure(ntile_bound * sizeof(int32_t))) : nullptr;
 
     {
         StageTimer t(prof, s, "gather");
         if (mode != kGridEps)  // (eps grids: the radix sort's final pass wrote inv)
             klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
                     inv);
-        if (mode != kGridNoPairs)
+        if (bucketed)
+            klaunch(prof, "scatter_bucket", scatter_bucket_kernel, dim3(nblk(ws.bucket.np)),
+                    dim3(kBlock), 0, s, ws.bucket.np, (const int32_t*)ws.bucket.idx,
+                    (const int32_t*)ws.bucket.inv, (const double2*)ws.bucket.xy, nf_p, perm, xy);
+        else if (mode != kGridNoPairs)
             klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);
         if (zs) {
@@ -3482,6 +3629,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                                offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
+            if (tpart)
+                klaunch(prof, "tile_part", tile_part_kernel, dim3(nblk(ntile_bound)),
+                        dim3(kBlock), 0, s, tstart, &st[kStTiles], perm, gp, tpart);
         }
         {
             StageTimer t(prof, s, "tables");
@@ -3539,7 +3689,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 default: break;
             }
             const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp,
-                              tcore};
+                              tcore, tpart};
             if (box) {
                 klaunch(prof, "box_count", box_count_kernel, dim3(tile_grid), dim3(kBlock), 0, s,
                         xy, cell, seg, nf_p, a.eps, eps2, a.min_points, core, parent,
@@ -3692,8 +3842,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "box_label", box_label_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                     cell, seg, nf_p, n, a.eps, eps2, core, lab, root_bits, word_rank, cmap,
                     packed);
-            klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0,
-                    s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+            if (bucketed)
+                klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
+                        0, s, n, (const int32_t*)ws.bucket.pos, (const int32_t*)ws.bucket.inv,
+                        (const uint32_t*)packed, a.cluster, a.flag);
+            else
+                klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
+                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
             DBSCAN_HIP_CHECK(hipGetLastError());
         } else {
             StageTimer t(prof, s, "output");
@@ -3702,8 +3857,23 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                cell, seg, nbr, nbr_k, nf_p, n, eps2, a.mode, perm, core, lab,
                                root_bits, word_rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
                                (const int64_t*)nullptr, (const int32_t*)nullptr, packed);
-            klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, n, inv,
-                               packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+            if (a.batch) {  // cluster ids per partition, and each partition's count
+                const GridParams& bg = a.batch->g;
+                klaunch(prof, "permute_out", permute_out_batch_kernel, dim3(nblk(n)), dim3(kBlock),
+                        0, s, n, inv, packed, bg.poffs, bg.nparts, (const uint64_t*)root_bits,
+                        (const int32_t*)word_rank, a.cluster, a.flag);
+                klaunch(prof, "batch_nclusters", batch_nclusters_kernel,
+                        dim3(nblk(bg.nparts)), dim3(kBlock), 0, s, n, bg.poffs, bg.nparts,
+                        (const uint64_t*)root_bits, (const int32_t*)word_rank,
+                        (const int32_t*)st, a.batch->nclusters);
+            } else if (bucketed) {
+                klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
+                        0, s, n, (const int32_t*)ws.bucket.pos, (const int32_t*)ws.bucket.inv,
+                        (const uint32_t*)packed, a.cluster, a.flag);
+            } else {
+                klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
+                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+            }
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
     } else {

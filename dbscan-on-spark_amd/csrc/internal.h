@@ -149,26 +149,58 @@ struct ScanState {
     uint64_t* prepare(hipStream_t s, int64_t ntiles);  // also advances the epoch
 };
 
+// Bucketed sort (fits of >= kBucketMinPoints points, whose arrays outgrow the Infinity Cache):
+// one MSD pass on the top 8 key bits into padded per-band segments (coordinates moved along),
+// then LSD passes inside the segments.  Outputs: key_fin[n] sorted keys, slot_place[n] the
+// padded place of each sorted slot, inv[place] its slot, idx[place] its input index (-1: pad),
+// xy[place] its coordinates, pos[i] the padded place of input i; np padded places.
+constexpr int64_t kBucketMinPoints = int64_t(1) << 24;
+struct BucketSort {
+    DevBuf ka, ia, kb, jb, kc, jc, xyb, posb, invb, kf, jf, tab;
+    uint32_t* key_fin = nullptr;
+    int32_t* slot_place = nullptr;
+    int32_t* inv = nullptr;
+    int32_t* idx = nullptr;
+    double2* xy = nullptr;
+    int32_t* pos = nullptr;
+    int64_t np = 0;
+    void release() {
+        for (DevBuf* b : {&ka, &ia, &kb, &jb, &kc, &jc, &xyb, &posb, &invb, &kf, &jf, &tab})
+            b->release();
+    }
+};
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots, box_edges, box_map, tcore;
+        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab;
     ScanState scan;
+    BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
     int fit_mode = 0;
     int32_t* perm_sorted = nullptr;  // perm or perm2, whichever holds the sorted order
     uint32_t* key_sorted = nullptr;  // key or key2, likewise
     void release() {
         scan.buf.release();
+        bucket.release();
         for (DevBuf* b : {&key, &key2, &perm, &perm2, &hist, &scan_tmp, &xy, &cell, &ckey, &cstart,
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
-                          &box_edges, &box_map, &tcore})
+                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab})
             b->release();
     }
+};
+
+// Batched fits (batch.hip): each partition of a batch gets its own eps grid (origin at its bbox
+// minimum, the common cell side), placed in one virtual tile grid at a tile-aligned cell offset
+// with at least one empty cell row and column after it, so no 3x3 stencil ever reaches another
+// partition and ONE tiled fit serves the whole batch.
+struct PartGrid {
+    double xmin2, ymin2;  // local origin: cell = floor((v*0.5 - vmin2) * inv) + c0
+    int32_t cx0, cy0;     // virtual cell offset of the partition's local cell (0, 0)
+    int32_t nx, ny;       // local cells per axis; 0: the partition's points are not binned
 };
 
 struct GridParams {
@@ -176,6 +208,18 @@ struct GridParams {
     uint32_t nx, ny;                  // eps cells per axis
     uint32_t ntx, nty;                // 8x8-cell tiles per axis
     int clique;  // cell side <= eps*(1+2^-14): quarter cells are cliques of the predicate
+    // batched fits: nparts > 0 partitions [poffs[p], poffs[p+1]) each binned on parts[p]'s grid
+    // (xmin2/ymin2 above unused)
+    int32_t nparts = 0;
+    const PartGrid* parts = nullptr;
+    const int64_t* poffs = nullptr;
+};
+
+// What enqueue_fit needs for a batched fit (planned on the host by plan_batch_grid).
+struct BatchFit {
+    GridParams g;                // the virtual grid (nparts, parts, poffs set)
+    int32_t nf = 0, bits = 0;    // points inside the grid, radix key width
+    int32_t* nclusters = nullptr;  // out (device): cluster count per partition
 };
 
 struct FitStats {
@@ -206,6 +250,8 @@ struct FitArgs {
     // full fits of n <= small_max points (and a mode / eps the one-workgroup kernel serves) run
     // small.hip's single-launch fit; 0 keeps every fit on the tiled pipeline
     int64_t small_max = kSmallMaxPoints;
+    // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
+    const BatchFit* batch = nullptr;
 };
 
 // What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).
@@ -232,6 +278,15 @@ constexpr int kFitStatsDoubles = 24;
 void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst);
 FitStats parse_fit_stats(const Workspace& ws, const double* buf);
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);
+// Batched fits (batch.hip).  enqueue_batch_bbox: per-partition {xmin, xmax, ymin, ymax, finite
+// count} of [d_offs[p], d_offs[p+1]) into d_box (5 doubles each).  plan_batch_grid: from those
+// boxes (host), the virtual grid and the partition table (host, nparts entries); partitions it
+// cannot place (no clique grid, absurd extents) are listed in *alone, to be fitted on their own.
+// Returns false when no partition is placed.
+void enqueue_batch_bbox(hipStream_t s, const double* x, const double* y, const int64_t* d_offs,
+                        int32_t n_parts, double* d_box);
+bool plan_batch_grid(const double* box, const int64_t* offs, int32_t n_parts, double eps,
+                     PartGrid* table, BatchFit* bf, std::vector<int32_t>* alone);
 // The slab label in two parts around the cluster numbering: prepare (labels in terms of local
 // roots, moved to slab order; needs only gs_of_root) and finish (roots numbered, one map pass).
 void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
@@ -326,6 +381,11 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
                       int32_t*& val2, uint32_t*& key3, int32_t*& val3, int64_t n,
                       const int32_t* bits_dev, DevBuf& hist, ScanState& scan, Profiler* prof,
                       int32_t* inv = nullptr, bool iota = false);
+
+int64_t bucket_padded(int64_t n);
+void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
+                 const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
+                 Profiler* prof);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

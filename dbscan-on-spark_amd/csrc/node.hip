@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -39,6 +40,28 @@ double ulp(double c) {
 }
 double margin1(double c, double R) { return R * (1.0 + 0x1p-10) + 16.0 * ulp(c); }
 double margin2(double c, double R) { return 2.0 * margin1(c, R) + 16.0 * ulp(c); }
+
+// Host threads for the slab plan: OMP_NUM_THREADS when set (the GPU box's per-GPU CPU share),
+// else the hardware's, at most 64.
+int64_t host_threads() {
+    int64_t n = (int64_t)std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) n = std::min<int64_t>(n > 0 ? n : v, v);
+    }
+    return std::max<int64_t>(1, std::min<int64_t>(n, 64));
+}
+
+template <class F>
+void parallel_for(int nth, F&& f) {
+    if (nth <= 1) {
+        f(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t) th.emplace_back([&, t]() { f(t); });
+    for (auto& t : th) t.join();
+}
 
 // node.py make_cuts: world-1 cuts at count quantiles of a strided sample of the finite x,
 // snapped down to the 2*eps grid, non-decreasing.
@@ -274,16 +297,16 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
     const int world = (int)cuts.size() + 1;
     const double R = reach(eps);
     std::vector<Shard> sh(world);
-    for (auto& s : sh) {  // (a slab holds ~n/world points plus its halos)
-        const size_t guess = (size_t)(n / world + n / (8 * world) + 16);
-        s.gid.reserve(guess);
-        s.x.reserve(guess);
-        s.y.reserve(guess);
-        s.zone.reserve(guess);
-    }
-    for (int64_t i = 0; i < n; ++i) {  // slab plan: points in increasing global visit order
-        // only the owner and shards whose halo can reach x need a look: scan neighbours of the
-        // owner until both directions fall out of reach
+    // slab plan: every shard's points in increasing global visit order, built by host threads
+    // over contiguous chunks of the input (count, then fill at the chunk's offsets)
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / 65536 + 1));
+    std::vector<int64_t> cnt((size_t)nth * world * 2, 0);  // [thread][shard]{points, shared}
+    const auto chunk = [&](int t) {
+        return std::make_pair(n * t / nth, n * (t + 1) / nth);
+    };
+    // only the owner and shards whose halo can reach x need a look: scan neighbours of the
+    // owner until both directions fall out of reach
+    const auto visit = [&](int64_t i, auto&& f) {
         const int own = std::isnan(x[i])  // NaN x is owned by shard 0 (node.py zones)
                             ? 0
                             : (int)(std::upper_bound(cuts.begin(), cuts.end(), x[i]) -
@@ -296,15 +319,48 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                     if (r != own) break;
                     continue;
                 }
-                Shard& s = sh[r];
-                if (shared) s.shared.push_back((int32_t)s.gid.size());
-                s.gid.push_back(i);
-                s.x.push_back(x[i]);
-                s.y.push_back(y[i]);
-                s.zone.push_back(z);
+                f(r, z, shared);
             }
         }
+    };
+    parallel_for(nth, [&](int t) {
+        int64_t* c = &cnt[(size_t)t * world * 2];
+        const auto [i0, i1] = chunk(t);
+        for (int64_t i = i0; i < i1; ++i)
+            visit(i, [&](int r, uint8_t, bool shared) {
+                ++c[2 * r];
+                c[2 * r + 1] += shared ? 1 : 0;
+            });
+    });
+    std::vector<int64_t> at((size_t)nth * world * 2, 0);
+    for (int r = 0; r < world; ++r) {
+        int64_t np = 0, ns = 0;
+        for (int t = 0; t < nth; ++t) {
+            at[((size_t)t * world + r) * 2] = np;
+            at[((size_t)t * world + r) * 2 + 1] = ns;
+            np += cnt[((size_t)t * world + r) * 2];
+            ns += cnt[((size_t)t * world + r) * 2 + 1];
+        }
+        sh[r].gid.resize((size_t)np);
+        sh[r].x.resize((size_t)np);
+        sh[r].y.resize((size_t)np);
+        sh[r].zone.resize((size_t)np);
+        sh[r].shared.resize((size_t)ns);
     }
+    parallel_for(nth, [&](int t) {
+        int64_t* a = &at[(size_t)t * world * 2];
+        const auto [i0, i1] = chunk(t);
+        for (int64_t i = i0; i < i1; ++i)
+            visit(i, [&](int r, uint8_t z, bool shared) {
+                Shard& s = sh[r];
+                const int64_t k = a[2 * r]++;
+                if (shared) s.shared[(size_t)a[2 * r + 1]++] = (int32_t)k;
+                s.gid[(size_t)k] = i;
+                s.x[(size_t)k] = x[i];
+                s.y[(size_t)k] = y[i];
+                s.zone[(size_t)k] = z;
+            });
+    });
     // one host thread and one handle per device; the shards of a device run one after another
     // on its handle (one workspace per device: 8 shards of a 10^9-point job on one GPU)
     const int nworkers = std::min(world, ndev);
@@ -364,12 +420,17 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             }
     }
     if (rc == DBSCAN_OK) {
-        for (auto& s : sh)
-            for (size_t p = 0; p < s.gid.size(); ++p)
-                if (s.zone[p] == 0) {
-                    cluster_out[s.gid[p]] = s.cluster[p];
-                    flag_out[s.gid[p]] = s.flag[p];
-                }
+        // zone-0 points: each input point is owned by exactly one shard (disjoint writes)
+        parallel_for(nth, [&](int t) {
+            for (auto& s : sh) {
+                const int64_t m = (int64_t)s.gid.size(), p0 = m * t / nth, p1 = m * (t + 1) / nth;
+                for (int64_t p = p0; p < p1; ++p)
+                    if (s.zone[(size_t)p] == 0) {
+                        cluster_out[s.gid[(size_t)p]] = s.cluster[(size_t)p];
+                        flag_out[s.gid[(size_t)p]] = s.flag[(size_t)p];
+                    }
+            }
+        });
         *n_clusters_out = (int64_t)all_roots.size();
     }
     for (auto* h : hs) dbscan_destroy(h);

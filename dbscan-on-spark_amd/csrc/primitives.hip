@@ -196,7 +196,12 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
                                                                int64_t nblocks,
                                                                int32_t* __restrict__ hist) {
     constexpr int RB = 1 << W;
-    if (shift >= *bits_p) return;  // digit beyond the key width: nothing left to sort
+    if (shift < 0) {  // the bucketed sort's MSD pass: the top 8 bits of the device-side width
+        const int b = *bits_p;
+        shift = b > 8 ? b - 8 : 0;
+    } else if (shift >= *bits_p) {
+        return;  // digit beyond the key width: nothing left to sort
+    }
     __shared__ uint32_t h[kWaves][RB];
     const int w = threadIdx.x >> 6;
     for (int d = threadIdx.x; d < kWaves * RB; d += kBlock) (&h[0][0])[d] = 0;
@@ -250,7 +255,7 @@ __global__ __launch_bounds__(kOffThreads) void radix_offsets_kernel(
     uint64_t* __restrict__ state, uint32_t epoch, const int32_t* __restrict__ bits_p,
     int shift) {
     constexpr int RB = 1 << W, G = kOffThreads / RB;
-    if (shift >= *bits_p) return;
+    if (shift >= 0 && shift >= *bits_p) return;  // (shift < 0: the bucketed sort's MSD pass)
     __shared__ int gsum[G][RB], gtot[G][RB], gbef[G][RB];
     __shared__ int wsum[RB / 64];
     const int d = threadIdx.x % RB, g = threadIdx.x / RB;
@@ -478,6 +483,297 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
     }
 }
 
+// ------------------------------- bucketed radix sort -------------------------------------
+// For fits whose arrays outgrow the Infinity Cache (DESIGN.md §3 "bucketed sort"): the plain LSD
+// sort's last pass and the coordinate scatter write to random places over the whole n-sized
+// targets, and out of the 256 MB MALL every such partial-line write costs a line read and a line
+// write of HBM.  Here the sort starts with ONE MSD pass on the top 8 key bits (tile-row bands):
+// every point is moved, with its coordinates, into its band's segment of a padded array (each
+// segment starts on a 2048-key tile, pads hold the sentinel key), and then the low bits are
+// sorted by LSD passes that stay inside each segment (per-segment digit offsets).  So every
+// later random write or read (the last pass's inverse, the coordinate scatter, the label
+// gather) lands inside one band's segment: a few MB to ~100 MB, cache-resident while the
+// launch sweeps the segments in order.
+
+// Segment tables after the MSD pass (one workgroup of 256 threads = the 256 top digits):
+// from the dense digit offsets of tile 0 (= the digit bases) the bucket sizes, their padded
+// bases, the per-digit shift padded - dense, the segment tile ranges and the low key width.
+//   seg layout (int32): [0..256] first padded tile of segment d (256: the all-pad tail),
+//   [257..513] padded base, [514..770] dense base, [771..1027] count, [1028] low bits
+constexpr int kSegTile = 0, kSegPBase = 257, kSegDBase = 514, kSegCnt = 771, kSegLBits = 1028;
+constexpr int kSegInts = 1032;
+
+__global__ __launch_bounds__(256) void bucket_table_kernel(const int32_t* __restrict__ hist_off,
+                                                           int64_t n, int64_t np_max,
+                                                           const int32_t* __restrict__ bits_p,
+                                                           int32_t* __restrict__ seg,
+                                                           int32_t* __restrict__ pshift) {
+    __shared__ int ws[4];
+    const int d = threadIdx.x, lane = lane_id(), w = d >> 6;
+    const int bits = *bits_p;
+    const int32_t db = hist_off[d];  // tile 0's offsets are the digit bases
+    __shared__ int32_t dbs[257];
+    dbs[d] = db;
+    if (d == 0) dbs[256] = (int32_t)n;
+    __syncthreads();
+    const int32_t cnt = dbs[d + 1] - db;
+    const int32_t pc = (cnt + kRTile - 1) / kRTile * kRTile;
+    const int incl = wave_incl_scan(pc);
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    int before = 0;
+    for (int k = 0; k < w; ++k) before += ws[k];
+    const int32_t pb = before + incl - pc;
+    seg[kSegTile + d] = pb / kRTile;
+    seg[kSegPBase + d] = pb;
+    seg[kSegDBase + d] = db;
+    seg[kSegCnt + d] = cnt;
+    pshift[d] = pb - db;
+    if (d == 255) {  // the all-pad tail up to np_max: a segment of no real keys
+        const int32_t used = pb + pc;
+        seg[kSegTile + 256] = used / kRTile;
+        seg[kSegPBase + 256] = used;
+        seg[kSegDBase + 256] = (int32_t)n;
+        seg[kSegCnt + 256] = 0;
+        seg[kSegTile + 257] = (int32_t)(np_max / kRTile);  // (= kSegPBase: read as the end)
+        seg[kSegLBits] = bits > 8 ? bits - 8 : 0;
+    }
+}
+
+// The pads: every padded slot no real key lands on gets the sentinel key and payload -1.
+__global__ __launch_bounds__(kBlock) void bucket_pad_kernel(const int32_t* __restrict__ seg,
+                                                            int64_t np_max,
+                                                            uint32_t* __restrict__ key,
+                                                            int32_t* __restrict__ idx) {
+    const int d = blockIdx.x;  // 0..256
+    const int64_t a = (int64_t)seg[kSegPBase + d] + seg[kSegCnt + d];
+    const int64_t b = d < 256 ? (int64_t)seg[kSegPBase + d + 1] : np_max;
+    for (int64_t j = a + threadIdx.x; j < b; j += kBlock) {
+        key[j] = kSentinelKey;
+        idx[j] = -1;
+    }
+}
+
+// Per padded tile: (padded base - dense base of its segment, end of its real keys).
+__global__ __launch_bounds__(kBlock) void bucket_tseg_kernel(const int32_t* __restrict__ seg,
+                                                             int64_t ntiles,
+                                                             int2* __restrict__ tseg) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= ntiles) return;
+    int lo = 0, hi = 257;  // segment s with seg[s] <= t < seg[s + 1] (tail: s = 256)
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (seg[kSegTile + mid] <= t) lo = mid; else hi = mid;
+    }
+    tseg[t] = make_int2(seg[kSegPBase + lo] - seg[kSegDBase + lo],
+                        seg[kSegPBase + lo] + seg[kSegCnt + lo]);
+}
+
+// Per-segment digit offsets for an LSD pass over the padded array: one workgroup per segment
+// (257: the tail's pads too), RB digits x G row groups; off[t][d] = padded base of t's segment
+// + the segment's keys of smaller digits + digit d's keys in the segment's earlier tiles.
+template <int W>
+__global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __restrict__ cnt,
+                                                              int32_t* __restrict__ off,
+                                                              const int32_t* __restrict__ seg,
+                                                              int shift) {
+    constexpr int RB = 1 << W, G = 1024 / RB;
+    if (shift >= seg[kSegLBits]) return;
+    __shared__ int gsum[G][RB];
+    __shared__ int dex[RB];
+    __shared__ int wsum[(RB + 63) / 64];
+    const int s = blockIdx.x;
+    const int64_t t0 = seg[kSegTile + s], t1 = seg[kSegTile + s + 1];
+    const int d = threadIdx.x % RB, g = threadIdx.x / RB;
+    const int64_t per = (t1 - t0 + G - 1) / G;
+    const int64_t r0 = t0 + g * per < t1 ? t0 + g * per : t1;
+    const int64_t r1 = r0 + per < t1 ? r0 + per : t1;
+    int agg = 0;
+    for (int64_t r = r0; r < r1; ++r) agg += cnt[r * RB + d];
+    gsum[g][d] = agg;
+    __syncthreads();
+    if (g == 0) {  // the segment's digit totals, exclusive scan over the digits
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < G; ++q) tot += gsum[q][d];
+        const int incl = wave_incl_scan(tot);
+        if ((d & 63) == 63) wsum[d >> 6] = incl;
+        dex[d] = incl - tot;
+    }
+    __syncthreads();
+    int run = seg[kSegPBase + s] + dex[d];
+    for (int q = 0; q < (d >> 6); ++q) run += wsum[q];
+    for (int q = 0; q < g; ++q) run += gsum[q][d];
+    for (int64_t r = r0; r < r1; ++r) {
+        const int c = cnt[r * RB + d];
+        off[r * RB + d] = run;
+        run += c;
+    }
+}
+
+// The MSD pass and the segmented LSD passes: radix_downsweep_kernel's ranking (one 2048-key
+// tile per workgroup, per-wave match-any ballots, the tile sorted in LDS, digit runs written
+// coalesced), with
+//   MODE 1 (MSD split, top 8 bits: shift = bits - 8 from the device): payload = input index;
+//          digit d's run goes to its padded segment (pshift[d]); each point's coordinates go
+//          to its padded place too (xy_out), and pos[i] = that place
+//   MODE 2 (LSD within segments, bits = the low width, seg[kSegLBits]): payload = padded
+//          place (identity on the first pass); the last pass writes the dense order: key_fin,
+//          val_fin (slot -> padded place) and inv (padded place -> slot), pads dropped
+struct BucketExtra {
+    const double* x;
+    const double* y;
+    double2* xy_out;
+    int32_t* pos;
+    const int32_t* pshift;
+    const int2* tseg;
+    int32_t* inv;
+};
+
+template <int W, int MODE>
+__global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
+    uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, uint32_t* __restrict__ key_fin,
+    int32_t* __restrict__ val_fin, int64_t n, int shift, const int32_t* __restrict__ bits_p,
+    const int32_t* __restrict__ hist_off, BucketExtra ex) {
+    constexpr int RB = 1 << W;
+    constexpr int DPT = RB > kBlock ? RB / kBlock : 1;
+    __shared__ DownsweepSmem<W> sm;
+    const int t = threadIdx.x, w = t >> 6, lane = lane_id();
+    const int64_t base = (int64_t)blockIdx.x * kRTile;
+    const int tile_n = (int)((n - base) < kRTile ? (n - base) : kRTile);
+    bool last = false;
+    if constexpr (MODE == 1) {
+        const int bits = *bits_p;
+        shift = bits > 8 ? bits - 8 : 0;
+    } else {
+        const int bits = *bits_p;
+        if (bits == 0) {  // the MSD pass sorted everything: the dense copy (first pass only)
+            if (shift != 0) return;
+            const int2 ts = ex.tseg[blockIdx.x];
+            for (int j = t; j < tile_n; j += kBlock) {
+                const int64_t gp = base + j;
+                if (gp >= ts.y) continue;
+                const int64_t g = gp - ts.x;
+                const int32_t v = val ? val[gp] : (int32_t)gp;
+                key_fin[g] = key[gp];
+                val_fin[g] = v;
+                ex.inv[v] = (int32_t)g;
+            }
+            return;
+        }
+        if (shift >= bits) return;
+        last = shift + W >= bits;
+    }
+    for (int k = t; k < kWaves * RB; k += kBlock) (&sm.cnt[0][0])[k] = 0;
+    __syncthreads();
+
+    uint32_t k_r[kRItems];
+    int32_t v_r[kRItems];
+    uint32_t dr[kRItems];
+    double2 c_r[MODE == 1 ? kRItems : 1];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {
+        const int64_t i = wbase + r * 64 + lane;
+        const bool valid = i < base + tile_n;
+        const uint32_t k = valid ? key[i] : kSentinelKey;
+        const int32_t v = valid ? (val ? val[i] : (int32_t)i) : 0;
+        if constexpr (MODE == 1)
+            c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
+        const uint32_t d = (k >> shift) & (RB - 1u);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < W; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        int old = 0;
+        if (valid && lane == leader) {
+            old = sm.cnt[w][d];
+            sm.cnt[w][d] = old + __popcll(peers);
+        }
+        old = __shfl(old, leader, 64);
+        k_r[r] = k;
+        v_r[r] = v;
+        dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 10)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    {
+        int tot[DPT];
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            int running = 0;
+            if (dd < RB) {
+#pragma unroll
+                for (int k = 0; k < kWaves; ++k) {
+                    const int c = sm.cnt[k][dd];
+                    sm.cnt[k][dd] = running;
+                    running += c;
+                }
+            }
+            tot[j] = running;
+            mine += running;
+        }
+        const int incl = wave_incl_scan(mine);
+        if (lane == 63) sm.wsum[w] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int q = 0; q < w; ++q) woff += sm.wsum[q];
+        int at = woff + incl - mine;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            if (dd < RB) {
+                sm.tile_start[dd] = at;
+                int32_t go = hist_off[(int64_t)blockIdx.x * RB + dd];
+                if constexpr (MODE == 1) go += ex.pshift[dd];
+                sm.gofs[dd] = go;
+            }
+            at += tot[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {
+        if (dr[r] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[r] & 1023u;
+            const int within = sm.cnt[w][d] + (int)(dr[r] >> 10);
+            const int lpos = sm.tile_start[d] + within;
+            sm.keys[lpos] = k_r[r];
+            sm.vals[lpos] = v_r[r];
+            if constexpr (MODE == 1) {  // coordinates and place straight from registers
+                const int64_t g = (int64_t)sm.gofs[d] + within;
+                ex.xy_out[g] = c_r[r];
+                ex.pos[v_r[r]] = (int32_t)g;
+            }
+        }
+    }
+    __syncthreads();
+    const int2 ts = (MODE == 2 && last) ? ex.tseg[blockIdx.x] : make_int2(0, 0);
+    for (int j = t; j < tile_n; j += kBlock) {
+        const uint32_t k = sm.keys[j];
+        const uint32_t d = (k >> shift) & (RB - 1u);
+        const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
+        const int32_t v = sm.vals[j];
+        if (MODE == 2 && last) {
+            if (g >= ts.y) continue;  // a pad (pads sort after the segment's keys)
+            const int64_t gd = g - ts.x;
+            key_fin[gd] = k;
+            val_fin[gd] = v;
+            ex.inv[v] = (int32_t)gd;
+        } else {
+            key_out[g] = k;
+            val_out[g] = v;
+        }
+    }
+}
+
 // ------------------------------------ bbox -----------------------------------------------
 
 __device__ __forceinline__ double wave_min(double v) {
@@ -674,6 +970,85 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
     // the sorted pairs are in C whatever the key width
     std::swap(key, key3);
     std::swap(val, val3);
+}
+
+int64_t bucket_padded(int64_t n) { return ((n + kRTile - 1) / kRTile + 256) * kRTile; }
+
+void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
+                 const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
+                 Profiler* prof) {
+    if (n <= 0) return;
+    const int64_t np = bucket_padded(n), ntp = np / kRTile, nb = (n + kRTile - 1) / kRTile;
+    int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * ntp * 512 * sizeof(int32_t)));
+    int32_t* ho = h + ntp * 512;
+    uint32_t* ka = static_cast<uint32_t*>(b.ka.ensure(np * sizeof(uint32_t)));
+    int32_t* ia = static_cast<int32_t*>(b.ia.ensure(np * sizeof(int32_t)));
+    uint32_t* kb = static_cast<uint32_t*>(b.kb.ensure(np * sizeof(uint32_t)));
+    int32_t* jb = static_cast<int32_t*>(b.jb.ensure(np * sizeof(int32_t)));
+    uint32_t* kc = static_cast<uint32_t*>(b.kc.ensure(np * sizeof(uint32_t)));
+    int32_t* jc = static_cast<int32_t*>(b.jc.ensure(np * sizeof(int32_t)));
+    b.xy = static_cast<double2*>(b.xyb.ensure(np * sizeof(double2)));
+    b.pos = static_cast<int32_t*>(b.posb.ensure(n * sizeof(int32_t)));
+    b.inv = static_cast<int32_t*>(b.invb.ensure(np * sizeof(int32_t)));
+    b.key_fin = static_cast<uint32_t*>(b.kf.ensure(n * sizeof(uint32_t)));
+    b.slot_place = static_cast<int32_t*>(b.jf.ensure(n * sizeof(int32_t)));
+    int32_t* tab = static_cast<int32_t*>(
+        b.tab.ensure((kSegInts + 256) * sizeof(int32_t) + ntp * sizeof(int2)));
+    int32_t* seg = tab;
+    int32_t* pshift = tab + kSegInts;
+    int2* tseg = reinterpret_cast<int2*>(tab + kSegInts + 256);
+    b.idx = ia;
+    b.np = np;
+    {  // the MSD pass: top 8 bits, into padded segments, coordinates moved along
+        StageTimer st(prof, s, "sort_msd");
+        klaunch(prof, "radix_upsweep<8>", radix_upsweep_kernel<8>, dim3((unsigned)nb),
+                dim3(kBlock), 0, s, key, n, -1, bits_dev, nb, h);
+        uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 512);
+        klaunch(prof, "radix_offsets<8>", radix_offsets_kernel<8>, dim3(kOffBlocks),
+                dim3(kOffThreads), 0, s, (const int32_t*)h, nb, ho, state, scan.epoch, bits_dev,
+                -1);
+        klaunch(prof, "bucket_table", bucket_table_kernel, dim3(1), dim3(256), 0, s,
+                (const int32_t*)ho, n, np, bits_dev, seg, pshift);
+        klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(257), dim3(kBlock), 0, s,
+                (const int32_t*)seg, np, ka, ia);
+        const BucketExtra ex{x, y, b.xy, b.pos, pshift, nullptr, nullptr};
+        klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
+                dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, ia, (uint32_t*)nullptr,
+                (int32_t*)nullptr, n, 0, bits_dev, (const int32_t*)ho, ex);
+        klaunch(prof, "bucket_tseg", bucket_tseg_kernel,
+                dim3((unsigned)((ntp + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                (const int32_t*)seg, ntp, tseg);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+    }
+    // LSD passes over the low bits inside the segments (payload: padded place)
+    const int32_t* lbits = seg + kSegLBits;
+    const uint32_t* kin = ka;
+    const int32_t* vin = nullptr;  // the first pass generates the identity
+    uint32_t* kout = kb;
+    int32_t* vout = jb;
+    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, tseg, b.inv};
+    const auto pass = [&](auto wtag, int shift) {
+        constexpr int W = decltype(wtag)::value;
+        StageTimer st(prof, s, "sort_bucket");
+        const char* dn = W == 8 ? "bucket_lsd<8>" : "bucket_lsd<9>";
+        klaunch(prof, W == 8 ? "radix_upsweep<8>" : "radix_upsweep<9>", radix_upsweep_kernel<W>,
+                dim3((unsigned)ntp), dim3(kBlock), 0, s, (const uint32_t*)kin, np, shift, lbits,
+                ntp, h);
+        klaunch(prof, W == 8 ? "bucket_offsets<8>" : "bucket_offsets<9>",
+                bucket_offsets_kernel<W>, dim3(257), dim3(1024), 0, s, (const int32_t*)h, ho,
+                (const int32_t*)seg, shift);
+        klaunch(prof, dn, bucket_downsweep_kernel<W, 2>, dim3((unsigned)ntp), dim3(kBlock), 0, s,
+                kin, vin, kout, vout, b.key_fin, b.slot_place, np, shift, lbits,
+                (const int32_t*)ho, ex);
+        DBSCAN_HIP_CHECK(hipGetLastError());
+        kin = kout;
+        vin = vout;
+        kout = kout == kb ? kc : kb;
+        vout = vout == jb ? jc : jb;
+    };
+    pass(std::integral_constant<int, 8>{}, 0);
+    pass(std::integral_constant<int, 8>{}, 8);
+    pass(std::integral_constant<int, 9>{}, 16);
 }
 
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
