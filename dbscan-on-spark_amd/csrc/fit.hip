@@ -239,23 +239,20 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
     if (p < *nf_p) xy[p] = make_double2(x[i], y[i]);
 }
 
-// Bucketed sort (large fits): perm and the sorted coordinates from the padded band segments,
-// one coalesced pass over the places; every write lands inside the place's band (its segment's
-// slot range), which stays cache-resident while the launch sweeps the bands in order.
-__global__ __launch_bounds__(kBlock) void scatter_bucket_kernel(int64_t np,
-                                                                const int32_t* __restrict__ idx,
-                                                                const int32_t* __restrict__ inv,
-                                                                const double2* __restrict__ xyb,
-                                                                const int32_t* __restrict__ nf_p,
-                                                                int32_t* __restrict__ perm,
-                                                                double2* __restrict__ xy) {
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= np) return;
-    const int32_t i = idx[j];
-    if (i < 0) return;  // a pad
-    const int32_t p = inv[j];
-    perm[p] = i;
-    if (p < *nf_p) xy[p] = xyb[j];
+// Bucketed sort (large fits): perm and the sorted coordinates from the padded places, in slot
+// order: one 32-B record (x, y, input index) read per slot from inside its band's segment
+// (cache-resident while the launch sweeps the bands in order), coalesced writes.
+__global__ __launch_bounds__(kBlock) void gather_bucket_kernel(int64_t n,
+                                                               const int32_t* __restrict__ place,
+                                                               const double4* __restrict__ rec,
+                                                               const int32_t* __restrict__ nf_p,
+                                                               int32_t* __restrict__ perm,
+                                                               double2* __restrict__ xy) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const double4 r = rec[place[p]];
+    perm[p] = (int32_t)__double_as_longlong(r.z);
+    if (p < *nf_p) xy[p] = make_double2(r.x, r.y);
 }
 
 // Slab fits: the zone-2 points (count candidates, never core) marked in sorted order (zs,
@@ -2820,7 +2817,8 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const uint64_t* __restrict__ root_bits, const int32_t* __restrict__ word_rank,
     const uint8_t* __restrict__ zone,
     const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
-    const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed) {
+    const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed,
+    const int32_t* __restrict__ place) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const int64_t nf = *nf_p;
@@ -2902,7 +2900,7 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
             v = cl << 1;  // Border
         }
     }
-    packed[p] = v;
+    packed[place ? place[p] : p] = v;  // (bucketed sort: at the slot's padded place)
 }
 
 // Input order: cluster = packed >> 1; flag Core (odd), Border (even, nonzero), Noise (0).
@@ -2967,15 +2965,15 @@ __global__ __launch_bounds__(kBlock) void tile_part_kernel(const int32_t* __rest
     tpart[t] = part_of(gp->poffs, gp->nparts, perm[tstart[t]]);
 }
 
-// Bucketed sort: input order through the padded places (pos: input -> place, inv: place ->
-// slot); pos reads are coalesced, the place reads hit each band's running segment.
+// Bucketed sort: input order from the labels at the padded places (pos: input -> place); pos
+// reads are coalesced, and a block's points read from the 256 bands' segments where they
+// stand in input order (runs that advance together).
 __global__ __launch_bounds__(kBlock) void permute_out_bucket_kernel(
-    int64_t n, const int32_t* __restrict__ pos, const int32_t* __restrict__ inv,
-    const uint32_t* __restrict__ packed, int32_t* __restrict__ cluster_out,
-    uint8_t* __restrict__ flag_out) {
+    int64_t n, const int32_t* __restrict__ pos, const uint32_t* __restrict__ packed,
+    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const uint32_t v = packed[inv[pos[i]]];
+    const uint32_t v = packed[pos[i]];
     cluster_out[i] = (int32_t)(v >> 1);
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
@@ -3116,7 +3114,8 @@ __global__ __launch_bounds__(kBlock) void box_label_kernel(
     const Seg* __restrict__ seg, const int32_t* __restrict__ nf_p, int64_t n, double eps,
     double eps2, const uint8_t* __restrict__ core, const int32_t* __restrict__ lab,
     const uint64_t* __restrict__ root_bits, const int32_t* __restrict__ word_rank,
-    const int32_t* __restrict__ cmap, uint32_t* __restrict__ packed) {
+    const int32_t* __restrict__ cmap, uint32_t* __restrict__ packed,
+    const int32_t* __restrict__ place) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     auto number = [&](int j) -> uint32_t {
@@ -3141,7 +3140,7 @@ __global__ __launch_bounds__(kBlock) void box_label_kernel(
         });
         if (best != 0xFFFFFFFFu) v = best << 1;  // Border
     }
-    packed[p] = v;
+    packed[place ? place[p] : p] = v;  // (bucketed sort: at the slot's padded place)
 }
 
 // Two-part slab label (dbscan_slab_roots_prepare_device + dbscan_slab_label_finish_device_async):
@@ -3470,8 +3469,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     ws.fit_n = n;
     ws.fit_mode = mode;
     double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
-    GridParams* gp = reinterpret_cast<GridParams*>(misc + 8);
-    int32_t* st = reinterpret_cast<int32_t*>(misc + 16);
+    GridParams* gp = reinterpret_cast<GridParams*>(misc + kMiscGrid);
+    int32_t* st = reinterpret_cast<int32_t*>(misc + kMiscState);
     DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
     if (n == 0) {
         if (slab) {
@@ -3600,9 +3599,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
                     inv);
         if (bucketed)
-            klaunch(prof, "scatter_bucket", scatter_bucket_kernel, dim3(nblk(ws.bucket.np)),
-                    dim3(kBlock), 0, s, ws.bucket.np, (const int32_t*)ws.bucket.idx,
-                    (const int32_t*)ws.bucket.inv, (const double2*)ws.bucket.xy, nf_p, perm, xy);
+            klaunch(prof, "gather_bucket", gather_bucket_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
+                    n, (const int32_t*)ws.bucket.slot_place, (const double4*)ws.bucket.rec, nf_p,
+                    perm, xy);
         else if (mode != kGridNoPairs)
             klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);
@@ -3838,25 +3837,28 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             StageTimer t(prof, s, "output");
             const int32_t* cmap = resolve_box_pairs(s, ws, st, lab, root_bits, word_rank, xy,
                                                     cell, seg, nf_p, n, a.eps, eps2, core);
-            uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
+            uint32_t* packed = static_cast<uint32_t*>(
+                ws.packed.ensure((bucketed ? ws.bucket.np : n) * sizeof(uint32_t)));
             klaunch(prof, "box_label", box_label_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                     cell, seg, nf_p, n, a.eps, eps2, core, lab, root_bits, word_rank, cmap,
-                    packed);
+                    packed, bucketed ? (const int32_t*)ws.bucket.slot_place : nullptr);
             if (bucketed)
                 klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
-                        0, s, n, (const int32_t*)ws.bucket.pos, (const int32_t*)ws.bucket.inv,
-                        (const uint32_t*)packed, a.cluster, a.flag);
+                        0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
+                        a.flag);
             else
                 klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
                         0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
             DBSCAN_HIP_CHECK(hipGetLastError());
         } else {
             StageTimer t(prof, s, "output");
-            uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(n * sizeof(uint32_t)));
+            uint32_t* packed = static_cast<uint32_t*>(
+                ws.packed.ensure((bucketed ? ws.bucket.np : n) * sizeof(uint32_t)));
             klaunch(prof, "label_sorted", label_sorted_kernel<false>, dim3(nblk(n)), dim3(kBlock), 0, s, xy,
                                cell, seg, nbr, nbr_k, nf_p, n, eps2, a.mode, perm, core, lab,
                                root_bits, word_rank, (const uint8_t*)nullptr, (const int64_t*)nullptr,
-                               (const int64_t*)nullptr, (const int32_t*)nullptr, packed);
+                               (const int64_t*)nullptr, (const int32_t*)nullptr, packed,
+                               bucketed ? (const int32_t*)ws.bucket.slot_place : nullptr);
             if (a.batch) {  // cluster ids per partition, and each partition's count
                 const GridParams& bg = a.batch->g;
                 klaunch(prof, "permute_out", permute_out_batch_kernel, dim3(nblk(n)), dim3(kBlock),
@@ -3868,8 +3870,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         (const int32_t*)st, a.batch->nclusters);
             } else if (bucketed) {
                 klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
-                        0, s, n, (const int32_t*)ws.bucket.pos, (const int32_t*)ws.bucket.inv,
-                        (const uint32_t*)packed, a.cluster, a.flag);
+                        0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
+                        a.flag);
             } else {
                 klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
                         0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
@@ -3919,7 +3921,7 @@ void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
         DBSCAN_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(int32_t), s));
         return;
     }
-    const int32_t* st = reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16);
+    const int32_t* st = reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + kMiscState);
     hipLaunchKernelGGL(nclusters_kernel, dim3(1), dim3(1), 0, s, st, d_out);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
@@ -3943,10 +3945,9 @@ FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
     stats.grid_mode = ws.fit_mode;
     if (ws.fit_n == 0) return stats;
     GridParams g;
-    memcpy(&g, buf + 8, sizeof(g));
+    memcpy(&g, buf + kMiscGrid, sizeof(g));
     int32_t v[kStTileBuckets];  // (the stats copy holds the states before the buckets)
-    static_assert(16 * sizeof(double) + sizeof(v) <= kFitStatsDoubles * sizeof(double), "stats copy too short");
-    memcpy(v, buf + 16, sizeof(v));
+    memcpy(v, buf + kMiscState, sizeof(v));
     if (v[kStError]) throw ArgError{"cannot size the eps grid"};
     stats.nf = v[kStNf];
     if (ws.fit_mode == kGridEps && stats.nf == 0) stats.grid_mode = kGridNoPairs;
@@ -3991,11 +3992,11 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     klaunch(prof, "label_sorted", label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
                        static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
-                       reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) +
+                       reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + kMiscState) +
                            kStNf,
                        st.n, st.eps2, mode, perm, core, lab, (const uint64_t*)nullptr,
                        (const int32_t*)nullptr, zone, gid,
-                       gs_of_root, label_of_root, packed);
+                       gs_of_root, label_of_root, packed, (const int32_t*)nullptr);
     klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
                        static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
@@ -4011,11 +4012,11 @@ void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
     klaunch(prof, "label_sorted", label_sorted_kernel<true, true>, dim3(nblk(st.n)), dim3(kBlock), 0,
             s, static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
             static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
-            reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + 16) + kStNf, st.n,
+            reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + kMiscState) + kStNf, st.n,
             st.eps2, mode, static_cast<const int32_t*>(ws.perm_sorted),
             static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
             (const uint64_t*)nullptr, (const int32_t*)nullptr, zone, gid, gs_of_root,
-            (const int32_t*)nullptr, packed);
+            (const int32_t*)nullptr, packed, (const int32_t*)nullptr);
     uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
     klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
             static_cast<const int32_t*>(ws.inv.p), packed, zone, spacked);

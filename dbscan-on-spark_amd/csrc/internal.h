@@ -150,25 +150,27 @@ struct ScanState {
 };
 
 // Bucketed sort (fits of >= kBucketMinPoints points, whose arrays outgrow the Infinity Cache):
-// one MSD pass on the top 8 key bits into padded per-band segments (coordinates moved along),
-// then LSD passes inside the segments.  Outputs: key_fin[n] sorted keys, slot_place[n] the
-// padded place of each sorted slot, inv[place] its slot, idx[place] its input index (-1: pad),
-// xy[place] its coordinates, pos[i] the padded place of input i; np padded places.
-constexpr int64_t kBucketMinPoints = int64_t(1) << 24;
+// one MSD pass on the top 8 key bits into padded per-band segments, each point's record (x, y,
+// input index) moved to its padded place, then LSD passes inside the segments.  Outputs:
+// key_fin[n] sorted keys, slot_place[n] the padded place of each sorted slot, rec[place] the
+// record there, pos[i] the padded place of input i; np padded places.
+// DBSCAN_AB_BUCKET_LOG2: A/B builds only (tools/build_ab.sh), never the shipped library
+#ifndef DBSCAN_AB_BUCKET_LOG2
+#define DBSCAN_AB_BUCKET_LOG2 24
+#endif
+constexpr int64_t kBucketMinPoints = int64_t(1) << DBSCAN_AB_BUCKET_LOG2;
 struct BucketSort {
-    DevBuf ka, ia, kb, jb, kc, jc, xyb, posb, invb, kf, jf, tab;
+    DevBuf ka, kb, jb, kc, jc, recb, posb, kf, jf, tab;
     uint32_t* key_fin = nullptr;
     int32_t* slot_place = nullptr;
-    int32_t* inv = nullptr;
-    int32_t* idx = nullptr;
-    double2* xy = nullptr;
+    double4* rec = nullptr;
     int32_t* pos = nullptr;
     int64_t np = 0;
     void release() {
-        for (DevBuf* b : {&ka, &ia, &kb, &jb, &kc, &jc, &xyb, &posb, &invb, &kf, &jf, &tab})
-            b->release();
+        for (DevBuf* b : {&ka, &kb, &jb, &kc, &jc, &recb, &posb, &kf, &jf, &tab}) b->release();
     }
 };
+
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
@@ -274,7 +276,14 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
 FitStats read_fit_stats(hipStream_t s, Workspace& ws);
 // read_fit_stats in two halves: an asynchronous copy of the stats block to dst (pinned host
 // memory, kFitStatsDoubles doubles), and its parse once the copy has completed.
-constexpr int kFitStatsDoubles = 24;
+constexpr int kFitStatsDoubles = 32;
+// The handle's misc block (doubles): [0, 8) bbox scratch, [kMiscGrid, kMiscState) the device
+// GridParams, then the FitState ints.
+constexpr int kMiscGrid = 8, kMiscState = 24;
+static_assert(sizeof(GridParams) <= (kMiscState - kMiscGrid) * sizeof(double),
+              "GridParams overlaps the fit state");
+static_assert(kMiscState * sizeof(double) + kStTileBuckets * sizeof(int32_t) <=
+                  kFitStatsDoubles * sizeof(double), "the stats copy must hold the states");
 void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst);
 FitStats parse_fit_stats(const Workspace& ws, const double* buf);
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);

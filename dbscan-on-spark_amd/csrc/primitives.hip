@@ -498,9 +498,9 @@ __global__ __launch_bounds__(kBlock) void radix_downsweep_kernel(
 // Segment tables after the MSD pass (one workgroup of 256 threads = the 256 top digits):
 // from the dense digit offsets of tile 0 (= the digit bases) the bucket sizes, their padded
 // bases, the per-digit shift padded - dense, the segment tile ranges and the low key width.
-//   seg layout (int32): [0..256] first padded tile of segment d (256: the all-pad tail),
-//   [257..513] padded base, [514..770] dense base, [771..1027] count, [1028] low bits
-constexpr int kSegTile = 0, kSegPBase = 257, kSegDBase = 514, kSegCnt = 771, kSegLBits = 1028;
+//   seg layout (int32): [0..257] first padded tile of segment d (256: the all-pad tail; 257:
+//   the end), [258..514] padded base, [515..771] dense base, [772..1028] count, [1029] low bits
+constexpr int kSegTile = 0, kSegPBase = 258, kSegDBase = 515, kSegCnt = 772, kSegLBits = 1029;
 constexpr int kSegInts = 1032;
 
 __global__ __launch_bounds__(256) void bucket_table_kernel(const int32_t* __restrict__ hist_off,
@@ -535,22 +535,20 @@ __global__ __launch_bounds__(256) void bucket_table_kernel(const int32_t* __rest
         seg[kSegPBase + 256] = used;
         seg[kSegDBase + 256] = (int32_t)n;
         seg[kSegCnt + 256] = 0;
-        seg[kSegTile + 257] = (int32_t)(np_max / kRTile);  // (= kSegPBase: read as the end)
+        seg[kSegTile + 257] = (int32_t)(np_max / kRTile);
         seg[kSegLBits] = bits > 8 ? bits - 8 : 0;
     }
 }
 
-// The pads: every padded slot no real key lands on gets the sentinel key and payload -1.
+// The pads: every padded slot no real key lands on gets the sentinel key.
 __global__ __launch_bounds__(kBlock) void bucket_pad_kernel(const int32_t* __restrict__ seg,
                                                             int64_t np_max,
-                                                            uint32_t* __restrict__ key,
-                                                            int32_t* __restrict__ idx) {
+                                                            uint32_t* __restrict__ key) {
     const int d = blockIdx.x;  // 0..256
     const int64_t a = (int64_t)seg[kSegPBase + d] + seg[kSegCnt + d];
     const int64_t b = d < 256 ? (int64_t)seg[kSegPBase + d + 1] : np_max;
     for (int64_t j = a + threadIdx.x; j < b; j += kBlock) {
         key[j] = kSentinelKey;
-        idx[j] = -1;
     }
 }
 
@@ -614,20 +612,20 @@ __global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __r
 // The MSD pass and the segmented LSD passes: radix_downsweep_kernel's ranking (one 2048-key
 // tile per workgroup, per-wave match-any ballots, the tile sorted in LDS, digit runs written
 // coalesced), with
-//   MODE 1 (MSD split, top 8 bits: shift = bits - 8 from the device): payload = input index;
-//          digit d's run goes to its padded segment (pshift[d]); each point's coordinates go
-//          to its padded place too (xy_out), and pos[i] = that place
+//   MODE 1 (MSD split, top 8 bits: shift = bits - 8 from the device): only the keys are
+//          written by digit run, to the digit's padded segment (pshift[d]); each point's record
+//          (x, y, input index) goes to its padded place straight from registers (rec_out), and
+//          pos[i] = that place
 //   MODE 2 (LSD within segments, bits = the low width, seg[kSegLBits]): payload = padded
-//          place (identity on the first pass); the last pass writes the dense order: key_fin,
-//          val_fin (slot -> padded place) and inv (padded place -> slot), pads dropped
+//          place (identity on the first pass); the last pass writes the dense order: key_fin
+//          and val_fin (slot -> padded place), pads dropped
 struct BucketExtra {
     const double* x;
     const double* y;
-    double2* xy_out;
+    double4* rec_out;  // MODE 1: (x, y, input index bits, 0) per padded place
     int32_t* pos;
     const int32_t* pshift;
     const int2* tseg;
-    int32_t* inv;
 };
 
 template <int W, int MODE>
@@ -658,7 +656,6 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
                 const int32_t v = val ? val[gp] : (int32_t)gp;
                 key_fin[g] = key[gp];
                 val_fin[g] = v;
-                ex.inv[v] = (int32_t)g;
             }
             return;
         }
@@ -747,9 +744,10 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
             const int lpos = sm.tile_start[d] + within;
             sm.keys[lpos] = k_r[r];
             sm.vals[lpos] = v_r[r];
-            if constexpr (MODE == 1) {  // coordinates and place straight from registers
+            if constexpr (MODE == 1) {  // the record and the place straight from registers
                 const int64_t g = (int64_t)sm.gofs[d] + within;
-                ex.xy_out[g] = c_r[r];
+                ex.rec_out[g] = make_double4(c_r[r].x, c_r[r].y,
+                                             __longlong_as_double((long long)v_r[r]), 0.0);
                 ex.pos[v_r[r]] = (int32_t)g;
             }
         }
@@ -766,10 +764,9 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
             const int64_t gd = g - ts.x;
             key_fin[gd] = k;
             val_fin[gd] = v;
-            ex.inv[v] = (int32_t)gd;
         } else {
             key_out[g] = k;
-            val_out[g] = v;
+            if (MODE != 1) val_out[g] = v;
         }
     }
 }
@@ -982,14 +979,12 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * ntp * 512 * sizeof(int32_t)));
     int32_t* ho = h + ntp * 512;
     uint32_t* ka = static_cast<uint32_t*>(b.ka.ensure(np * sizeof(uint32_t)));
-    int32_t* ia = static_cast<int32_t*>(b.ia.ensure(np * sizeof(int32_t)));
     uint32_t* kb = static_cast<uint32_t*>(b.kb.ensure(np * sizeof(uint32_t)));
     int32_t* jb = static_cast<int32_t*>(b.jb.ensure(np * sizeof(int32_t)));
     uint32_t* kc = static_cast<uint32_t*>(b.kc.ensure(np * sizeof(uint32_t)));
     int32_t* jc = static_cast<int32_t*>(b.jc.ensure(np * sizeof(int32_t)));
-    b.xy = static_cast<double2*>(b.xyb.ensure(np * sizeof(double2)));
+    b.rec = static_cast<double4*>(b.recb.ensure(np * sizeof(double4)));
     b.pos = static_cast<int32_t*>(b.posb.ensure(n * sizeof(int32_t)));
-    b.inv = static_cast<int32_t*>(b.invb.ensure(np * sizeof(int32_t)));
     b.key_fin = static_cast<uint32_t*>(b.kf.ensure(n * sizeof(uint32_t)));
     b.slot_place = static_cast<int32_t*>(b.jf.ensure(n * sizeof(int32_t)));
     int32_t* tab = static_cast<int32_t*>(
@@ -997,7 +992,6 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     int32_t* seg = tab;
     int32_t* pshift = tab + kSegInts;
     int2* tseg = reinterpret_cast<int2*>(tab + kSegInts + 256);
-    b.idx = ia;
     b.np = np;
     {  // the MSD pass: top 8 bits, into padded segments, coordinates moved along
         StageTimer st(prof, s, "sort_msd");
@@ -1010,10 +1004,11 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
         klaunch(prof, "bucket_table", bucket_table_kernel, dim3(1), dim3(256), 0, s,
                 (const int32_t*)ho, n, np, bits_dev, seg, pshift);
         klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(257), dim3(kBlock), 0, s,
-                (const int32_t*)seg, np, ka, ia);
-        const BucketExtra ex{x, y, b.xy, b.pos, pshift, nullptr, nullptr};
+                (const int32_t*)seg, np, ka);
+        const BucketExtra ex{x, y, b.rec, b.pos, pshift, nullptr};
         klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
-                dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, ia, (uint32_t*)nullptr,
+                dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, (int32_t*)nullptr,
+                (uint32_t*)nullptr,
                 (int32_t*)nullptr, n, 0, bits_dev, (const int32_t*)ho, ex);
         klaunch(prof, "bucket_tseg", bucket_tseg_kernel,
                 dim3((unsigned)((ntp + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
@@ -1026,7 +1021,7 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     const int32_t* vin = nullptr;  // the first pass generates the identity
     uint32_t* kout = kb;
     int32_t* vout = jb;
-    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, tseg, b.inv};
+    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, tseg};
     const auto pass = [&](auto wtag, int shift) {
         constexpr int W = decltype(wtag)::value;
         StageTimer st(prof, s, "sort_bucket");
@@ -1046,9 +1041,11 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
         kout = kout == kb ? kc : kb;
         vout = vout == jb ? jc : jb;
     };
-    pass(std::integral_constant<int, 8>{}, 0);
-    pass(std::integral_constant<int, 8>{}, 8);
-    pass(std::integral_constant<int, 9>{}, 16);
+    // 9 + 9 + 8 bits: the low width is <= 24 (32-bit keys minus the MSD pass's 8); keys of
+    // <= 26 bits (low width <= 18) sort in two passes
+    pass(std::integral_constant<int, 9>{}, 0);
+    pass(std::integral_constant<int, 9>{}, 9);
+    pass(std::integral_constant<int, 8>{}, 18);
 }
 
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
