@@ -60,6 +60,10 @@ ALG_BYTES = {
     "count_tiny": 21,
     "count32": 21, "big_count": 21, "edge_union": 0, "quarter_root": 0, "final": 13,
     "label_sorted": 13, "permute_out": 13,
+    # bucketed sort (fits of >= 2^23 points): the MSD pass reads key + x,y and
+    # writes key, the 32-B place record and pos; an LSD pass reads and writes key + place;
+    # the gather reads place + record and writes perm + sorted x,y
+    "bucket_msd": 60, "bucket_lsd": 16, "gather_bucket": 56,
 }
 # The clique-grid count kernels each process one class of tiles: their per-launch algorithmic
 # bytes count that class's points only (dbscan_last_stats [11..13]).
@@ -470,6 +474,11 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "points/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "value_basis": ("device-resident: coordinates already in HBM when the timed region "
+                            "starts, labels left in HBM (the bench contract); the PCIe-inclusive "
+                            "host-array rate is end_to_end, and vs_baseline stays null because "
+                            "BASELINE.md holds no published number (GPU/CPU ratio: "
+                            "cpu_baseline.gpu_over_cpu)"),
             "data": "synthetic (device generator G(n, noise, dense, seed), SURVEY §8d)",
             "config": {
                 "workload": workload + f", eps={args.eps}, minPoints={args.min_points}, "

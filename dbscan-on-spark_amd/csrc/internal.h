@@ -156,7 +156,7 @@ struct ScanState {
 // record there, pos[i] the padded place of input i; np padded places.
 // DBSCAN_AB_BUCKET_LOG2: A/B builds only (tools/build_ab.sh), never the shipped library
 #ifndef DBSCAN_AB_BUCKET_LOG2
-#define DBSCAN_AB_BUCKET_LOG2 24
+#define DBSCAN_AB_BUCKET_LOG2 23
 #endif
 constexpr int64_t kBucketMinPoints = int64_t(1) << DBSCAN_AB_BUCKET_LOG2;
 struct BucketSort {

@@ -55,7 +55,22 @@ constexpr int kSmPer = kSmN / kSmT;         // points per thread in the load pha
 constexpr int kSmCells = 8192;              // dense cell table entries
 constexpr int kSmCellPer = kSmCells / kSmT;
 constexpr uint32_t kNoCell = 0xFFFFu;
+constexpr uint32_t kCellMask = 0x1FFFu;  // info: visit << 16 | quadrant << 13 | cell
 static_assert(kSmN % kSmT == 0 && kSmCells % kSmT == 0, "whole rounds per thread");
+
+// DBSCAN_AB_STAMPS (timing builds only, never the shipped library): thread 0 of workgroup 0
+// records the 100 MHz clock at the phase boundaries (dbscan_ab_small_stamps).
+#if DBSCAN_AB_STAMPS
+__device__ long long g_sm_stamps[16];
+#define SM_STAMP(k)                                                               \
+    do {                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_sm_stamps[(k)] = wall_clock64(); \
+    } while (0)
+#else
+#define SM_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
 static_assert(kSmN <= 65536 && kSmCells < 65535, "16-bit visit indices, cells and cell starts");
 
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77 (no FMA: -ffp-contract=off and
@@ -80,6 +95,7 @@ struct SmGrid {
     double cx2, cy2, invs;            // record = fl32((v*0.5 - c*0.5) * invs)
     float lo, hi;                     // F <= lo: neighbour; F > hi: not; else exact fp64
     int nx, ny, ncells, nf, exact_only, bad;
+    int clique;  // the side was not grown and <= |eps|*(1+2^-14): quarter cells are cliques
 };
 
 // Workgroup exclusive scan of one int per thread; *total = the sum.  ws: kSmW + 1 ints.
@@ -159,6 +175,7 @@ __device__ void sm_make_grid(double xmin, double xmax, double ymin, double ymax,
     g->bad = 0;
     g->exact_only = 0;
     g->nx = g->ny = g->ncells = 1;
+    g->clique = 0;
     if (nf == 0) return;
     double R = fabs(eps) * (1.0 + 0x1p-40);
     if (R < 0x1p-500) R = 0x1p-500;
@@ -184,6 +201,7 @@ __device__ void sm_make_grid(double xmin, double xmax, double ymin, double ymax,
     }
     g->nx = (int)cx;
     g->ny = (int)cy;
+    g->clique = (hx == h0 && hy == h0 && h0 <= fabs(eps) * (1.0 + 0x1p-14)) ? 1 : 0;
     g->ncells = g->nx * g->ny;
     g->xmin2 = xmin * 0.5;
     g->ymin2 = ymin * 0.5;
@@ -238,6 +256,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     const int m = (int)m64;  // the host routes only m <= kSmN here
     const double* px = x + off;
     const double* py = y + off;
+    SM_STAMP(0);
 
     // ---- load + bbox ----
     double vx[kSmPer], vy[kSmPer];
@@ -290,6 +309,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         }
         __syncthreads();
     }
+    SM_STAMP(1);
     const int nf = G.nf;
     const int nx = G.nx, ny = G.ny, ncells = G.ncells;
     if (G.bad) {  // (unreachable for finite bboxes: 4096 doublings span every double extent)
@@ -306,12 +326,14 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         const int i = tid + k * kSmT;
         mycell[k] = -1;
         if (i < m && isfinite(vx[k]) && isfinite(vy[k])) {
-            int cx = (int)floor((vx[k] * 0.5 - G.xmin2) * G.invx);
-            int cy = (int)floor((vy[k] * 0.5 - G.ymin2) * G.invy);
-            cx = min(max(cx, 0), nx - 1);
-            cy = min(max(cy, 0), ny - 1);
-            mycell[k] = cy * nx + cx;
-            atomicAdd(&par[mycell[k]], 1);
+            // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
+            int qx = (int)floor(2.0 * ((vx[k] * 0.5 - G.xmin2) * G.invx));
+            int qy = (int)floor(2.0 * ((vy[k] * 0.5 - G.ymin2) * G.invy));
+            qx = min(max(qx, 0), 2 * nx - 1);
+            qy = min(max(qy, 0), 2 * ny - 1);
+            const int c = (qy >> 1) * nx + (qx >> 1);
+            mycell[k] = c | (((qy & 1) << 1 | (qx & 1)) << 13);
+            atomicAdd(&par[c], 1);
         }
     }
     __syncthreads();
@@ -344,7 +366,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         const int i = tid + k * kSmT;
         if (i >= m) continue;
         if (mycell[k] >= 0) {
-            const int s = atomicAdd(&par[mycell[k]], 1);
+            const int s = atomicAdd(&par[mycell[k] & kCellMask], 1);
             rec[s] = make_float2((float)((vx[k] * 0.5 - G.cx2) * G.invs),
                                  (float)((vy[k] * 0.5 - G.cy2) * G.invs));
             info[s] = ((uint32_t)i << 16) | (uint32_t)mycell[k];
@@ -355,6 +377,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     }
     __syncthreads();
 
+    SM_STAMP(2);
     // ---- stencil walk helpers ----
     const float lo = G.lo, hi = G.hi;
     const bool exact_only = G.exact_only != 0;
@@ -371,7 +394,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // f(q) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own row first);
     // f returns false to stop
     auto for_stencil = [&](int p, int qmin, auto&& f) {
-        const int c = (int)(info[p] & 0xFFFFu);
+        const int c = (int)(info[p] & kCellMask);
         const int cy = c / nx, cx = c - cy * nx;
         const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
 #pragma unroll
@@ -402,17 +425,40 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         ncore_local += c ? 1 : 0;
     }
     __syncthreads();
+    SM_STAMP(3);
 
-    // ---- union over core-core pairs (each unordered pair once: q > p) ----
+    // ---- union over core-core pairs (each unordered pair from its smaller slot: q > p) ----
+    // Clique grids: every core p unites with the FIRST core q > p of each quarter cell (side
+    // ~eps/2, a clique) of its stencil within eps, and no other of that quarter.  Enough: the
+    // cores of one quarter are chained (each to the next core of its quarter), and a pair p < q
+    // within eps makes p unite with some core of q's quarter.  So a dense cell costs a few
+    // unions per point instead of one per neighbour.
+    const bool quarters = G.clique != 0;
     for (int p = tid; p < nf; p += kSmT) {
         if (!core[p]) continue;
         const float2 me = rec[p];
+        const uint32_t ip = info[p];
+        const int pc = (int)(ip & kCellMask), pcy = pc / nx, pcx = pc - pcy * nx;
+        uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
         for_stencil(p, p + 1, [&](int q) {
-            if (core[q] && pair(p, me, q)) sm_unite(par, info, p, q);
+            if (!core[q]) return true;
+            int bit = 0;
+            if (quarters) {
+                const uint32_t iq = info[q];
+                const int qc = (int)(iq & kCellMask), qcy = qc / nx, qcx = qc - qcy * nx;
+                const int qd = (int)((iq >> 13) & 3u);
+                bit = (2 * (qcy - pcy + 1) + (qd >> 1)) * 6 + 2 * (qcx - pcx + 1) + (qd & 1);
+                if ((done >> bit) & 1ull) return true;
+            }
+            if (pair(p, me, q)) {
+                sm_unite(par, info, p, q);
+                if (quarters) done |= 1ull << bit;
+            }
             return true;
         });
     }
     __syncthreads();
+    SM_STAMP(4);
 
     // ---- roots: s(K) flagged by visit index; then every core points at its root ----
     // (read-only walks first, writes after a barrier: a path-halving find racing with the
@@ -443,6 +489,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         if (tid < kSmN / 32) wrank[tid] = r;
     }
     __syncthreads();
+    SM_STAMP(5);
     auto cluster_of = [&](uint32_t s) -> int {  // 1 + roots with a smaller visit index
         return wrank[s >> 5] + __popc(rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
     };
@@ -476,6 +523,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         fl_out[v] = f;
     }
 
+    SM_STAMP(6);
     // ---- counts and statistics ----
     {
         int tot = 0;
@@ -502,6 +550,13 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
 }
 
 }  // namespace
+
+#if DBSCAN_AB_STAMPS
+extern "C" int dbscan_ab_small_stamps(long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), 16 * sizeof(long long)) == hipSuccess
+               ? 0 : -1;
+}
+#endif
 
 bool small_fit_eligible(int64_t n, double eps, int32_t mode) {
     const double eps2 = eps * eps;

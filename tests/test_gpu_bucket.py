@@ -2,8 +2,8 @@
 8 key bits into padded per-band segments, then LSD passes inside the segments), bit-exact
 against the CPU oracle.
 
-Fits of >= 2^24 points take this path (kBucketMinPoints); the BASELINE configs 4 and 5 (its
-per-GPU share) run through it in tests/test_gpu_configs.py.  Here: sizes just over the threshold
+Fits of >= 2^23 points take this path (kBucketMinPoints); the BASELINE configs 2-5 (per-GPU
+shares) run through it in tests/test_gpu_configs.py.  Here: sizes just over the threshold
 with non-finite points (sentinel keys, which share the last band with real keys), both
 LocalDBSCANNaive and LocalDBSCANArchery rules, archery's float32 box (its own output kernels),
 an input with no finite point (no key bits: the MSD pass alone sorts), and idempotence."""
@@ -15,7 +15,7 @@ from conftest import gen_blobs
 
 pytestmark = pytest.mark.gpu
 
-N = (1 << 24) + 4099
+N = (1 << 23) + 4099
 
 
 @pytest.fixture(scope="module")
