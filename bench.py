@@ -514,8 +514,10 @@ def seam(args, h, threads):
     partition of <= maxPointsPerPartition points + eps halo).
       per_call   one fit of m points per call, m in 250 / 2k / 8k / 64k: dbscan_fit_h (host
                  arrays, PCIe included) and dbscan_fit_device (device-resident, synchronous),
-                 median of repeated calls; m <= 8192 runs the one-workgroup kernel (small.hip),
-                 'tiled' is the same call through the tiled pipeline (dbscan_set_small_max 0)
+                 median of repeated calls; the plain columns force the one-workgroup kernel
+                 (small.hip) up to 8192 points, 'tiled' is the same call through the tiled
+                 pipeline (dbscan_set_small_max 0); a handle's default routes single fits of
+                 <= DBSCAN_SMALL_DEFAULT_POINTS (3072) points to the one-workgroup kernel
       train      G(10^7) (config 2) cut by the reference's EvenSplitPartitioner with
                  maxPointsPerPartition 8192 and duplicated into eps-grown partitions
                  (DBSCAN.scala:105-137): every partition fitted (a) by one dbscan_fit_h call each
@@ -532,6 +534,7 @@ def seam(args, h, threads):
 
     out = {"per_call": {}}
     eps, mp = args.eps, args.min_points
+    default_small = h.set_small_max(8192)  # (restored below: the handle's default cap)
     for m in (250, 2000, 8192, 65536):
         tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
         hx, hy = tx.cpu().numpy(), ty.cpu().numpy()
@@ -557,7 +560,7 @@ def seam(args, h, threads):
                     if i >= 2:
                         ts.append(time.perf_counter() - t0)
                 row[f"{tag}{kind}_us"] = round(float(np.median(ts)) * 1e6, 1)
-        h.set_small_max(8192)
+        h.set_small_max(default_small)
         out["per_call"][str(m)] = row
 
     n = 10_000_000

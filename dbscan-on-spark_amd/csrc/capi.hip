@@ -184,7 +184,7 @@ struct dbscan_handle {
     void* bpinned = nullptr;          // pinned staging of the batch tables (grow-only)
     size_t bpinned_bytes = 0;
     hipEvent_t bcopied = nullptr;     // the last batch tables' upload (pinned buffer reusable)
-    int64_t small_max = dbscan::kSmallMaxPoints;  // one-workgroup fits up to this many points
+    int64_t small_max = DBSCAN_SMALL_DEFAULT_POINTS;  // one-workgroup fits up to this many points
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)

@@ -242,17 +242,35 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
 // Bucketed sort (large fits): perm and the sorted coordinates from the padded places, in slot
 // order: one 32-B record (x, y, input index) read per slot from inside its band's segment
 // (cache-resident while the launch sweeps the bands in order), coalesced writes.
+// Slab fits: zs[p] = the slot's zone (from the record), and for the listed shared points
+// sinv[i] = their slot (a scattered write per shared point only).
 __global__ __launch_bounds__(kBlock) void gather_bucket_kernel(int64_t n,
                                                                const int32_t* __restrict__ place,
                                                                const double4* __restrict__ rec,
                                                                const int32_t* __restrict__ nf_p,
                                                                int32_t* __restrict__ perm,
-                                                               double2* __restrict__ xy) {
+                                                               double2* __restrict__ xy,
+                                                               uint8_t* __restrict__ zs,
+                                                               int32_t* __restrict__ sinv) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const double4 r = rec[place[p]];
-    perm[p] = (int32_t)__double_as_longlong(r.z);
+    const int32_t i = (int32_t)__double_as_longlong(r.z);
+    perm[p] = i;
     if (p < *nf_p) xy[p] = make_double2(r.x, r.y);
+    if (zs) {
+        const uint32_t z = (uint32_t)__double_as_longlong(r.w);
+        zs[p] = (uint8_t)(z & 255u);
+        if (sinv && (z >> 8)) sinv[i] = (int32_t)p;
+    }
+}
+
+// Lean slab fits with the bucketed sort: the listed shared points flagged in slab order.
+__global__ __launch_bounds__(kBlock) void shared_mark_kernel(int64_t m,
+                                                             const int64_t* __restrict__ idx,
+                                                             uint8_t* __restrict__ shm) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < m) shm[idx[k]] = 1;
 }
 
 // Slab fits: the zone-2 points (count candidates, never core) marked in sorted order (zs,
@@ -2303,6 +2321,14 @@ __global__ __launch_bounds__(kBlock) void zone_fix_kernel(int64_t n,
     if (i < n && zone[i] == 2) core[inv[i]] = 0;
 }
 
+// The same from the zones in sorted order (bucketed sort: zs holds every slot's zone).
+__global__ __launch_bounds__(kBlock) void zone_fix_sorted_kernel(int64_t n,
+                                                                 const uint8_t* __restrict__ zs,
+                                                                 uint8_t* __restrict__ core) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p < n && zs[p] == 2) core[p] = 0;
+}
+
 // Slots outside the grid (non-finite coordinates, or every slot when eps*eps is NaN): no
 // neighbours, not even themselves.
 __global__ __launch_bounds__(kBlock) void count_rest_kernel(const int32_t* __restrict__ nf_p,
@@ -3176,9 +3202,10 @@ __global__ __launch_bounds__(kBlock) void slab_map_kernel(int64_t n,
 __global__ __launch_bounds__(kBlock) void slab_pack_kernel(int64_t n,
                                                            const uint8_t* __restrict__ core,
                                                            const int32_t* __restrict__ lab,
-                                                           int32_t* __restrict__ packed) {
+                                                           int32_t* __restrict__ packed,
+                                                           const int32_t* __restrict__ place) {
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p < n) packed[p] = core[p] ? lab[p] : -1;
+    if (p < n) packed[place ? place[p] : p] = core[p] ? lab[p] : -1;
 }
 
 __global__ __launch_bounds__(kBlock) void slab_roots_kernel(int64_t n,
@@ -3492,7 +3519,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
 
     // large direct fits sort through the padded bands (bucket_sort: cache-resident random writes)
-    const bool bucketed = !a.zone && !a.batch && mode == kGridEps && n >= kBucketMinPoints &&
+    const bool bucketed = !a.batch && mode == kGridEps && n >= kBucketMinPoints &&
                           n + 256 * 2048 < (int64_t)INT32_MAX;
     uint32_t* key = static_cast<uint32_t*>(ws.key.ensure(n * sizeof(uint32_t)));
     uint32_t* key2 = static_cast<uint32_t*>(ws.key2.ensure(n * sizeof(uint32_t)));
@@ -3516,7 +3543,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         if (bucketed) {  // large fits: MSD band split, then LSD inside the bands
-            bucket_sort(s, a.x, a.y, key, n, &st[kStBits], ws.bucket, ws.hist, ws.scan, prof);
+            uint8_t* shm = nullptr;  // lean slab fits: the listed shared points, in slab order
+            if (a.zone && a.shared_idx && a.n_shared > 0) {
+                shm = static_cast<uint8_t*>(ws.shm.ensure(n));
+                DBSCAN_HIP_CHECK(hipMemsetAsync(shm, 0, n, s));
+                klaunch(prof, "shared_mark", shared_mark_kernel, dim3(nblk(a.n_shared)),
+                        dim3(kBlock), 0, s, a.n_shared, a.shared_idx, shm);
+            }
+            bucket_sort(s, a.x, a.y, key, n, &st[kStBits], ws.bucket, ws.hist, ws.scan, prof,
+                        a.zone, shm);
             key = ws.bucket.key_fin;  // (perm: written by scatter_bucket_kernel below)
         } else {
             uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));
@@ -3567,7 +3602,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     const bool box = a.mode == kModeArcheryBox;
     const bool fuse = !box && mode == kGridEps && fuse_union() && count_cap() == 0 &&
                       (!a.zone || f32_count());
-    uint8_t* zs = (a.zone && fuse) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
+    uint8_t* zs =
+        (a.zone && (fuse || bucketed)) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
     // clique grids: the fp32-record count kernels by tile class (tile_class_kernel);
     // DBSCAN_F32=0 keeps the fp64 count_tile_kernel for A/B measurements
     const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
@@ -3598,14 +3634,14 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         if (mode != kGridEps)  // (eps grids: the radix sort's final pass wrote inv)
             klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
                     inv);
-        if (bucketed)
+        if (bucketed)  // (slab fits: zs from the records, inv only for the shared points)
             klaunch(prof, "gather_bucket", gather_bucket_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
                     n, (const int32_t*)ws.bucket.slot_place, (const double4*)ws.bucket.rec, nf_p,
-                    perm, xy);
+                    perm, xy, zs, (a.zone && a.shared_idx) ? inv : (int32_t*)nullptr);
         else if (mode != kGridNoPairs)
             klaunch(prof, "scatter_xy", scatter_xy_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n,
                                nf_p, inv, xy);
-        if (zs) {
+        if (zs && !bucketed) {
             DBSCAN_HIP_CHECK(hipMemsetAsync(zs, 0, n, s));
             klaunch(prof, "zone_mark", zone_mark_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
                     a.zone, inv, zs);
@@ -3760,7 +3796,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = nmain + rest_grid;
         exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan);
-        if (a.zone)  // (the core count above then includes zone-2 points: a statistic only)
+        if (a.zone && bucketed)  // (the core count above then includes zone-2 points: a statistic)
+            klaunch(prof, "zone_fix", zone_fix_sorted_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
+                    n, (const uint8_t*)zs, core);
+        else if (a.zone)
             klaunch(prof, "zone_fix", zone_fix_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, a.zone, inv,
                                core);
     }
@@ -3896,12 +3935,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                     klaunch(prof, "slab_shared", slab_shared_kernel, dim3(nblk(a.n_shared)),
                             dim3(kBlock), 0, s, a.n_shared, a.shared_idx, inv, core, lab,
                             a.core_out, a.root_out);
-            } else {
-                int32_t* packed = static_cast<int32_t*>(ws.packed.ensure(n * sizeof(int32_t)));
+            } else {  // (bucketed sort: packed at the slots' places, read back through pos)
+                int32_t* packed = static_cast<int32_t*>(
+                    ws.packed.ensure((bucketed ? ws.bucket.np : n) * sizeof(int32_t)));
                 klaunch(prof, "slab_pack", slab_pack_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n,
-                        core, lab, packed);
+                        core, lab, packed,
+                        bucketed ? (const int32_t*)ws.bucket.slot_place : nullptr);
                 klaunch(prof, "slab_roots", slab_roots_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
-                        n, inv, packed, a.core_out, a.root_out);
+                        n, bucketed ? (const int32_t*)ws.bucket.pos : (const int32_t*)inv,
+                        (const int32_t*)packed, a.core_out, a.root_out);
             }
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
@@ -3911,6 +3953,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         slab->nlroots = -1;
         slab->n = n;
         slab->eps2 = eps2;
+        slab->to_packed = bucketed ? ws.bucket.pos : inv;
+        slab->place = bucketed ? ws.bucket.slot_place : nullptr;
+        slab->npacked = bucketed ? ws.bucket.np : n;
         slab->nbr = nbr;
         slab->nbr_k = nbr_k;
     }
@@ -3988,7 +4033,7 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
     int32_t* label_of_root = static_cast<int32_t*>(ws.slab_lor.ensure(st.n * sizeof(int32_t)));
     klaunch(prof, "slab_root_labels", slab_root_labels_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n, perm,
                        core, lab, gs_of_root, all_roots, n_roots, label_of_root);
-    uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
+    uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.npacked * sizeof(uint32_t)));
     klaunch(prof, "label_sorted", label_sorted_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s,
                        static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
                        static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
@@ -3996,9 +4041,9 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                            kStNf,
                        st.n, st.eps2, mode, perm, core, lab, (const uint64_t*)nullptr,
                        (const int32_t*)nullptr, zone, gid,
-                       gs_of_root, label_of_root, packed, (const int32_t*)nullptr);
+                       gs_of_root, label_of_root, packed, st.place);
     klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-                       static_cast<const int32_t*>(ws.inv.p), packed, zone, cluster, flag);
+                       st.to_packed, packed, zone, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
@@ -4008,7 +4053,7 @@ void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
     if (!st.valid) throw ArgError{"dbscan_slab_roots_prepare_device: no slab fit on this handle"};
     if (st.n == 0) return;
     StageTimer t(prof, s, "slab_label");
-    uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.n * sizeof(uint32_t)));
+    uint32_t* packed = static_cast<uint32_t*>(ws.packed.ensure(st.npacked * sizeof(uint32_t)));
     klaunch(prof, "label_sorted", label_sorted_kernel<true, true>, dim3(nblk(st.n)), dim3(kBlock), 0,
             s, static_cast<const double2*>(ws.xy.p), static_cast<const int32_t*>(ws.cell.p),
             static_cast<const Seg*>(ws.seg.p), st.nbr, st.nbr_k,
@@ -4016,10 +4061,10 @@ void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
             st.eps2, mode, static_cast<const int32_t*>(ws.perm_sorted),
             static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
             (const uint64_t*)nullptr, (const int32_t*)nullptr, zone, gid, gs_of_root,
-            (const int32_t*)nullptr, packed, (const int32_t*)nullptr);
+            (const int32_t*)nullptr, packed, st.place);
     uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
     klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-            static_cast<const int32_t*>(ws.inv.p), packed, zone, spacked);
+            st.to_packed, packed, zone, spacked);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 

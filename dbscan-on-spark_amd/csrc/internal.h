@@ -175,7 +175,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab;
+        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm;
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
@@ -190,7 +190,7 @@ struct Workspace {
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
-                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab})
+                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm})
             b->release();
     }
 };
@@ -265,6 +265,11 @@ struct SlabState {
     const int32_t* nbr = nullptr;  // non-core neighbour lists (nullptr: label by stencil scan)
     int nbr_k = 0;
     int64_t nlroots = -1;  // local roots listed in ws.lroots by the last prepare (-1: none)
+    // where a point's packed label lives: packed[to_packed[i]] for slab index i, written at
+    // place[slot] (bucketed sort: pos / slot_place) or at the slot (plain sort: inv / none)
+    const int32_t* to_packed = nullptr;
+    const int32_t* place = nullptr;
+    int64_t npacked = 0;  // entries of the packed array
 };
 
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
@@ -392,9 +397,11 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
                       int32_t* inv = nullptr, bool iota = false);
 
 int64_t bucket_padded(int64_t n);
+// zone (slab fits): each point's zone rides in its record (gather_bucket writes zs from it);
+// shm (lean slab fits): the listed shared points, whose slots gather_bucket writes by input index
 void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
                  const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
-                 Profiler* prof);
+                 Profiler* prof, const uint8_t* zone = nullptr, const uint8_t* shm = nullptr);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

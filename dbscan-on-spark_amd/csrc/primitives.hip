@@ -622,8 +622,10 @@ __global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __r
 struct BucketExtra {
     const double* x;
     const double* y;
-    double4* rec_out;  // MODE 1: (x, y, input index bits, 0) per padded place
+    double4* rec_out;  // MODE 1: (x, y, input index bits, zone | shared << 8) per padded place
     int32_t* pos;
+    const uint8_t* zone;  // MODE 1, slab fits: zone per input point (else nullptr)
+    const uint8_t* shm;   // MODE 1, lean slab fits: 1 for the listed shared points (or nullptr)
     const int32_t* pshift;
     const int2* tseg;
 };
@@ -669,6 +671,7 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
     int32_t v_r[kRItems];
     uint32_t dr[kRItems];
     double2 c_r[MODE == 1 ? kRItems : 1];
+    uint32_t z_r[MODE == 1 ? kRItems : 1];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
 #pragma unroll
@@ -678,7 +681,12 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
         const uint32_t k = valid ? key[i] : kSentinelKey;
         const int32_t v = valid ? (val ? val[i] : (int32_t)i) : 0;
         if constexpr (MODE == 1)
+        {
             c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
+            z_r[r] = (valid && ex.zone) ? (uint32_t)ex.zone[i] |
+                                              ((ex.shm && ex.shm[i]) ? 256u : 0u)
+                                        : 0u;
+        }
         const uint32_t d = (k >> shift) & (RB - 1u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -747,7 +755,8 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
             if constexpr (MODE == 1) {  // the record and the place straight from registers
                 const int64_t g = (int64_t)sm.gofs[d] + within;
                 ex.rec_out[g] = make_double4(c_r[r].x, c_r[r].y,
-                                             __longlong_as_double((long long)v_r[r]), 0.0);
+                                             __longlong_as_double((long long)v_r[r]),
+                                             __longlong_as_double((long long)z_r[r]));
                 ex.pos[v_r[r]] = (int32_t)g;
             }
         }
@@ -973,7 +982,7 @@ int64_t bucket_padded(int64_t n) { return ((n + kRTile - 1) / kRTile + 256) * kR
 
 void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
                  const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
-                 Profiler* prof) {
+                 Profiler* prof, const uint8_t* zone, const uint8_t* shm) {
     if (n <= 0) return;
     const int64_t np = bucket_padded(n), ntp = np / kRTile, nb = (n + kRTile - 1) / kRTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * ntp * 512 * sizeof(int32_t)));
@@ -1005,7 +1014,7 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                 (const int32_t*)ho, n, np, bits_dev, seg, pshift);
         klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(257), dim3(kBlock), 0, s,
                 (const int32_t*)seg, np, ka);
-        const BucketExtra ex{x, y, b.rec, b.pos, pshift, nullptr};
+        const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr};
         klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
                 dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, (int32_t*)nullptr,
                 (uint32_t*)nullptr,
@@ -1021,7 +1030,7 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     const int32_t* vin = nullptr;  // the first pass generates the identity
     uint32_t* kout = kb;
     int32_t* vout = jb;
-    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, tseg};
+    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tseg};
     const auto pass = [&](auto wtag, int shift) {
         constexpr int W = decltype(wtag)::value;
         StageTimer st(prof, s, "sort_bucket");

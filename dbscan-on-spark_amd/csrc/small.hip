@@ -381,18 +381,22 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // ---- stencil walk helpers ----
     const float lo = G.lo, hi = G.hi;
     const bool exact_only = G.exact_only != 0;
-    // neighbour test of slots p (record me) and q
-    auto pair = [&](int p, float2 me, int q) -> bool {
+    // neighbour test of slots p (record me) and q (record rq)
+    auto pair = [&](int p, float2 me, int q, float2 rq) -> bool {
         if (!exact_only) {
-            const float F = sm_d2(me, rec[q]);
+            const float F = sm_d2(me, rq);
             if (F <= lo) return true;
             if (F > hi) return false;
         }
         const int vp = (int)(info[p] >> 16), vq = (int)(info[q] >> 16);
         return sm_within(px[vp], py[vp], px[vq], py[vq], eps2);
     };
-    // f(q) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own row first);
-    // f returns false to stop
+    // f(q, rec[q], w) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own
+    // row first), w = the 6x6 quarter-window position of q's cell: (row 0..2) * 3 + col 0..2
+    // (rows cy-1, cy, cy+1 -> 0, 1, 2); f returns false to stop.  The candidates' records are
+    // loaded kSmBatch at a time (their LDS reads in flight together: the walks are bound by
+    // the latency of dependent LDS reads, not by their count).
+    constexpr int kSmBatch = 4;
     auto for_stencil = [&](int p, int qmin, auto&& f) {
         const int c = (int)(info[p] & kCellMask);
         const int cy = c / nx, cx = c - cy * nx;
@@ -401,9 +405,24 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         for (int d = 0; d < 3; ++d) {
             const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
             if (r < 0 || r >= ny) continue;
-            const int e = cst[r * nx + x1 + 1];
-            for (int q = max((int)cst[r * nx + x0], qmin); q < e; ++q)
-                if (!f(q)) return;
+            const int rb = r * nx;
+            const int e = cst[rb + x1 + 1];
+            // boundaries of the row's second and third cell (q's column = x0 + crossings)
+            const int b1 = x0 + 1 <= x1 ? (int)cst[rb + x0 + 1] : 0x7FFFFFFF;
+            const int b2 = x0 + 2 <= x1 ? (int)cst[rb + x0 + 2] : 0x7FFFFFFF;
+            const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
+            for (int q = max((int)cst[rb + x0], qmin); q < e; q += kSmBatch) {
+                float2 rq[kSmBatch];
+#pragma unroll
+                for (int u = 0; u < kSmBatch; ++u) rq[u] = rec[min(q + u, e - 1)];
+#pragma unroll
+                for (int u = 0; u < kSmBatch; ++u) {
+                    const int qq = q + u;
+                    if (qq < e &&
+                        !f(qq, rq[u], wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0)))
+                        return;
+                }
+            }
         }
     };
 
@@ -414,8 +433,8 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         if (!c && p < nf) {
             const float2 me = rec[p];
             int cnt = 0;
-            for_stencil(p, 0, [&](int q) {
-                cnt += pair(p, me, q) ? 1 : 0;
+            for_stencil(p, 0, [&](int q, float2 rq, int) {
+                cnt += pair(p, me, q, rq) ? 1 : 0;
                 return cnt < min_points;
             });
             c = cnt >= min_points;
@@ -437,21 +456,26 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     for (int p = tid; p < nf; p += kSmT) {
         if (!core[p]) continue;
         const float2 me = rec[p];
-        const uint32_t ip = info[p];
-        const int pc = (int)(ip & kCellMask), pcy = pc / nx, pcx = pc - pcy * nx;
         uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
-        for_stencil(p, p + 1, [&](int q) {
-            if (!core[q]) return true;
+        // a root of p's set (possibly stale: it stays an ancestor of p, so a q whose parent it
+        // is belongs to p's set already and needs neither a pair test nor a union)
+        int rp = sm_find(par, p);
+        for_stencil(p, p + 1, [&](int q, float2 rq, int w) {
+            const uint32_t iq = info[q];
+            const bool cq = core[q] != 0;
             int bit = 0;
             if (quarters) {
-                const uint32_t iq = info[q];
-                const int qc = (int)(iq & kCellMask), qcy = qc / nx, qcx = qc - qcy * nx;
                 const int qd = (int)((iq >> 13) & 3u);
-                bit = (2 * (qcy - pcy + 1) + (qd >> 1)) * 6 + 2 * (qcx - pcx + 1) + (qd & 1);
-                if ((done >> bit) & 1ull) return true;
+                bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
             }
-            if (pair(p, me, q)) {
+            if (!cq || ((done >> bit) & 1ull)) return true;
+            if (par[q] == rp) {
+                if (quarters) done |= 1ull << bit;
+                return true;
+            }
+            if (pair(p, me, q, rq)) {
                 sm_unite(par, info, p, q);
+                rp = sm_find(par, p);
                 if (quarters) done |= 1ull << bit;
             }
             return true;
@@ -507,10 +531,10 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         } else if (p < nf) {
             const float2 me = rec[p];
             uint32_t best = 0xFFFFFFFFu;
-            for_stencil(p, 0, [&](int q) {
+            for_stencil(p, 0, [&](int q, float2 rq, int) {
                 if (core[q]) {
                     const uint32_t s = info[par[q]] >> 16;
-                    if (s < best && pair(p, me, q)) best = s;
+                    if (s < best && pair(p, me, q, rq)) best = s;
                 }
                 return true;
             });

@@ -188,13 +188,16 @@ int64_t dbscan_scala_range_count(double start, double end, double step, int32_t 
  * Partition-sized fits: the seam's real call pattern.  DBSCAN.scala:150-155 runs one
  * LocalDBSCANNaive(eps, minPoints).fit per spatial partition -- at most maxPointsPerPartition
  * points (EvenSplitPartitioner.scala:44-209) plus the eps halo (DBSCAN.scala:116-137).
- * Full fits of at most dbscan_set_small_max(h, ...) points (default and ceiling
- * DBSCAN_SMALL_MAX_POINTS) with a finite eps*eps in mode NAIVE or ARCHERY run ONE kernel in
+ * Full fits of at most dbscan_set_small_max(h, ...) points (default
+ * DBSCAN_SMALL_DEFAULT_POINTS, where the one-workgroup kernel stops beating the tiled pipeline
+ * on a single call; ceiling DBSCAN_SMALL_MAX_POINTS) with a finite eps*eps in mode NAIVE or
+ * ARCHERY run ONE kernel in
  * which one workgroup holds the whole partition in LDS (same results bit for bit as the tiled
  * pipeline; dbscan_fit / dbscan_fit_h / dbscan_fit_device / dbscan_fit_device_async all route
  * there).  dbscan_set_small_max returns the previous value (0 sends every fit through the tiled
  * pipeline). */
 #define DBSCAN_SMALL_MAX_POINTS 8192
+#define DBSCAN_SMALL_DEFAULT_POINTS 3072
 int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is

@@ -44,6 +44,23 @@ def test_gpu_node_world8_config3_shape(tmp_path, chunks):
     assert ks == {rk}
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_gpu_node_bucketed_slabs(tmp_path, chunks):
+    """Slabs of >= 2^23 points take the bucketed sort (zones and the shared points' slots ride
+    in the place records, labels at the places): 2 ranks over 1.8*10^7 points of config 3's
+    shape, the global-input and host-chunk forms, bit-exact against one oracle fit."""
+    n = 18_000_000
+    x, y = gen_blobs(n, noise=0.2, seed=3)
+    cl, fl, seen, ks, parts = run_ranks(tmp_path, x, y, 2, 2.55, 10, 0, use_gpu=True,
+                                        timeout=800, chunks=chunks)
+    assert np.all(seen == 1)
+    rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
+    np.testing.assert_array_equal(fl, rf)
+    np.testing.assert_array_equal(cl, rc)
+    assert ks == {rk}
+
+
 @pytest.mark.parametrize("world,mode", [(2, 0), (3, 1)])
 def test_gpu_node_chunks_equals_single_fit(tmp_path, world, mode):
     """Host-to-slab path with the HIP slab kernels: each rank starts from its chunk of the input,
