@@ -2857,7 +2857,7 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     } else if (p < nf) {
         const int32_t o = perm[p];
         if (SLAB && zone[o] != 0) {
-            packed[p] = 0;
+            packed[place ? place[p] : p] = 0;
             return;  // zone 2 has no neighbour list; zones 1/2 are not labelled here
         }
         int64_t m = 0x7FFFFFFFFFFFFFFFll;
