@@ -244,6 +244,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     __shared__ int wsc[kSmW + 1];
     __shared__ int nonfin;
     __shared__ SmGrid G;
+    __shared__ uint32_t sbest[kSmT / 3 + 1];  // row-split labels: min root per point
 
     const int tid = threadIdx.x;
     int64_t off = 0, m64 = single_n;
@@ -397,12 +398,14 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // loaded kSmBatch at a time (their LDS reads in flight together: the walks are bound by
     // the latency of dependent LDS reads, not by their count).
     constexpr int kSmBatch = 4;
-    auto for_stencil = [&](int p, int qmin, auto&& f) {
+    // only = 0..2: that row alone (row-split fits), -1: all three
+    auto for_stencil = [&](int p, int qmin, auto&& f, int only = -1) {
         const int c = (int)(info[p] & kCellMask);
         const int cy = c / nx, cx = c - cy * nx;
         const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
+            if (only >= 0 && d != only) continue;
             const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
             if (r < 0 || r >= ny) continue;
             const int rb = r * nx;
@@ -426,22 +429,51 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         }
     };
 
+    // Row split (partitions of <= kSmT / 3 points, where most threads would idle): each point's
+    // three stencil rows are walked by three threads, counts summed and label minima taken in
+    // LDS -- a third of the dependent chain per thread.
+    const bool split = 3 * m <= kSmT;
+
     // ---- count: core <=> |N(p)| >= minPoints (LocalDBSCANNaive.scala:52-56,99-101) ----
     int ncore_local = 0;
-    for (int p = tid; p < m; p += kSmT) {
-        bool c = min_points <= 0;
-        if (!c && p < nf) {
-            const float2 me = rec[p];
-            int cnt = 0;
-            for_stencil(p, 0, [&](int q, float2 rq, int) {
-                cnt += pair(p, me, q, rq) ? 1 : 0;
-                return cnt < min_points;
-            });
-            c = cnt >= min_points;
+    if (split) {
+        if (tid < m) par[tid] = 0;  // (per-point counters until the union needs par)
+        __syncthreads();
+        if (tid < 3 * m && min_points > 0) {
+            const int p = tid / 3, d = tid - 3 * (tid / 3);
+            if (p < nf) {
+                const float2 me = rec[p];
+                int cnt = 0;  // a row alone reaching minPoints decides the point
+                for_stencil(p, 0, [&](int q, float2 rq, int) {
+                    cnt += pair(p, me, q, rq) ? 1 : 0;
+                    return cnt < min_points;
+                }, d);
+                if (cnt) atomicAdd(&par[p], cnt);
+            }
         }
-        core[p] = c ? 1 : 0;
-        par[p] = p;
-        ncore_local += c ? 1 : 0;
+        __syncthreads();
+        if (tid < m) {
+            const bool c = min_points <= 0 || (tid < nf && par[tid] >= min_points);
+            core[tid] = c ? 1 : 0;
+            par[tid] = tid;
+            ncore_local = c ? 1 : 0;
+        }
+    } else {
+        for (int p = tid; p < m; p += kSmT) {
+            bool c = min_points <= 0;
+            if (!c && p < nf) {
+                const float2 me = rec[p];
+                int cnt = 0;
+                for_stencil(p, 0, [&](int q, float2 rq, int) {
+                    cnt += pair(p, me, q, rq) ? 1 : 0;
+                    return cnt < min_points;
+                });
+                c = cnt >= min_points;
+            }
+            core[p] = c ? 1 : 0;
+            par[p] = p;
+            ncore_local += c ? 1 : 0;
+        }
     }
     __syncthreads();
     SM_STAMP(3);
@@ -453,7 +485,9 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // within eps makes p unite with some core of q's quarter.  So a dense cell costs a few
     // unions per point instead of one per neighbour.
     const bool quarters = G.clique != 0;
-    for (int p = tid; p < nf; p += kSmT) {
+    const int R = split ? 3 : 1;  // stencil rows per work item
+    for (int it = tid; it < nf * R; it += kSmT) {
+        const int p = split ? it / 3 : it, only = split ? it - 3 * (it / 3) : -1;
         if (!core[p]) continue;
         const float2 me = rec[p];
         uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
@@ -479,7 +513,7 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
                 if (quarters) done |= 1ull << bit;
             }
             return true;
-        });
+        }, only);
     }
     __syncthreads();
     SM_STAMP(4);
@@ -521,30 +555,48 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // ---- labels (LocalDBSCANNaive.scala:89-106; Archery re-claim :103-106) ----
     int32_t* cl_out = cluster + off;
     uint8_t* fl_out = flag + off;
-    for (int p = tid; p < m; p += kSmT) {
+    // the smallest root visit index among p's core neighbours in stencil row `only`
+    auto best_root = [&](int p, int only) -> uint32_t {
+        const float2 me = rec[p];
+        uint32_t best = 0xFFFFFFFFu;
+        for_stencil(p, 0, [&](int q, float2 rq, int) {
+            if (core[q]) {
+                const uint32_t s = info[par[q]] >> 16;
+                if (s < best && pair(p, me, q, rq)) best = s;
+            }
+            return true;
+        }, only);
+        return best;
+    };
+    auto write_label = [&](int p, uint32_t best) {
         const uint32_t v = info[p] >> 16;
         int cid = 0;
         uint8_t f = DBSCAN_FLAG_NOISE;
         if (core[p]) {
             cid = cluster_of(info[par[p]] >> 16);
             f = DBSCAN_FLAG_CORE;
-        } else if (p < nf) {
-            const float2 me = rec[p];
-            uint32_t best = 0xFFFFFFFFu;
-            for_stencil(p, 0, [&](int q, float2 rq, int) {
-                if (core[q]) {
-                    const uint32_t s = info[par[q]] >> 16;
-                    if (s < best && pair(p, me, q, rq)) best = s;
-                }
-                return true;
-            });
-            if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
-                cid = cluster_of(best);
-                f = DBSCAN_FLAG_BORDER;
-            }
+        } else if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
+            cid = cluster_of(best);
+            f = DBSCAN_FLAG_BORDER;
         }
         cl_out[v] = cid;
         fl_out[v] = f;
+    };
+    if (split) {
+        if (tid < m) sbest[tid] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid < 3 * m) {
+            const int p = tid / 3;
+            if (!core[p] && p < nf) {
+                const uint32_t b = best_root(p, tid - 3 * p);
+                if (b != 0xFFFFFFFFu) atomicMin(&sbest[p], b);
+            }
+        }
+        __syncthreads();
+        if (tid < m) write_label(tid, sbest[tid]);
+    } else {
+        for (int p = tid; p < m; p += kSmT)
+            write_label(p, (!core[p] && p < nf) ? best_root(p, -1) : 0xFFFFFFFFu);
     }
 
     SM_STAMP(6);
