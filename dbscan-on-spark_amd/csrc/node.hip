@@ -20,7 +20,9 @@
 #include "internal.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -51,6 +53,23 @@ int64_t host_threads() {
     }
     return std::max<int64_t>(1, std::min<int64_t>(n, 64));
 }
+
+// DBSCAN_NODE_TRACE=1: phase wall times on stderr (observability only; nothing computed changes)
+struct PhaseTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    PhaseTrace() {
+        const char* e = std::getenv("DBSCAN_NODE_TRACE");
+        on = e && e[0] == '1';
+    }
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[train_node] %-22s %9.3f s\n", what,
+                     std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    }
+};
 
 template <class F>
 void parallel_for(int nth, F&& f) {
@@ -280,7 +299,9 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         return DBSCAN_EHIP;
     }
     if (n_shards <= 0) n_shards = ndev;
+    PhaseTrace tr;
     const std::vector<double> cuts = make_cuts(x, n, n_shards, eps);
+    tr.mark("cuts");
     if (cuts.empty()) {  // one slab (or eps*eps not finite: all-pairs / no-pairs do not shard)
         dbscan_handle* h = dbscan_create(0);
         if (!h) {
@@ -332,6 +353,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                 c[2 * r + 1] += shared ? 1 : 0;
             });
     });
+    tr.mark("plan count");
     std::vector<int64_t> at((size_t)nth * world * 2, 0);
     for (int r = 0; r < world; ++r) {
         int64_t np = 0, ns = 0;
@@ -347,6 +369,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         sh[r].zone.resize((size_t)np);
         sh[r].shared.resize((size_t)ns);
     }
+    tr.mark("plan alloc");
     parallel_for(nth, [&](int t) {
         int64_t* a = &at[(size_t)t * world * 2];
         const auto [i0, i1] = chunk(t);
@@ -361,6 +384,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                 s.zone[(size_t)k] = z;
             });
     });
+    tr.mark("plan fill");
     // one host thread and one handle per device; the shards of a device run one after another
     // on its handle (one workspace per device: 8 shards of a 10^9-point job on one GPU)
     const int nworkers = std::min(world, ndev);
@@ -384,6 +408,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         for (auto& t : th) t.join();
     };
     each_device([&](int r, int w) { shard_fit(sh[r], hs[w], w, eps, min_points); });
+    tr.mark("slab fits");
     int32_t rc = DBSCAN_OK;
     for (auto& s : sh)
         if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
@@ -410,9 +435,11 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             std::vector<int32_t>().swap(s.root);
         }
         std::sort(all_roots.begin(), all_roots.end());
+        tr.mark("merge + numbering");
         each_device([&](int r, int w) {
             shard_label(sh[r], hs[w], w, eps, min_points, all_roots, mode, shared_dev);
         });
+        tr.mark("slab labels");
         for (auto& s : sh)
             if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
                 rc = s.rc;
@@ -432,8 +459,10 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             }
         });
         *n_clusters_out = (int64_t)all_roots.size();
+        tr.mark("output scatter");
     }
     for (auto* h : hs) dbscan_destroy(h);
+    tr.mark("teardown");
     return rc;
 }
 

@@ -1,6 +1,9 @@
 """Summarize a tools/profile.sh run into profiles/ (committed evidence).
 
-    python tools/pmc_summary.py gpurun_out/prof rNN
+    python tools/pmc_summary.py gpurun_out/prof rNN [--no-json]
+
+--no-json: the two CSVs only (a profile of another workload than the bench default's, e.g.
+config 5's share, leaves the bench's pmc_traffic.json alone).
 
 Writes
   profiles/<tag>_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (copied)
@@ -27,7 +30,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE_OF = {"count_tile_kernel": "count", "count_tile32_kernel": "count32",
             "tile_union_kernel": "tile_union", "edge_union_kernel": "edge_union",
-            "slab_root_labels_list_kernel": "slab_root_labels"}
+            "slab_root_labels_list_kernel": "slab_root_labels",
+            "tcell_kernel": "tslot", "thalo_kernel": "tstage"}
 
 
 def symbol(name):
@@ -122,10 +126,13 @@ def main():
                    "avg_ns": round(wavg("avg_ns"), 1), "valu_insts_per_launch": valu, "sq": sq,
                    "instances": {k: {kk: vv for kk, vv in v.items() if kk != "counters"}
                                  for k, v in inst.items()}}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump({"src_sha": stamp, "n_points": n_points,
-                   "source": f"profiles/{tag}_pmc.csv", "stages": out}, f, indent=1,
-                  sort_keys=True)
+    if "--no-json" in sys.argv[3:]:
+        out = None
+    if out is not None:
+        with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+            json.dump({"src_sha": stamp, "n_points": n_points,
+                       "source": f"profiles/{tag}_pmc.csv", "stages": out}, f, indent=1,
+                      sort_keys=True)
     for s, c, a, hbm, avg in rows[:25]:
         print(f"{s:40s} n={c:4d} avg_ns={a or 0:10.0f} hbm={hbm:14.0f}")
 

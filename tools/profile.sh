@@ -6,7 +6,7 @@
 #   bash tools/profile.sh && python tools/pmc_summary.py gpurun_out/prof rNN
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 rm -rf $OUT; mkdir -p $OUT
 ARGS="${BENCH_ARGS:---steps 5 --warmup 2} --no-cpu-baseline --e2e-steps 0"
 python3 -c "import bench; print(bench.src_stamp())" > $OUT/src_sha || exit 1
