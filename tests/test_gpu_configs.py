@@ -166,6 +166,8 @@ def test_config5_full_size_train_node(dm, handle):
     import json
     import time
 
+    if not os.path.exists(CONFIG5_DIGEST):
+        pytest.skip("no oracle digest yet: run test_config5_full_size_vs_oracle on demand")
     with open(CONFIG5_DIGEST) as f:
         gold = json.load(f)
     hx, hy = _config5_host_data(handle)
