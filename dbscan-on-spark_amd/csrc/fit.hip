@@ -515,7 +515,8 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
                 tqq[64] = qidx[end - 1] + 1;
                 const GridParams g = *gp;
                 const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
-                tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
+                if (tnb)  // (else thalo_kernel writes it)
+                    tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
                                    tile_occ(tmap, g, tx + 1, ty + 1), tile_occ(tmap, g, tx - 1, ty + 1));
             }
         }
@@ -636,63 +637,18 @@ __global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restri
     }
 }
 
-// The same three tables (tslot / tq, tstage, tsz; and tnb) without per-tile dependent-load
-// chains.  tslot_kernel and tstage_kernel walk the tiles one wave per tile with a grid stride:
-// at config 5's per-GPU share (1.46 M tiles, 178 per resident wave) each trip is a chain of
-// 3-5 dependent loads, so they took 0.85 + 0.75 ms there for ~1 KB per tile.  Here:
-// tcell_kernel: one thread per occupied cell (a tile's cells are contiguous in key order).  A
-// cell at local index l whose tile's previous occupied cell is at lp writes the entries
-// lp+1..l of its tile's tslot / tq rows and the interior staging entries of those local cells;
-// the tile's last cell also writes the entries past it (tile end).
-__global__ __launch_bounds__(kBlock) void tcell_kernel(const uint32_t* __restrict__ ckey,
-                                                       const int32_t* __restrict__ cstart,
-                                                       const int32_t* __restrict__ ncells_p,
-                                                       const int32_t* __restrict__ qidx,
-                                                       const int32_t* __restrict__ tmap,
-                                                       int32_t* __restrict__ tslot,
-                                                       int32_t* __restrict__ tq,
-                                                       int2* __restrict__ tstage) {
-    const int ncells = *ncells_p;
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= ncells) return;
-    const uint32_t k = ckey[c], tk = k >> 6;
-    const uint32_t kp = c > 0 ? ckey[c - 1] : ~0u;
-    const uint32_t kn = c + 1 < ncells ? ckey[c + 1] : ~0u;
-    const int st = cstart[c], en = cstart[c + 1];
-    const int t = tmap[tk];
-    const int l = (int)(k & 63u);
-    const int lp = (kp >> 6) == tk ? (int)(kp & 63u) : -1;
-    const bool last = (kn >> 6) != tk;
-    const int qs = qidx ? qidx[st] : 0;
-    const int qe = (qidx && last) ? qidx[en - 1] + 1 : 0;
-    int32_t* ts = tslot + (int64_t)t * kTslot;
-    int32_t* tqq = tq ? tq + (int64_t)t * kTslot : nullptr;
-    int2* stg = tstage + (int64_t)t * 100;
-    for (int m = lp + 1; m <= l; ++m) {
-        ts[m] = st;
-        if (tqq) tqq[m] = qs;
-        stg[((m >> 3) + 1) * 10 + (m & 7) + 1] = make_int2(st, m == l ? en - st : 0);
-    }
-    if (last) {
-        for (int m = l + 1; m < 64; ++m) {
-            ts[m] = en;
-            if (tqq) tqq[m] = qe;
-            stg[((m >> 3) + 1) * 10 + (m & 7) + 1] = make_int2(en, 0);
-        }
-        ts[64] = en;
-        if (tqq) tqq[64] = qe;
-    }
-}
-
-// thalo_kernel: the 36 halo entries of each tile's staging table (tstage_entry over the
-// neighbour tiles' tslot rows, written by tcell_kernel), tsz = own points + halo points, and
-// tnb (quarter grids).  One thread per halo entry of kHaloTiles tiles per trip; each thread
-// handles kHaloU trips' tiles with their loads issued together, so a resident wave keeps
-// kHaloU independent load chains in flight instead of one.
-constexpr int kHaloTiles = kBlock / 36;  // 7 tiles per block and trip (252 threads busy)
+// tstage / tsz / tnb with more loads in flight per wave.  tstage_kernel walks the tiles one wave
+// per tile with a grid stride: at config 5's per-GPU share (1.46 M tiles, ~178 per resident
+// wave) each trip is a chain of 3 dependent loads (tile key -> neighbour's occupied index ->
+// its tslot row).
+// thalo_kernel: the 100 staging entries of each tile (tstage_entry: the own tile's and the
+// neighbour tiles' tslot rows), tsz = their point count, and tnb (quarter grids).  One thread per
+// entry of kHaloTiles tiles per trip; each thread handles kHaloU trips' tiles with their loads
+// issued together, so a resident wave keeps kHaloU independent load chains in flight instead
+// of one.
+constexpr int kHaloTiles = kBlock / 100;  // 2 tiles per block and trip (200 threads busy)
 constexpr int kHaloU = 4;
 __global__ __launch_bounds__(kBlock) void thalo_kernel(const uint32_t* __restrict__ tkey,
-                                                       const int32_t* __restrict__ tstart,
                                                        const int32_t* __restrict__ ntiles_p,
                                                        const int32_t* __restrict__ tmap,
                                                        const int32_t* __restrict__ tslot,
@@ -703,21 +659,8 @@ __global__ __launch_bounds__(kBlock) void thalo_kernel(const uint32_t* __restric
     __shared__ int sum[kHaloU * kHaloTiles];
     const GridParams g = *gp;
     const int ntiles = *ntiles_p;
-    const int j = (int)threadIdx.x / 36, h = (int)threadIdx.x - j * 36;
-    // halo entry h -> extended cell (ex, ey): the top row, the bottom row, then the two side
-    // columns row by row
-    int ex, ey;
-    if (h < 10) {
-        ey = -1;
-        ex = h - 1;
-    } else if (h < 20) {
-        ey = 8;
-        ex = h - 11;
-    } else {
-        ey = (h - 20) >> 1;
-        ex = ((h - 20) & 1) ? 8 : -1;
-    }
-    const int k = (ey + 1) * 10 + ex + 1;
+    const int j = (int)threadIdx.x / 100, k = (int)threadIdx.x - j * 100;
+    const int ey = k / 10 - 1, ex = k % 10 - 1;  // extended cell k
     const int l = (ey & 7) * 8 + (ex & 7);
     const int dx = ex < 0 ? -1 : (ex > 7 ? 1 : 0), dy = ey < 0 ? -1 : (ey > 7 ? 1 : 0);
     // the entries that also name tnb's E, S, SE, SW neighbour
@@ -739,7 +682,9 @@ __global__ __launch_bounds__(kBlock) void thalo_kernel(const uint32_t* __restric
 #pragma unroll
             for (int u = 0; u < kHaloU; ++u) {
                 const int ty0 = (int)(tk[u] / g.ntx), tx0 = (int)(tk[u] - (uint32_t)ty0 * g.ntx);
-                occ[u] = t[u] < ntiles ? tile_occ(tmap, g, tx0 + dx, ty0 + dy) : -1;
+                occ[u] = t[u] >= ntiles ? -1
+                         : (dx == 0 && dy == 0) ? (int)t[u]
+                                                : tile_occ(tmap, g, tx0 + dx, ty0 + dy);
             }
             int2 e[kHaloU];
 #pragma unroll
@@ -762,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void thalo_kernel(const uint32_t* __restric
         if (threadIdx.x < kHaloU * kHaloTiles) {
             const int u = (int)threadIdx.x / kHaloTiles, jj = (int)threadIdx.x - u * kHaloTiles;
             const int64_t t = t0 + u * kHaloTiles + jj;
-            if (t < ntiles) tsz[t] = sum[threadIdx.x] + tstart[t + 1] - tstart[t];
+            if (t < ntiles) tsz[t] = sum[threadIdx.x];
         }
     }
 }
@@ -3521,12 +3466,11 @@ static constexpr int count_cap() { return DBSCAN_AB_COUNT_CAP; }
 static constexpr bool f32_count() { return DBSCAN_AB_F32 != 0; }
 static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
 // DBSCAN_AB_CAP32: staging capacity of count_tile32 (tiles over it take the big-tile path)
-// Per-tile tables by tcell_kernel + thalo_kernel (1) or the per-tile waves tslot_kernel +
-// tstage_kernel (0, A/B builds)
+// Staging tables by thalo_kernel (1) or tstage_kernel (0, A/B builds)
 #ifndef DBSCAN_AB_TABLES
-#define DBSCAN_AB_TABLES 0
+#define DBSCAN_AB_TABLES 1
 #endif
-constexpr bool kTablesPerCell = DBSCAN_AB_TABLES != 0;
+constexpr bool kTablesHalo = DBSCAN_AB_TABLES != 0;
 #ifndef DBSCAN_AB_CAP32
 #define DBSCAN_AB_CAP32 1536
 #endif
@@ -3812,16 +3756,18 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            if (kTablesPerCell) {
-                klaunch(prof, "tslot", tcell_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, ckey,
-                        cstart, &st[kStCells], qidx, tmap, tslot, qidx ? tq : nullptr, tstage);
+            if (kTablesHalo) {  // (tnb: thalo_kernel)
+                klaunch(prof, "tslot", tslot_kernel,
+                        dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
+                        dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
+                        &st[kStCells], qidx, tmap, gp, tslot, tq, (int4*)nullptr);
                 DBSCAN_HIP_CHECK(hipGetLastError());
                 klaunch(prof, "tstage", thalo_kernel,
                         dim3((unsigned)std::min<int64_t>(
                             (ntile_bound + kHaloTiles * kHaloU - 1) / (kHaloTiles * kHaloU),
                             kTileGrid)),
-                        dim3(kBlock), 0, s, tkey, tstart, &st[kStTiles], tmap, tslot, gp, tstage,
-                        tsz, qidx ? tnb : nullptr);
+                        dim3(kBlock), 0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz,
+                        qidx ? tnb : nullptr);
                 DBSCAN_HIP_CHECK(hipGetLastError());
             } else {
                 klaunch(prof, "tslot", tslot_kernel,
