@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
     const int32_t* __restrict__ offs,
     int32_t* __restrict__ cell, uint32_t* __restrict__ ckey, int32_t* __restrict__ cstart,
     int32_t* __restrict__ qidx, uint32_t* __restrict__ qkey, int32_t* __restrict__ qstart,
-    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart) {
+    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart, int32_t* __restrict__ cq) {
     __shared__ int wcnt[2][3][kBlock / 64];
     const int64_t nf = *nf_p;
     const int64_t base = (int64_t)blockIdx.x * kHeadTile;
@@ -441,6 +441,7 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
             if (h.c) {
                 ckey[ic] = k >> 2;
                 cstart[ic] = (int32_t)p;
+                if (cq) cq[ic] = iq;  // (a cell head heads a quarter)
             }
             if (qidx) {
                 qidx[p] = iq + h.q - 1;
@@ -456,6 +457,7 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
             if (p == nf - 1) {  // end sentinels
                 cstart[ic + h.c] = (int32_t)nf;
                 if (qidx) qstart[iq + h.q] = (int32_t)nf;
+                if (cq) cq[ic + h.c] = iq + h.q;
                 tstart[it + h.t] = (int32_t)nf;
             }
         }
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
     const int32_t* __restrict__ ncells_p, const int32_t* __restrict__ qidx,
     const int32_t* __restrict__ tmap, const GridParams* __restrict__ gp,
     int32_t* __restrict__ tslot,
-    int32_t* __restrict__ tq, int4* __restrict__ tnb) {
+    int32_t* __restrict__ tq, int4* __restrict__ tnb, const int32_t* __restrict__ cq) {
     // one wave per tile, one lane per local cell
     const int lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
@@ -500,9 +502,11 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
         for (int o = 1; o < 64; o <<= 1) occ |= __shfl_xor(occ, o, 64);
         const uint64_t rest = occ >> lane;
         int st = end;
+        // first occupied local cell >= lane: its rank in the tile (the tile's cell count if none)
+        int rank = __popcll(occ);
         if (rest) {
-            const int nl = lane + __builtin_ctzll(rest);  // first occupied local >= lane
-            const int rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
+            const int nl = lane + __builtin_ctzll(rest);
+            rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
             st = cstart[c0 + rank];
         }
         int32_t* ts = tslot + (int64_t)t * kTslot;
@@ -510,9 +514,13 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
         if (lane == 0) ts[64] = end;
         if (qidx) {
             int32_t* tqq = tq + (int64_t)t * kTslot;
-            tqq[lane] = st < end ? qidx[st] : qidx[end - 1] + 1;
+            // cq (heads_down): each cell's first quarter, cq[C] = Q, so the entry past the tile's
+            // last cell is the next tile's first quarter = qidx[end - 1] + 1; read next to
+            // cstart instead of gathering qidx at each cell's first slot
+            const int qend = cq ? cq[c0 + __popcll(occ)] : qidx[end - 1] + 1;
+            tqq[lane] = cq ? cq[c0 + rank] : (st < end ? qidx[st] : qend);
             if (lane == 0) {
-                tqq[64] = qidx[end - 1] + 1;
+                tqq[64] = qend;
                 const GridParams g = *gp;
                 const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
                 if (tnb)  // (else thalo_kernel writes it)
@@ -3471,6 +3479,12 @@ static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
 #define DBSCAN_AB_TABLES 1
 #endif
 constexpr bool kTablesHalo = DBSCAN_AB_TABLES != 0;
+// tslot_kernel's quarter table from a per-cell first-quarter array written by heads_down (1) or
+// by gathering qidx at each cell's first slot (0, A/B builds)
+#ifndef DBSCAN_AB_CQ
+#define DBSCAN_AB_CQ 1
+#endif
+constexpr bool kCellQuarter = DBSCAN_AB_CQ != 0;
 #ifndef DBSCAN_AB_CAP32
 #define DBSCAN_AB_CAP32 1536
 #endif
@@ -3674,6 +3688,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* qidx = static_cast<int32_t*>(ws.qidx.ensure(n * sizeof(int32_t)));
     uint32_t* qkey = static_cast<uint32_t*>(ws.qkey.ensure(n * sizeof(uint32_t)));
     int32_t* qstart = static_cast<int32_t*>(ws.qstart.ensure((n + 1) * sizeof(int32_t)));
+    // each cell's first quarter (+ the quarter count), for tslot_kernel's quarter table
+    int32_t* cq = kCellQuarter ? static_cast<int32_t*>(ws.cq.ensure((n + 1) * sizeof(int32_t)))
+                               : nullptr;
     int4* qinfo = static_cast<int4*>(ws.qrep.ensure(n * sizeof(int4)));
     int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
     // the tile-local quarter union runs inside the count kernels (slab fits: the fp32 count
@@ -3743,7 +3760,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan);
             exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
-                               offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
+                    offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart, cq);
             DBSCAN_HIP_CHECK(hipGetLastError());
             if (tpart)
                 klaunch(prof, "tile_part", tile_part_kernel, dim3(nblk(ntile_bound)),
@@ -3760,7 +3777,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "tslot", tslot_kernel,
                         dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
                         dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
-                        &st[kStCells], qidx, tmap, gp, tslot, tq, (int4*)nullptr);
+                        &st[kStCells], qidx, tmap, gp, tslot, tq, (int4*)nullptr, cq);
                 DBSCAN_HIP_CHECK(hipGetLastError());
                 klaunch(prof, "tstage", thalo_kernel,
                         dim3((unsigned)std::min<int64_t>(
@@ -3773,7 +3790,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "tslot", tslot_kernel,
                         dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
                         dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
-                        &st[kStCells], qidx, tmap, gp, tslot, tq, tnb);
+                        &st[kStCells], qidx, tmap, gp, tslot, tq, tnb, cq);
                 DBSCAN_HIP_CHECK(hipGetLastError());
                 klaunch(prof, "tstage", tstage_kernel,
                         dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),

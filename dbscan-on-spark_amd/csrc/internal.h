@@ -175,7 +175,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm;
+        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, cq;
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
@@ -190,7 +190,7 @@ struct Workspace {
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
-                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm})
+                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm, &cq})
             b->release();
     }
 };
