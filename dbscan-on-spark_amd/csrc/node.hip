@@ -26,7 +26,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -82,22 +84,62 @@ void parallel_for(int nth, F&& f) {
     for (auto& t : th) t.join();
 }
 
+// Host arrays of the slab plan: resize() leaves the elements uninitialized (every element is
+// written before it is read), so the 10^9-point plan's ~40 GB are first touched by the parallel
+// fill instead of being zeroed by one thread.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using HostVec = std::vector<T, NoInitAlloc<T>>;
+
 // node.py make_cuts: world-1 cuts at count quantiles of a strided sample of the finite x,
-// snapped down to the 2*eps grid, non-decreasing.
+// snapped down to the 2*eps grid, non-decreasing.  The finite count and the sample (every
+// step-th finite x in input order) by host threads over contiguous chunks.
 std::vector<double> make_cuts(const double* x, int64_t n, int world, double eps) {
     std::vector<double> cuts;
     if (world <= 1 || !std::isfinite(eps * eps)) return cuts;
-    std::vector<double> xf;
-    int64_t nfin = 0;
-    for (int64_t i = 0; i < n; ++i) nfin += std::isfinite(x[i]) ? 1 : 0;
+    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / 65536 + 1));
+    const auto chunk = [&](int t) { return std::make_pair(n * t / nth, n * (t + 1) / nth); };
+    std::vector<int64_t> fin(nth + 1, 0);
+    parallel_for(nth, [&](int t) {
+        const auto [i0, i1] = chunk(t);
+        int64_t c = 0;
+        for (int64_t i = i0; i < i1; ++i) c += std::isfinite(x[i]) ? 1 : 0;
+        fin[t + 1] = c;
+    });
+    for (int t = 0; t < nth; ++t) fin[t + 1] += fin[t];
+    const int64_t nfin = fin[nth];
     if (nfin == 0) return cuts;
     const int64_t step = std::max<int64_t>(1, nfin / (1 << 20));
-    int64_t k = 0;
-    for (int64_t i = 0; i < n; ++i)
-        if (std::isfinite(x[i])) {
-            if (k % step == 0) xf.push_back(x[i]);
-            ++k;
-        }
+    // finite index k is sampled when k % step == 0; chunk t starts at finite index fin[t]
+    std::vector<int64_t> soff(nth + 1, 0);
+    for (int t = 0; t < nth; ++t) soff[t + 1] = (fin[t + 1] + step - 1) / step;
+    std::vector<double> xf((size_t)soff[nth]);
+    parallel_for(nth, [&](int t) {
+        const auto [i0, i1] = chunk(t);
+        int64_t k = fin[t], o = soff[t];
+        for (int64_t i = i0; i < i1; ++i)
+            if (std::isfinite(x[i])) {
+                if (k % step == 0) xf[(size_t)o++] = x[i];
+                ++k;
+            }
+    });
     std::sort(xf.begin(), xf.end());
     const double grid = 2.0 * std::fabs(eps);
     const int64_t m = (int64_t)xf.size();
@@ -111,14 +153,14 @@ std::vector<double> make_cuts(const double* x, int64_t n, int world, double eps)
 }
 
 struct Shard {
-    std::vector<int64_t> gid;  // slab points, increasing global visit index
-    std::vector<double> x, y;
-    std::vector<uint8_t> zone;
-    std::vector<int32_t> shared;  // slab indices of points in zones 0/1 of another shard too
-    std::vector<int32_t> root;    // slab fit output (-1: not core)
-    std::vector<int64_t> gs;      // global s(K) per local root
-    std::vector<int32_t> cluster;
-    std::vector<uint8_t> flag;
+    HostVec<int64_t> gid;  // slab points, increasing global visit index
+    HostVec<double> x, y;
+    HostVec<uint8_t> zone;
+    HostVec<int32_t> shared;  // slab indices of points in zones 0/1 of another shard too
+    HostVec<int32_t> root;    // slab fit output (-1: not core)
+    HostVec<int64_t> gs;      // global s(K) per local root (only the roots' entries are read)
+    HostVec<int32_t> cluster;
+    HostVec<uint8_t> flag;
     std::string err;
     int32_t rc = DBSCAN_OK;
 };
@@ -191,7 +233,7 @@ bool shard_upload_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_
 // Phase 1 of one shard: slab fit, roots back to the host.
 void shard_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points) {
     const int64_t m = (int64_t)s.gid.size();
-    s.root.assign(m, -1);
+    s.root.resize(m);  // (downloaded whole)
     if (m == 0) return;
     ShardDev d;
     if (shard_upload_fit(s, h, device, eps, min_points, &d)) {
@@ -211,8 +253,8 @@ void shard_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_p
 void shard_label(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points,
                  const std::vector<int64_t>& all_roots, int32_t mode, bool refit) {
     const int64_t m = (int64_t)s.gid.size();
-    s.cluster.assign(m, 0);
-    s.flag.assign(m, DBSCAN_FLAG_NOT_FLAGGED);
+    s.cluster.resize(m);  // (downloaded whole; only zone-0 entries are used)
+    s.flag.resize(m);
     if (m == 0) return;
     ShardDev fitd;
     if (refit && !shard_upload_fit(s, h, device, eps, min_points, &fitd)) {
@@ -235,8 +277,9 @@ void shard_label(Shard& s, dbscan_handle* h, int device, double eps, int32_t min
     if (e == hipSuccess) e = hipMemcpy(dgs, s.gs.data(), m * sizeof(int64_t), hipMemcpyHostToDevice);
     if (e == hipSuccess && nr > 0)
         e = hipMemcpy(droots, all_roots.data(), nr * sizeof(int64_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dcl, s.cluster.data(), m * sizeof(int32_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dfl, s.flag.data(), m, hipMemcpyHostToDevice);
+    // zone 1/2 entries are not labelled here (the output takes zone-0 entries only)
+    if (e == hipSuccess) e = hipMemset(dcl, 0, m * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemset(dfl, DBSCAN_FLAG_NOT_FLAGGED, m);
     if (e != hipSuccess) {
         s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
         s.err = std::string("shard label upload: ") + hipGetErrorString(e);
@@ -425,14 +468,21 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             }
         for (auto& s : sh) {
             const int64_t m = (int64_t)s.gid.size();
-            s.gs.assign(m, 0);
-            for (int64_t p = 0; p < m; ++p)
-                if (s.root[p] == (int32_t)p) {
-                    const int64_t g = s.gid[p], gs = uf.find(g);
-                    s.gs[p] = gs;
-                    if (s.zone[p] == 0 && gs == g) all_roots.push_back(g);
+            s.gs.resize(m);  // (only the local roots' entries are read)
+            // the local roots by host threads (per-thread lists in slab order), then their global
+            // s(K) on this thread (the union-find compresses paths as it goes)
+            std::vector<std::vector<int32_t>> lr(nth);
+            parallel_for(nth, [&](int t) {
+                for (int64_t p = m * t / nth, p1 = m * (t + 1) / nth; p < p1; ++p)
+                    if (s.root[(size_t)p] == (int32_t)p) lr[t].push_back((int32_t)p);
+            });
+            for (auto& l : lr)
+                for (int32_t p : l) {
+                    const int64_t g = s.gid[(size_t)p], gs = uf.find(g);
+                    s.gs[(size_t)p] = gs;
+                    if (s.zone[(size_t)p] == 0 && gs == g) all_roots.push_back(g);
                 }
-            std::vector<int32_t>().swap(s.root);
+            HostVec<int32_t>().swap(s.root);
         }
         std::sort(all_roots.begin(), all_roots.end());
         tr.mark("merge + numbering");
