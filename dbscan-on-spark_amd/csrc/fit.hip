@@ -3482,7 +3482,7 @@ constexpr bool kTablesHalo = DBSCAN_AB_TABLES != 0;
 // tslot_kernel's quarter table from a per-cell first-quarter array written by heads_down (1) or
 // by gathering qidx at each cell's first slot (0, A/B builds)
 #ifndef DBSCAN_AB_CQ
-#define DBSCAN_AB_CQ 1
+#define DBSCAN_AB_CQ 0
 #endif
 constexpr bool kCellQuarter = DBSCAN_AB_CQ != 0;
 #ifndef DBSCAN_AB_CAP32

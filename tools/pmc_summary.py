@@ -2,6 +2,8 @@
 
     python tools/pmc_summary.py gpurun_out/prof rNN [--no-json]
 
+PROF_DEST=dir: write there instead of profiles/ (on the GPU box: under gpurun_out/, so the
+summaries come back while the raw traces, over gpurun's 64 MiB return limit, are deleted).
 --no-json: the two CSVs only (a profile of another workload than the bench default's, e.g.
 config 5's share, leaves the bench's pmc_traffic.json alone).
 
@@ -72,7 +74,7 @@ def stage_of(sym):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    prof = os.path.join(ROOT, "profiles")
+    prof = os.environ.get("PROF_DEST") or os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, f"{tag}_kernel_stats.csv"))
