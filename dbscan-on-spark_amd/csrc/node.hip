@@ -166,25 +166,46 @@ struct Shard {
 };
 
 // node.py zones(): zone of x for shard r (0 owned, 1 inner halo, 2 outer halo, kOut) and
-// whether the point is shared (in zone 0/1 of an adjacent shard as well).
-uint8_t zone_of(double x, int r, int world, const std::vector<double>& cuts, double R,
-                bool* shared) {
-    const bool has_lo = r > 0, has_hi = r < world - 1;
-    const double lo = has_lo ? cuts[r - 1] : 0.0, hi = has_hi ? cuts[r] : 0.0;
-    bool own = (!has_lo || x >= lo) && (!has_hi || x < hi);
+// whether the point is shared (in zone 0/1 of an adjacent shard as well).  The margins depend on
+// the cut values alone, so they are computed once per shard (ZoneCut), not per point.
+struct ZoneCut {
+    bool has_lo = false, has_hi = false;
+    double lo = 0, hi = 0, m1lo = 0, m2lo = 0, m1hi = 0, m2hi = 0;
+};
+
+std::vector<ZoneCut> zone_cuts(int world, const std::vector<double>& cuts, double R) {
+    std::vector<ZoneCut> zc(world);
+    for (int r = 0; r < world; ++r) {
+        ZoneCut& z = zc[r];
+        z.has_lo = r > 0;
+        z.has_hi = r < world - 1;
+        if (z.has_lo) {
+            z.lo = cuts[r - 1];
+            z.m1lo = margin1(z.lo, R);
+            z.m2lo = margin2(z.lo, R);
+        }
+        if (z.has_hi) {
+            z.hi = cuts[r];
+            z.m1hi = margin1(z.hi, R);
+            z.m2hi = margin2(z.hi, R);
+        }
+    }
+    return zc;
+}
+
+uint8_t zone_of(double x, int r, int world, const ZoneCut& c, bool* shared) {
+    bool own = (!c.has_lo || x >= c.lo) && (!c.has_hi || x < c.hi);
     if (r == 0 && world > 1 && std::isnan(x)) own = true;
     bool in1 = false, in2 = false, sh = false;
-    if (has_lo) {
-        const double m1 = margin1(lo, R), m2 = margin2(lo, R);
-        in1 = in1 || (x >= lo - m1 && x < lo);
-        in2 = in2 || (x >= lo - m2 && x < lo - m1);
-        sh = sh || (own && x <= lo + m1);
+    if (c.has_lo) {
+        in1 = in1 || (x >= c.lo - c.m1lo && x < c.lo);
+        in2 = in2 || (x >= c.lo - c.m2lo && x < c.lo - c.m1lo);
+        sh = sh || (own && x <= c.lo + c.m1lo);
     }
-    if (has_hi) {
-        const double m1 = margin1(hi, R), m2 = margin2(hi, R);
-        in1 = in1 || (x >= hi && x <= hi + m1);
-        in2 = in2 || (x > hi + m1 && x <= hi + m2);
-        sh = sh || (own && x >= hi - m1);
+    if (c.has_hi) {
+        in1 = in1 || (x >= c.hi && x <= c.hi + c.m1hi);
+        in2 = in2 || (x > c.hi + c.m1hi && x <= c.hi + c.m2hi);
+        sh = sh || (own && x >= c.hi - c.m1hi);
     }
     const uint8_t z = own ? 0 : (in1 ? 1 : (in2 ? 2 : kOut));
     *shared = sh || z == 1;
@@ -360,6 +381,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
     }
     const int world = (int)cuts.size() + 1;
     const double R = reach(eps);
+    const std::vector<ZoneCut> zc = zone_cuts(world, cuts, R);
     std::vector<Shard> sh(world);
     // slab plan: every shard's points in increasing global visit order, built by host threads
     // over contiguous chunks of the input (count, then fill at the chunk's offsets)
@@ -378,7 +400,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         for (int dir = -1; dir <= 1; dir += 2) {
             for (int r = (dir < 0 ? own : own + 1); r >= 0 && r < world; r += dir) {
                 bool shared = false;
-                const uint8_t z = zone_of(x[i], r, world, cuts, R, &shared);
+                const uint8_t z = zone_of(x[i], r, world, zc[r], &shared);
                 if (z == kOut) {
                     if (r != own) break;
                     continue;

@@ -8,7 +8,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=${PROF_OUT:-gpurun_out/prof}
 rm -rf $OUT; mkdir -p $OUT
-ARGS="${BENCH_ARGS:---steps 5 --warmup 2} --no-cpu-baseline --e2e-steps 0"
+ARGS="${BENCH_ARGS:---steps 5 --warmup 2} --no-cpu-baseline --e2e-steps 0 --no-seam"
 python3 -c "import bench; print(bench.src_stamp())" > $OUT/src_sha || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 1; }
 echo "trace ok"

@@ -2,7 +2,8 @@
 # Round-end evidence in one GPU call: smoke, the default bench (config 2 with the CPU baseline and
 # the end-to-end leg and the seam leg), the node path at N = 1 on config 3's per-GPU share, its
 # one-rank RCCL rehearsal (--force-collectives), configs 3/4/5 per-GPU shares, then tools/profile.sh (kernel trace + PMC passes).
-# Each step under its own limit; the first failure ends the script.  NO_PROFILE=1: benches only.
+# Each step under its own limit; the first failure ends the script.  NO_PROFILE=1: benches only;
+# TAG names the profile summaries (gpurun_out/ev/profiles/<TAG>_*, copy them to profiles/).
 set -o pipefail
 mkdir -p gpurun_out/ev
 run() {  # name, limit, command...
@@ -18,4 +19,10 @@ run bench_noise 300 python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-ba
 run bench_dense 300 python bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-seam
 run bench_big 300 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 2 --no-seam
 grep -h '^{' gpurun_out/ev/bench_*.log | cut -c1-200
-[ "${NO_PROFILE:-0}" = 1 ] || bash tools/profile.sh
+[ "${NO_PROFILE:-0}" = 1 ] && exit 0
+# the raw traces exceed gpurun's 64 MiB return limit: summarize here, keep the summaries only
+bash tools/profile.sh || exit 1
+mkdir -p gpurun_out/ev/profiles
+PROF_DEST=gpurun_out/ev/profiles python3 tools/pmc_summary.py gpurun_out/prof ${TAG:-round_ev} > gpurun_out/ev/pmc_summary.txt 2>&1 || exit 1
+cp gpurun_out/prof/trace.log gpurun_out/ev/profile_trace.log
+rm -rf gpurun_out/prof
