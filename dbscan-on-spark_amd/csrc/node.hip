@@ -399,6 +399,11 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                                     cuts.begin());
         for (int dir = -1; dir <= 1; dir += 2) {
             for (int r = (dir < 0 ? own : own + 1); r >= 0 && r < world; r += dir) {
+                // a shard past the owner's is reached only through its outer halo margin
+                // (zone_of would say kOut; NaN included): most points stop here at once
+                if (r != own && (dir < 0 ? !(x[i] <= zc[r].hi + zc[r].m2hi)
+                                         : !(x[i] >= zc[r].lo - zc[r].m2lo)))
+                    break;
                 bool shared = false;
                 const uint8_t z = zone_of(x[i], r, world, zc[r], &shared);
                 if (z == kOut) {

@@ -17,6 +17,11 @@
   DBSCANRectangle corners, EvenSplitPartitioner.scala:186-197), one per line with its file:line:
   java.lang.Double.toString outputs of the reference's runtime, so format_double must print
   each parsed value back as the same string.  Needs /root/reference (generation only).
+* config5_oracle_digest.json -- NOT made here: needs an MI355X (the device generator's 10^9
+  points) and ~3 minutes of the oracle on the box's cores.  Written by
+  `DBSCAN_TEST_FULL_SCALE=1 pytest tests/test_gpu_configs.py -k config5_full_size_vs_oracle`
+  (gpurun_out/config5_oracle_digest.json: sha256 of oracle_fit_grid's cluster and flag arrays,
+  cluster and core counts) and copied here.
 """
 from __future__ import annotations
 
