@@ -221,11 +221,12 @@ class HipSlabOps:
         self.close()
         return False
 
-    def __del__(self):
+    def __del__(self, _finalizing=sys.is_finalizing):
         # Callers close() explicitly (NodeJob.close, the bench, the tests).  A finalizer may run
         # at interpreter shutdown, after torch has torn down its streams: HIP calls from here are
         # best-effort only, and never once the interpreter is finalizing or the handle is gone.
-        if not self._bound or sys.is_finalizing() or not getattr(self.h, "_h", None):
+        # (sys.is_finalizing is bound at definition: module globals may already be None here.)
+        if not getattr(self, "_bound", False) or _finalizing() or not getattr(self.h, "_h", None):
             return
         try:
             self.close()

@@ -44,3 +44,4 @@ for _ in range(K):
 torch.cuda.synchronize()
 tot = (time.perf_counter() - t0) * 1e3 / K
 print({k: round(v / K, 3) for k, v in T.items()}, "total_ms", round(tot, 3))
+job.close()
