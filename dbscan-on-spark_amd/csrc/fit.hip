@@ -175,9 +175,13 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
     if (i >= n) return;
     const GridParams g = *gp;
     const double a = x[i], b = y[i];
+    if (g.nparts == 0) {  // the fit's own grid (the bucketed sort's MSD pass bins the same way)
+        key[i] = grid_key(a, b, g);
+        return;
+    }
     uint32_t k = kSentinelKey;
-    // the grid of this point: the fit's own, or (batched fits) its partition's local grid at
-    // that partition's place in the virtual tile grid
+    // batched fits: the point's partition's local grid at that partition's place in the
+    // virtual tile grid
     double xmin2 = g.xmin2, ymin2 = g.ymin2, mx = 2.0 * (double)g.nx - 1.0,
            my = 2.0 * (double)g.ny - 1.0;
     uint32_t qx0 = 0, qy0 = 0;
@@ -3485,6 +3489,11 @@ constexpr bool kTablesHalo = DBSCAN_AB_TABLES != 0;
 #define DBSCAN_AB_CQ 0
 #endif
 constexpr bool kCellQuarter = DBSCAN_AB_CQ != 0;
+// Bucketed sort: the MSD pass bins the points itself (1) or reads bin_kernel's keys (0, A/B)
+#ifndef DBSCAN_AB_BIN_MSD
+#define DBSCAN_AB_BIN_MSD 1
+#endif
+constexpr bool kBinInMsd = DBSCAN_AB_BIN_MSD != 0;
 #ifndef DBSCAN_AB_CAP32
 #define DBSCAN_AB_CAP32 1536
 #endif
@@ -3632,7 +3641,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "grid", grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        {
+        if (!bucketed || !kBinInMsd) {
             StageTimer t(prof, s, "bin");
             klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key);
             DBSCAN_HIP_CHECK(hipGetLastError());
@@ -3645,8 +3654,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "shared_mark", shared_mark_kernel, dim3(nblk(a.n_shared)),
                         dim3(kBlock), 0, s, a.n_shared, a.shared_idx, shm);
             }
-            bucket_sort(s, a.x, a.y, key, n, &st[kStBits], ws.bucket, ws.hist, ws.scan, prof,
-                        a.zone, shm);
+            bucket_sort(s, a.x, a.y, kBinInMsd ? nullptr : key, n, &st[kStBits], ws.bucket,
+                        ws.hist, ws.scan, prof, a.zone, shm, gp);
             key = ws.bucket.key_fin;  // (perm: written by scatter_bucket_kernel below)
         } else {
             uint32_t* key3 = static_cast<uint32_t*>(ws.key3.ensure(n * sizeof(uint32_t)));

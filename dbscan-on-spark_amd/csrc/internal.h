@@ -217,6 +217,24 @@ struct GridParams {
     const int64_t* poffs = nullptr;
 };
 
+// The sort key of a point on a fit's own grid (not batched): tile << 8 | cell-in-tile << 2 |
+// quadrant, the sentinel for a non-finite point.  bin_kernel and the bucketed sort's MSD pass
+// (which bins on the fly instead of reading bin_kernel's keys) share it.
+__device__ __forceinline__ uint32_t grid_key(double a, double b, const GridParams& g) {
+    if (!__builtin_isfinite(a) || !__builtin_isfinite(b)) return kSentinelKey;
+    const double mx = 2.0 * (double)g.nx - 1.0, my = 2.0 * (double)g.ny - 1.0;
+    // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
+    double fx = floor(2.0 * ((a * 0.5 - g.xmin2) * g.invx));
+    double fy = floor(2.0 * ((b * 0.5 - g.ymin2) * g.invy));
+    fx = fx < 0 ? 0 : (fx > mx ? mx : fx);
+    fy = fy < 0 ? 0 : (fy > my ? my : fy);
+    const uint32_t qx = (uint32_t)fx, qy = (uint32_t)fy;
+    const uint32_t cx = qx >> 1, cy = qy >> 1;
+    const uint32_t tile = (cy >> 3) * g.ntx + (cx >> 3);
+    const uint32_t local = ((cy & 7u) << 3) | (cx & 7u);
+    return (tile << 8) | (local << 2) | ((qy & 1u) << 1) | (qx & 1u);
+}
+
 // What enqueue_fit needs for a batched fit (planned on the host by plan_batch_grid).
 struct BatchFit {
     GridParams g;                // the virtual grid (nparts, parts, poffs set)
@@ -399,9 +417,12 @@ void radix_sort_pairs(hipStream_t s, uint32_t*& key, int32_t*& val, uint32_t*& k
 int64_t bucket_padded(int64_t n);
 // zone (slab fits): each point's zone rides in its record (gather_bucket writes zs from it);
 // shm (lean slab fits): the listed shared points, whose slots gather_bucket writes by input index
+// key == nullptr: the MSD pass bins x, y on *gp itself (grid_key), so bin_kernel's key pass
+// and its 4 B/point key array are skipped.
 void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
                  const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
-                 Profiler* prof, const uint8_t* zone = nullptr, const uint8_t* shm = nullptr);
+                 Profiler* prof, const uint8_t* zone = nullptr, const uint8_t* shm = nullptr,
+                 const GridParams* gp = nullptr);
 
 // Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
 void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,

@@ -236,6 +236,44 @@ __global__ __launch_bounds__(kBlock) void radix_upsweep_kernel(const uint32_t* _
     }
 }
 
+// The bucketed sort's MSD histogram (top 8 bits of the device-side key width) binning x, y on
+// the fly (grid_key): the MSD pass never reads a key array, so bin_kernel's pass is skipped.
+__global__ __launch_bounds__(kBlock) void msd_upsweep_xy_kernel(const double* __restrict__ x,
+                                                                const double* __restrict__ y,
+                                                                int64_t n,
+                                                                const GridParams* __restrict__ gp,
+                                                                const int32_t* __restrict__ bits_p,
+                                                                int32_t* __restrict__ hist) {
+    constexpr int RB = 256;
+    const int b = *bits_p;
+    const int shift = b > 8 ? b - 8 : 0;
+    const GridParams g = *gp;
+    __shared__ uint32_t h[kWaves][RB];
+    const int w = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < kWaves * RB; d += kBlock) (&h[0][0])[d] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kRTile;
+    double a[kRItems], c[kRItems];
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {  // every load in flight together
+        const int64_t i = base + r * kBlock + threadIdx.x;
+        a[r] = i < n ? x[i] : 0.0;
+        c[r] = i < n ? y[i] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {
+        const int64_t i = base + r * kBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[w][(grid_key(a[r], c[r], g) >> shift) & (RB - 1u)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < RB; d += kBlock) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; ++k) t += h[k][d];
+        hist[(int64_t)blockIdx.x * RB + d] = (int32_t)t;  // block-major: one coalesced row
+    }
+}
+
 // Global offset of every (radix tile, digit) from the block-major count table, in one launch:
 // off[b][d] = sum over digits d' < d of all tiles' counts + sum over tiles b' < b of digit d.
 // kOffBlocks workgroups of 1024 threads, RB digits x (1024 / RB) row groups: each sums its
@@ -628,6 +666,7 @@ struct BucketExtra {
     const uint8_t* shm;   // MODE 1, lean slab fits: 1 for the listed shared points (or nullptr)
     const int32_t* pshift;
     const int2* tseg;
+    const GridParams* gp;  // MODE 1 with key == nullptr: bin x, y here (grid_key)
 };
 
 template <int W, int MODE>
@@ -678,14 +717,17 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
     for (int r = 0; r < kRItems; ++r) {
         const int64_t i = wbase + r * 64 + lane;
         const bool valid = i < base + tile_n;
-        const uint32_t k = valid ? key[i] : kSentinelKey;
+        uint32_t k = kSentinelKey;
         const int32_t v = valid ? (val ? val[i] : (int32_t)i) : 0;
         if constexpr (MODE == 1)
         {
             c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
+            if (valid) k = key ? key[i] : grid_key(c_r[r].x, c_r[r].y, *ex.gp);
             z_r[r] = (valid && ex.zone) ? (uint32_t)ex.zone[i] |
                                               ((ex.shm && ex.shm[i]) ? 256u : 0u)
                                         : 0u;
+        } else {
+            if (valid) k = key[i];
         }
         const uint32_t d = (k >> shift) & (RB - 1u);
         uint64_t peers = __ballot(valid);
@@ -982,7 +1024,8 @@ int64_t bucket_padded(int64_t n) { return ((n + kRTile - 1) / kRTile + 256) * kR
 
 void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t* key, int64_t n,
                  const int32_t* bits_dev, BucketSort& b, DevBuf& hist, ScanState& scan,
-                 Profiler* prof, const uint8_t* zone, const uint8_t* shm) {
+                 Profiler* prof, const uint8_t* zone, const uint8_t* shm, const GridParams* gp) {
+    if (!key && !gp) throw ArgError{"bucket_sort: no keys and no grid"};
     if (n <= 0) return;
     const int64_t np = bucket_padded(n), ntp = np / kRTile, nb = (n + kRTile - 1) / kRTile;
     int32_t* h = static_cast<int32_t*>(hist.ensure((size_t)2 * ntp * 512 * sizeof(int32_t)));
@@ -1004,8 +1047,12 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     b.np = np;
     {  // the MSD pass: top 8 bits, into padded segments, coordinates moved along
         StageTimer st(prof, s, "sort_msd");
-        klaunch(prof, "radix_upsweep<8>", radix_upsweep_kernel<8>, dim3((unsigned)nb),
-                dim3(kBlock), 0, s, key, n, -1, bits_dev, nb, h);
+        if (key)
+            klaunch(prof, "radix_upsweep<8>", radix_upsweep_kernel<8>, dim3((unsigned)nb),
+                    dim3(kBlock), 0, s, key, n, -1, bits_dev, nb, h);
+        else  // (bins x, y itself: no bin_kernel pass)
+            klaunch(prof, "msd_upsweep", msd_upsweep_xy_kernel, dim3((unsigned)nb), dim3(kBlock),
+                    0, s, x, y, n, gp, bits_dev, h);
         uint64_t* state = scan.prepare(s, (int64_t)kOffBlocks * 512);
         klaunch(prof, "radix_offsets<8>", radix_offsets_kernel<8>, dim3(kOffBlocks),
                 dim3(kOffThreads), 0, s, (const int32_t*)h, nb, ho, state, scan.epoch, bits_dev,
@@ -1014,7 +1061,7 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                 (const int32_t*)ho, n, np, bits_dev, seg, pshift);
         klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(257), dim3(kBlock), 0, s,
                 (const int32_t*)seg, np, ka);
-        const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr};
+        const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr, gp};
         klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
                 dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, (int32_t*)nullptr,
                 (uint32_t*)nullptr,
@@ -1030,7 +1077,8 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     const int32_t* vin = nullptr;  // the first pass generates the identity
     uint32_t* kout = kb;
     int32_t* vout = jb;
-    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tseg};
+    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tseg,
+                         nullptr};
     const auto pass = [&](auto wtag, int shift) {
         constexpr int W = decltype(wtag)::value;
         StageTimer st(prof, s, "sort_bucket");
