@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void bin_kernel(const double* __restrict__ 
     const GridParams g = *gp;
     const double a = x[i], b = y[i];
     if (g.nparts == 0) {  // the fit's own grid (the bucketed sort's MSD pass bins the same way)
-        key[i] = grid_key(a, b, g);
+        key[i] = grid_key(a, b, g.xmin2, g.ymin2, g.invx, g.invy, g.nx, g.ny, g.ntx);
         return;
     }
     uint32_t k = kSentinelKey;

@@ -220,17 +220,21 @@ struct GridParams {
 // The sort key of a point on a fit's own grid (not batched): tile << 8 | cell-in-tile << 2 |
 // quadrant, the sentinel for a non-finite point.  bin_kernel and the bucketed sort's MSD pass
 // (which bins on the fly instead of reading bin_kernel's keys) share it.
-__device__ __forceinline__ uint32_t grid_key(double a, double b, const GridParams& g) {
+// (Scalars, not a GridParams reference: a reference to a kernel's local copy of the struct put
+// that copy in scratch memory, bin_kernel 0.035 -> 0.18 ms per 10^7 points.)
+__device__ __forceinline__ uint32_t grid_key(double a, double b, double xmin2, double ymin2,
+                                             double invx, double invy, uint32_t nx, uint32_t ny,
+                                             uint32_t ntx) {
     if (!__builtin_isfinite(a) || !__builtin_isfinite(b)) return kSentinelKey;
-    const double mx = 2.0 * (double)g.nx - 1.0, my = 2.0 * (double)g.ny - 1.0;
+    const double mx = 2.0 * (double)nx - 1.0, my = 2.0 * (double)ny - 1.0;
     // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
-    double fx = floor(2.0 * ((a * 0.5 - g.xmin2) * g.invx));
-    double fy = floor(2.0 * ((b * 0.5 - g.ymin2) * g.invy));
+    double fx = floor(2.0 * ((a * 0.5 - xmin2) * invx));
+    double fy = floor(2.0 * ((b * 0.5 - ymin2) * invy));
     fx = fx < 0 ? 0 : (fx > mx ? mx : fx);
     fy = fy < 0 ? 0 : (fy > my ? my : fy);
     const uint32_t qx = (uint32_t)fx, qy = (uint32_t)fy;
     const uint32_t cx = qx >> 1, cy = qy >> 1;
-    const uint32_t tile = (cy >> 3) * g.ntx + (cx >> 3);
+    const uint32_t tile = (cy >> 3) * ntx + (cx >> 3);
     const uint32_t local = ((cy & 7u) << 3) | (cx & 7u);
     return (tile << 8) | (local << 2) | ((qy & 1u) << 1) | (qx & 1u);
 }

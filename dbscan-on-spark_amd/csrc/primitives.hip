@@ -263,7 +263,9 @@ __global__ __launch_bounds__(kBlock) void msd_upsweep_xy_kernel(const double* __
 #pragma unroll
     for (int r = 0; r < kRItems; ++r) {
         const int64_t i = base + r * kBlock + threadIdx.x;
-        if (i < n) atomicAdd(&h[w][(grid_key(a[r], c[r], g) >> shift) & (RB - 1u)], 1u);
+        if (i < n)
+            atomicAdd(&h[w][(grid_key(a[r], c[r], g.xmin2, g.ymin2, g.invx, g.invy, g.nx, g.ny,
+                                      g.ntx) >> shift) & (RB - 1u)], 1u);
     }
     __syncthreads();
     for (int d = threadIdx.x; d < RB; d += kBlock) {
@@ -722,7 +724,10 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
         if constexpr (MODE == 1)
         {
             c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
-            if (valid) k = key ? key[i] : grid_key(c_r[r].x, c_r[r].y, *ex.gp);
+            if (valid)
+                k = key ? key[i]
+                        : grid_key(c_r[r].x, c_r[r].y, ex.gp->xmin2, ex.gp->ymin2, ex.gp->invx,
+                                   ex.gp->invy, ex.gp->nx, ex.gp->ny, ex.gp->ntx);
             z_r[r] = (valid && ex.zone) ? (uint32_t)ex.zone[i] |
                                               ((ex.shm && ex.shm[i]) ? 256u : 0u)
                                         : 0u;
