@@ -494,26 +494,59 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         // a root of p's set (possibly stale: it stays an ancestor of p, so a q whose parent it
         // is belongs to p's set already and needs neither a pair test nor a union)
         int rp = sm_find(par, p);
-        for_stencil(p, p + 1, [&](int q, float2 rq, int w) {
-            const uint32_t iq = info[q];
-            const bool cq = core[q] != 0;
-            int bit = 0;
-            if (quarters) {
-                const int qd = (int)((iq >> 13) & 3u);
-                bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
+        // the stencil walk of for_stencil with each batch's records, infos, core flags and
+        // parents loaded together (the walk is bound by dependent LDS reads: one round trip per
+        // batch instead of three per candidate).  A parent read before a union of this batch is
+        // still an ancestor of that candidate, so `parent == rp` still proves p's set.
+        const int c = (int)(info[p] & kCellMask);
+        const int cy = c / nx, cx = c - cy * nx;
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (only >= 0 && d != only) continue;
+            const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+            if (r < 0 || r >= ny) continue;
+            const int rb = r * nx;
+            const int e = cst[rb + x1 + 1];
+            const int b1 = x0 + 1 <= x1 ? (int)cst[rb + x0 + 1] : 0x7FFFFFFF;
+            const int b2 = x0 + 2 <= x1 ? (int)cst[rb + x0 + 2] : 0x7FFFFFFF;
+            const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
+            for (int q = max((int)cst[rb + x0], p + 1); q < e; q += kSmBatch) {
+                float2 rq[kSmBatch];
+                uint32_t iq[kSmBatch];
+                int pq[kSmBatch];
+                bool cq[kSmBatch];
+#pragma unroll
+                for (int u = 0; u < kSmBatch; ++u) {
+                    const int qq = min(q + u, e - 1);
+                    rq[u] = rec[qq];
+                    iq[u] = info[qq];
+                    cq[u] = core[qq] != 0;
+                    pq[u] = sm_ld(par + qq);
+                }
+#pragma unroll
+                for (int u = 0; u < kSmBatch; ++u) {
+                    const int qq = q + u;
+                    if (qq >= e || !cq[u]) continue;
+                    int bit = 0;
+                    if (quarters) {
+                        const int w = wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0);
+                        const int qd = (int)((iq[u] >> 13) & 3u);
+                        bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
+                        if ((done >> bit) & 1ull) continue;
+                    }
+                    if (pq[u] == rp) {
+                        if (quarters) done |= 1ull << bit;
+                        continue;
+                    }
+                    if (pair(p, me, qq, rq[u])) {
+                        sm_unite(par, info, p, qq);
+                        rp = sm_find(par, p);
+                        if (quarters) done |= 1ull << bit;
+                    }
+                }
             }
-            if (!cq || ((done >> bit) & 1ull)) return true;
-            if (par[q] == rp) {
-                if (quarters) done |= 1ull << bit;
-                return true;
-            }
-            if (pair(p, me, q, rq)) {
-                sm_unite(par, info, p, q);
-                rp = sm_find(par, p);
-                if (quarters) done |= 1ull << bit;
-            }
-            return true;
-        }, only);
+        }
     }
     __syncthreads();
     SM_STAMP(4);
