@@ -3284,6 +3284,21 @@ __global__ __launch_bounds__(kBlock) void slab_map_kernel(int64_t n,
     flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
 }
 
+// slab_permute_kernel + slab_map_kernel in one pass (the finish of a prepared slab label):
+// each zone-0 point reads its packed label through to_packed (its sorted slot or padded place)
+// and maps its local root to the cluster id, so the packed labels are not copied to slab order
+// first (config 3's share at N = 1: 0.076 + 0.038 ms).
+__global__ __launch_bounds__(kBlock) void slab_map_packed_kernel(
+    int64_t n, const int32_t* __restrict__ to_packed, const uint32_t* __restrict__ packed,
+    const uint8_t* __restrict__ zone, const int32_t* __restrict__ label_of_root,
+    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || zone[i] != 0) return;
+    const uint32_t v = packed[to_packed[i]];
+    cluster_out[i] = v == 0 ? 0 : label_of_root[(v >> 1) - 1u];
+    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
+}
+
 // Slab fit, phase 1 output (multi-GPU node path): per sorted slot, the slab index of the
 // minimum-index core of its local component (lab) or -1 for a non-core, packed coalesced, then
 // moved to slab order through inv (one random read per point): root_out, core_out = root >= 0.
@@ -3494,6 +3509,12 @@ constexpr bool kCellQuarter = DBSCAN_AB_CQ != 0;
 #define DBSCAN_AB_BIN_MSD 1
 #endif
 constexpr bool kBinInMsd = DBSCAN_AB_BIN_MSD != 0;
+// Prepared slab labels: the finish maps the packed labels straight from their sorted slots (1)
+// or the prepare first copies them to slab order (0, A/B)
+#ifndef DBSCAN_AB_SLABMAP
+#define DBSCAN_AB_SLABMAP 1
+#endif
+constexpr bool kSlabMapPacked = DBSCAN_AB_SLABMAP != 0;
 #ifndef DBSCAN_AB_CAP32
 #define DBSCAN_AB_CAP32 1536
 #endif
@@ -4182,9 +4203,11 @@ void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
             static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
             (const uint64_t*)nullptr, (const int32_t*)nullptr, zone, gid, gs_of_root,
             (const int32_t*)nullptr, packed, st.place);
-    uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
-    klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-            st.to_packed, packed, zone, spacked);
+    if (!kSlabMapPacked) {
+        uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
+        klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+                st.n, st.to_packed, packed, zone, spacked);
+    }
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
@@ -4207,8 +4230,13 @@ void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const S
                 static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
                 gs_of_root, all_roots, n_roots, label_of_root);
     }
-    klaunch(prof, "slab_map", slab_map_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-            static_cast<const uint32_t*>(ws.spacked.p), zone, label_of_root, cluster, flag);
+    if (kSlabMapPacked)  // (the packed labels of the prepare, still in the workspace)
+        klaunch(prof, "slab_map", slab_map_packed_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
+                st.n, st.to_packed, static_cast<const uint32_t*>(ws.packed.p), zone,
+                label_of_root, cluster, flag);
+    else
+        klaunch(prof, "slab_map", slab_map_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
+                static_cast<const uint32_t*>(ws.spacked.p), zone, label_of_root, cluster, flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
