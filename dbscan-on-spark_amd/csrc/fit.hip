@@ -1239,7 +1239,6 @@ struct FuseArgs {
     uint8_t* tcore;          // out (f32): per tile, bit 0 its east cell column holds a core,
                              // bit 1 its south cell row does (edge_union skips the other sides)
     const int32_t* tpart = nullptr;  // batched fits: partition of each occupied tile
-    const int32_t* nq_p = nullptr;   // the occupied quarter count (device)
 };
 
 struct UnionLds {  // aliases the count's neighbour-list staging (the two never overlap in time)
@@ -2331,32 +2330,6 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
 // counts from global memory, spread over kBigChunks workgroups per tile (such tiles are the
 // dense cores of clusters: thousands of points each), then each tile's quarter union.
 constexpr int kBigChunks = 8;
-// big_count's lower bound over the quarters of a point's own cell (1) or its own quarter only
-// (0, A/B builds)
-#ifndef DBSCAN_AB_BIG_BOUND
-#define DBSCAN_AB_BIG_BOUND 1
-#endif
-constexpr bool kBigCellBound = DBSCAN_AB_BIG_BOUND != 0;
-
-// Is every point of quarter cell qk (a fit's own grid) within eps of (px, py) by the reference's
-// predicate?  The quarter's box from the grid (column gx spans x in [2*xmin2 + gx/invx,
-// + 1/invx), as bin_kernel bins), widened by a margin far above the binning's rounding (the
-// clique grid's extent is below 2^26 sides), its far corner's squared distance against
-// lim2 = eps2 * (1 - 2^-30): then fl(fl(dx)^2 + fl(dy)^2) <= eps2 for every point inside.
-__device__ __forceinline__ bool quarter_within(double px, double py, uint32_t qk,
-                                               const GridParams& g, double lim2) {
-    uint32_t cx, cy;
-    cell_xy(qk >> 2, g.ntx, cx, cy);
-    const double hx = 1.0 / g.invx, hy = 1.0 / g.invy;  // quarter sides
-    const double x0 = 2.0 * g.xmin2 + (double)(2u * cx + (qk & 1u)) * hx, x1 = x0 + hx;
-    const double y0 = 2.0 * g.ymin2 + (double)(2u * cy + ((qk >> 1) & 1u)) * hy, y1 = y0 + hy;
-    const double mx = hx * 0x1p-20 + (fabs(x0) + fabs(x1)) * 0x1p-40;
-    const double my = hy * 0x1p-20 + (fabs(y0) + fabs(y1)) * 0x1p-40;
-    const double dx = fmax(fabs(px - (x0 - mx)), fabs(px - (x1 + mx)));
-    const double dy = fmax(fabs(py - (y0 - my)), fabs(py - (y1 + my)));
-    return dx * dx + dy * dy <= lim2;
-}
-
 template <int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
@@ -2368,9 +2341,6 @@ __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
     __shared__ TileStage st;  // (unused by the global-memory count)
     int mine = 0;
     if (fa.gp->clique) {
-        const GridParams g = *fa.gp;
-        const int nparts = g.nparts, nq = fa.nq_p ? *fa.nq_p : 0;
-        const double lim2 = eps2 * (1.0 - 0x1p-30);
         const int nb = fa.tl.n[kTileBig];
         for (int k = blockIdx.x; k < nb * kBigChunks; k += gridDim.x) {
             const int t = fa.tl.big[k / kBigChunks], c = k % kBigChunks;
@@ -2380,23 +2350,7 @@ __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
                 // a quarter cell is a clique on these grids: one holding minPoints points makes
                 // each of them core without a count (a third of the big tiles' points at 10^7)
                 const int q = qidx[p];
-                int lb = fa.qstart[q + 1] - fa.qstart[q];  // a lower bound of |N(p)|
-                if (kBigCellBound && lb < min_points && nparts == 0) {
-                    // the other quarters of p's cell wholly within eps of p count too (the
-                    // quarters of one cell are adjacent in key order): decides most points of
-                    // a dense tile without a scan
-                    const uint32_t qk = fa.qkey[q];
-                    const double2 me = xy[p];
-#pragma unroll
-                    for (int o = -3; o <= 3; ++o) {
-                        const int q2 = q + o;
-                        if (o == 0 || q2 < 0 || q2 >= nq) continue;
-                        const uint32_t k2 = fa.qkey[q2];
-                        if ((k2 >> 2) != (qk >> 2)) continue;
-                        if (quarter_within(me.x, me.y, k2, g, lim2))
-                            lb += fa.qstart[q2 + 1] - fa.qstart[q2];
-                    }
-                }
+                const int lb = fa.qstart[q + 1] - fa.qstart[q];  // a lower bound of |N(p)|
                 const bool is_core =
                     (min_points <= 0 || lb >= min_points ||
                      count_point<false>(st, nullptr, xy, cell, seg, 0, 0, p, eps2, min_points,
@@ -3911,7 +3865,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 default: break;
             }
             const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp,
-                              tcore, tpart, &st[kStQuarters]};
+                              tcore, tpart};
             if (box) {
                 klaunch(prof, "box_count", box_count_kernel, dim3(tile_grid), dim3(kBlock), 0, s,
                         xy, cell, seg, nf_p, a.eps, eps2, a.min_points, core, parent,
