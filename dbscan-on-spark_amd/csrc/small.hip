@@ -167,6 +167,30 @@ __device__ void sm_unite(int* par, const uint32_t* info, int a, int b) {
     }
 }
 
+// sm_unite from ra, a (possibly stale) root of a's set: returns a root of the merged set at the
+// time of the hook (an ancestor of every member of both sets since), so the caller's next walk
+// starts from it instead of finding a's root again from a.
+__device__ int sm_unite_from(int* par, const uint32_t* info, int ra, int b) {
+    while (true) {
+        ra = sm_find(par, ra);
+        b = sm_find(par, b);
+        if (ra == b) return ra;
+        int hi = ra, lo = b;  // hi: the root with the larger visit index, hooked under lo
+        if ((info[ra] >> 16) < (info[b] >> 16)) {
+            hi = b;
+            lo = ra;
+        }
+        if (atomicCAS(par + hi, hi, lo) == hi) return lo;
+    }
+}
+
+// DBSCAN_AB_SMUNION: 0 unite from p and find p's root again; 1 unite from p's last root (the
+// default); 2 also skip a candidate whose grandparent is p's root (A/B builds)
+#ifndef DBSCAN_AB_SMUNION
+#define DBSCAN_AB_SMUNION 1
+#endif
+constexpr int kSmUnion = DBSCAN_AB_SMUNION;
+
 // The grid of one partition (one thread).  Sides as make_grid (fit.hip): >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500); doubled along the axis with more cells until nx*ny fits.
 __device__ void sm_make_grid(double xmin, double xmax, double ymin, double ymax, int nf,
@@ -535,13 +559,17 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
                         bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
                         if ((done >> bit) & 1ull) continue;
                     }
-                    if (pq[u] == rp) {
+                    if (pq[u] == rp || (kSmUnion >= 2 && sm_ld(par + pq[u]) == rp)) {
                         if (quarters) done |= 1ull << bit;
                         continue;
                     }
                     if (pair(p, me, qq, rq[u])) {
-                        sm_unite(par, info, p, qq);
-                        rp = sm_find(par, p);
+                        if (kSmUnion >= 1) {
+                            rp = sm_unite_from(par, info, rp, qq);
+                        } else {
+                            sm_unite(par, info, p, qq);
+                            rp = sm_find(par, p);
+                        }
                         if (quarters) done |= 1ull << bit;
                     }
                 }
