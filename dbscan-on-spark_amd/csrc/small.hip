@@ -190,6 +190,12 @@ __device__ int sm_unite_from(int* par, const uint32_t* info, int ra, int b) {
 #define DBSCAN_AB_SMUNION 1
 #endif
 constexpr int kSmUnion = DBSCAN_AB_SMUNION;
+// DBSCAN_AB_SMSKIP: the union walk marks the window's quarters beyond eps as done and skips the
+// rest of a cell whose four quarters are done (1, default) or visits every candidate (0, A/B)
+#ifndef DBSCAN_AB_SMSKIP
+#define DBSCAN_AB_SMSKIP 1
+#endif
+constexpr bool kSmSkip = DBSCAN_AB_SMSKIP != 0;
 
 // The grid of one partition (one thread).  Sides as make_grid (fit.hip): >= R*(1+2^-16) with
 // R = max(|eps|*(1+2^-40), 2^-500); doubled along the axis with more cells until nx*ny fits.
@@ -509,6 +515,9 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // within eps makes p unite with some core of q's quarter.  So a dense cell costs a few
     // unions per point instead of one per neighbour.
     const bool quarters = G.clique != 0;
+    // record -> cell-local coordinate: (v*0.5 - xmin2)*invx - cx = rec + (cx2 - xmin2)*invx - cx
+    // (clique grids: invx = invy = invs)
+    const double reach_kx = (G.cx2 - G.xmin2) * G.invx, reach_ky = (G.cy2 - G.ymin2) * G.invy;
     const int R = split ? 3 : 1;  // stencil rows per work item
     for (int it = tid; it < nf * R; it += kSmT) {
         const int p = split ? it / 3 : it, only = split ? it - 3 * (it / 3) : -1;
@@ -525,6 +534,24 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         const int c = (int)(info[p] & kCellMask);
         const int cy = c / nx, cx = c - cy * nx;
         const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+        if (kSmSkip && quarters && !exact_only) {
+            // quarters of the 6x6 window wholly beyond eps of p (their nearest point farther
+            // than the F threshold plus a margin over the fp32 records' error) count as done
+            const float tx = (float)((double)me.x + reach_kx - (double)cx);
+            const float ty = (float)((double)me.y + reach_ky - (double)cy);
+            const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
+            const float rr = (sqrtf(hi) + mg) * (sqrtf(hi) + mg);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const float y0 = 0.5f * (float)a - 1.0f, dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
+#pragma unroll
+                for (int b = 0; b < 6; ++b) {
+                    const float xb = 0.5f * (float)b - 1.0f;
+                    const float dx = fmaxf(0.0f, fmaxf(xb - tx, tx - (xb + 0.5f)));
+                    if (dx * dx + dy * dy > rr) done |= 1ull << (a * 6 + b);
+                }
+            }
+        }
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             if (only >= 0 && d != only) continue;
@@ -536,6 +563,16 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
             const int b2 = x0 + 2 <= x1 ? (int)cst[rb + x0 + 2] : 0x7FFFFFFF;
             const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
             for (int q = max((int)cst[rb + x0], p + 1); q < e; q += kSmBatch) {
+                if (kSmSkip && quarters) {
+                    // every quarter of q's cell done: the rest of the cell needs no visit
+                    const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
+                    const int sh = 2 * (w / 3) * 6 + 2 * (w % 3);
+                    const uint64_t m4 = (3ull << sh) | (3ull << (sh + 6));
+                    if ((done & m4) == m4) {
+                        q = min(q < b1 ? b1 : (q < b2 ? b2 : e), e) - kSmBatch;
+                        continue;
+                    }
+                }
                 float2 rq[kSmBatch];
                 uint32_t iq[kSmBatch];
                 int pq[kSmBatch];
