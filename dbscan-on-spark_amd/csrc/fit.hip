@@ -1633,12 +1633,6 @@ __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy
 #define DBSCAN_AB_SCAN_BATCH 4
 #endif
 constexpr int kScanBatch = DBSCAN_AB_SCAN_BATCH;
-// count_tile32: a short second round of own points split over two threads per point (1) or one
-// thread per point (0, A/B builds)
-#ifndef DBSCAN_AB_PAIR_TAIL
-#define DBSCAN_AB_PAIR_TAIL 1
-#endif
-constexpr bool kPairTail = DBSCAN_AB_PAIR_TAIL != 0;
 template <bool REC, int STRIDE = kBlock, class ExactF>
 __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
                                              float2 me, F32Cut cut, int min_points, int& cnt,
@@ -1926,112 +1920,68 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
             AB_STAMP(2);
             const int own = rowoff[8];
             AB_NOTE(11, own);
-            const bool counting = min_points > 0 && ablate != 1;
-            const int k_rec = ablate == 2 ? 0 : nbr_k;
-            // own point i -> its tile row r, column ex, LDS index j and sorted slot p
-            const auto locate = [&](int i, int& r, int& ex, int& j, int& p) {
-                r = 0;
+            for (int i = (int)threadIdx.x; i < own; i += kBlock) {
+                int r = 0;
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
                     if (r + s < 8 && rowoff[r + s] <= i) r += s;
                 const int base = (r + 1) * 10 + 1;
-                j = st.off[base] + (i - rowoff[r]);
-                ex = 0;
+                const int j = st.off[base] + (i - rowoff[r]);
+                int ex = 0;
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
-                p = st.cb[base + ex] + (j - st.off[base + ex]);
-            };
-            // the stencil scan of point (j, p): part -1 all of it (own cell first, then the
-            // rows ly, ly-1, ly+1), part 0 the own cell and the rest of row ly, part 1 the rows
-            // ly-1 and ly+1; early exit at minPoints of this part's own count
-            const auto scan = [&](int j, int p, int l, int part, int& cnt, int& nrec) {
-                const float2 me = buf[j];
-                const LdsRanges rg = lds_ranges(st, l);
-                const auto exact = [&](int q) {
-                    const double2 a = xy[p], o = xy[stage_slot(st, q)];
-                    return within_eps(a.x, a.y, o.x, o.y, eps2);
-                };
-                bool done = part == 1 ? false
-                                      : scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points,
-                                                           cnt, lst, nrec, k_rec, 0, exact);
+                const int p = st.cb[base + ex] + (j - st.off[base + ex]);
+                bool is_core = true;
+                if (min_points > 0 && ablate != 1) {
+                    const int l = r * 8 + ex;
+                    const float2 me = buf[j];
+                    const LdsRanges rg = lds_ranges(st, l);
+                    const auto exact = [&](int q) {
+                        const double2 a = xy[p], o = xy[stage_slot(st, q)];
+                        return within_eps(a.x, a.y, o.x, o.y, eps2);
+                    };
+                    int cnt = 0, nrec = 0;
+                    const int k_rec = ablate == 2 ? 0 : nbr_k;
+                    bool done = scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points, cnt,
+                                                   lst, nrec, k_rec, 0, exact);
 #pragma unroll
-                for (int k = 0; k < 3 && !done; ++k) {
-                    if ((part == 0 && k != 0) || (part == 1 && k == 0)) continue;
-                    const int lo = rg.b[k], hi = rg.e[k];
-                    if (lo <= rg.cs && rg.ce <= hi) {
-                        done = scan_count32<true>(buf, lo, rg.cs, me, cut, min_points, cnt, lst,
-                                                  nrec, k_rec, k, exact) ||
-                               scan_count32<true>(buf, rg.ce, hi, me, cut, min_points, cnt, lst,
-                                                  nrec, k_rec, k, exact);
-                    } else {
-                        done = scan_count32<true>(buf, lo, hi, me, cut, min_points, cnt, lst,
-                                                  nrec, k_rec, k, exact);
+                    for (int k = 0; k < 3 && !done; ++k) {
+                        const int lo = rg.b[k], hi = rg.e[k];
+                        if (lo <= rg.cs && rg.ce <= hi) {
+                            done = scan_count32<true>(buf, lo, rg.cs, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact) ||
+                                   scan_count32<true>(buf, rg.ce, hi, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact);
+                        } else {
+                            done = scan_count32<true>(buf, lo, hi, me, cut, min_points, cnt, lst,
+                                                      nrec, k_rec, k, exact);
+                        }
+                    }
+                    is_core = cnt >= min_points;
+                    if (!is_core && k_rec > 0) {  // (a complete list: cnt < minPoints)
+                        // the non-core's neighbours (self excluded), -1 terminated
+                        int32_t* out = nbr + (int64_t)p * nbr_k;
+                        int w = 0;
+                        for (int rr = 0; rr < nrec; ++rr) {
+                            const uint32_t v = lst[rr * kBlock];
+                            const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
+                            const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
+                            for (uint32_t m = v >> 16; m; m &= m - 1) {
+                                const int qq = q + __ffs(m) - 1;
+                                const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
+                                              (qq >= st.off[k0 + 2] ? 1 : 0);
+                                const int sq = st.cb[c] + (qq - st.off[c]);
+                                if (sq != p) out[w++] = sq;
+                            }
+                        }
+                        if (w < nbr_k) out[w] = -1;
                     }
                 }
-            };
-            // the non-core's neighbours (self excluded) from this thread's records, written from
-            // out[w]; returns the next index
-            const auto write_list = [&](int p, int r, int ex, int nrec, int w) {
-                int32_t* out = nbr + (int64_t)p * nbr_k;
-                for (int rr = 0; rr < nrec; ++rr) {
-                    const uint32_t v = lst[rr * kBlock];
-                    const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
-                    const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
-                    for (uint32_t m = v >> 16; m; m &= m - 1) {
-                        const int qq = q + __ffs(m) - 1;
-                        const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
-                                      (qq >= st.off[k0 + 2] ? 1 : 0);
-                        const int sq = st.cb[c] + (qq - st.off[c]);
-                        if (sq != p) out[w++] = sq;
-                    }
-                }
-                return w;
-            };
-            const auto finish = [&](int j, int p, bool is_core) {
                 if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
                 if (is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
-            };
-            // a second round of at most half a workgroup of points: two threads per point
-            // (adjacent lanes: the own cell and row, the rows above and below), so that the
-            // round's chain is half as long and the other half of the threads do not idle
-            const bool pair_tail = kPairTail && own > kBlock && own - kBlock <= kBlock / 2;
-            for (int i = (int)threadIdx.x; i < (pair_tail ? kBlock : own); i += kBlock) {
-                int r, ex, j, p;
-                locate(i, r, ex, j, p);
-                bool is_core = true;
-                if (counting) {
-                    int cnt = 0, nrec = 0;
-                    scan(j, p, r * 8 + ex, -1, cnt, nrec);
-                    is_core = cnt >= min_points;
-                    if (!is_core && k_rec > 0) {  // (a complete list: cnt < minPoints)
-                        const int w = write_list(p, r, ex, nrec, 0);
-                        if (w < nbr_k) nbr[(int64_t)p * nbr_k + w] = -1;
-                    }
-                }
-                finish(j, p, is_core);
-            }
-            if (pair_tail) {
-                const int i = kBlock + ((int)threadIdx.x >> 1), h = (int)threadIdx.x & 1;
-                const bool act = i < own;
-                int r = 0, ex = 0, j = 0, p = 0, cnt = 0, nrec = 0;
-                if (act) {
-                    locate(i, r, ex, j, p);
-                    if (counting) scan(j, p, r * 8 + ex, h, cnt, nrec);
-                }
-                const int other = __shfl_xor(cnt, 1, 64);  // (both lanes of every pair)
-                if (act) {
-                    const bool is_core = !counting || cnt + other >= min_points;
-                    if (!is_core && k_rec > 0) {
-                        // both parts are complete: part 0 (which holds self) writes its hits
-                        // first, part 1 after them and the terminator
-                        const int w = write_list(p, r, ex, nrec, h ? other - 1 : 0);
-                        if (h && w < nbr_k) nbr[(int64_t)p * nbr_k + w] = -1;
-                    }
-                    if (h == 0) finish(j, p, is_core);
-                }
             }
             AB_STAMP(3);
             __syncthreads();
