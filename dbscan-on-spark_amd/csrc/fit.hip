@@ -1861,7 +1861,7 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
 
 // Count + fused tile union on clique grids with the fp32 tile records above (the fp64
 // count_tile_kernel<.., true> runs the other grids; each exits at once on the other's).
-template <int CAP, int MINW, int NR = kMaxNbr>
+template <int CAP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
@@ -1878,8 +1878,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
     __shared__ float2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
     __shared__ int rowoff[9];
-    // NR neighbour records per thread (the host launches NR < kMaxNbr only for nbr_k <= NR)
-    __shared__ __attribute__((aligned(16))) uint32_t lsts[NR * kBlock];
+    __shared__ __attribute__((aligned(16))) uint32_t lsts[kMaxNbr * kBlock];
     __shared__ uint32_t lcore[(CAP + 31) / 32 + 1];
     static_assert(CAP < 2048, "LDS ranges are packed in 11 bits");
     static_assert(sizeof(UnionLds) <= sizeof(lsts), "UnionLds must fit");
@@ -3516,12 +3515,6 @@ constexpr bool kBinInMsd = DBSCAN_AB_BIN_MSD != 0;
 #define DBSCAN_AB_SLABMAP 1
 #endif
 constexpr bool kSlabMapPacked = DBSCAN_AB_SLABMAP != 0;
-// count_tile32 with 9 neighbour records per thread at 7 workgroups per CU when nbr_k <= 9 (1),
-// or always kMaxNbr records at 6 per CU (0, A/B builds)
-#ifndef DBSCAN_AB_NR9
-#define DBSCAN_AB_NR9 1
-#endif
-constexpr bool kCount32Nr9 = DBSCAN_AB_NR9 != 0;
 #ifndef DBSCAN_AB_CAP32
 #define DBSCAN_AB_CAP32 1536
 #endif
@@ -3915,11 +3908,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                                         (3 - used) * tile_grid * sizeof(int32_t), s));
                     }
                 }
-                // minPoints <= 10 (nbr_k <= 9, the reference's tests and the bench): 9 neighbour
-                // records per thread, 22.5 KB of LDS, 7 workgroups per CU
-                auto k32 = (kCount32Nr9 && nbr_k <= 9) ? count_tile32_kernel<kCap32, 7, 9>
-                           : union_w() == 5             ? count_tile32_kernel<kCap32, 5>
-                                                        : count_tile32_kernel<kCap32, 6>;
+                auto k32 =
+                    union_w() == 5 ? count_tile32_kernel<kCap32, 5> : count_tile32_kernel<kCap32, 6>;
                 klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
                         tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
                         block_cores, nbr, nbr_k, count_ablate(), fa);
