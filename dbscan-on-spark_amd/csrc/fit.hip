@@ -2668,11 +2668,6 @@ __global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
 // not yet joined in LDS.  A found edge is one global union of the two tile components, so the
 // global union-find sees about one operation per component pair per tile side.
 constexpr int kEdgeNodes = 72;
-// edge_union loads its nodes' records one node per lane (1) or per cell lane in turn (0, A/B)
-#ifndef DBSCAN_AB_EDGE_SPREAD
-#define DBSCAN_AB_EDGE_SPREAD 1
-#endif
-constexpr bool kEdgeSpread = DBSCAN_AB_EDGE_SPREAD != 0;
 
 // edge_union's full pair test (the reps were not within eps) and its global union.
 __device__ __forceinline__ bool edge_pair_full(const double2* __restrict__ xy, int4 me, int4 o,
@@ -2706,7 +2701,6 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     // facing nodes by position along the strip: facing cell f (0..7; the corner cell is f = 8
     // on side 0, f = -1 on side 1) holds nodes [fnb[f + 1], fne[f + 1])
     __shared__ int fnb[kBlock / 64][10], fne[kBlock / 64][10];
-    __shared__ int ncq0[kBlock / 64][17], ncs[kBlock / 64][17];  // per cell lane: first quarter, first node
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
@@ -2755,35 +2749,12 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                 fnb[w][f + 1] = incl - cnt;
                 fne[w][f + 1] = incl;
             }
-            if (kEdgeSpread) {
-                // the nodes' records loaded one node per lane (<= 72 nodes: two rounds at
-                // most) instead of each cell's lane walking its <= 4 quarters one after another
-                if (lane <= 16) {
-                    ncq0[w][lane] = q0;
-                    ncs[w][lane] = incl - cnt;
-                }
-                wave_sync();
-                for (int idx = lane; idx < ntot; idx += 64) {
-                    int c = 0;  // the cell (lane) holding node idx: last start <= idx
-#pragma unroll
-                    for (int s = 16; s > 0; s >>= 1)
-                        if (c + s <= 16 && ncs[w][c + s] <= idx) c += s;
-                    const int q = ncq0[w][c] + (idx - ncs[w][c]);
-                    const int4 qi = qinfo[q];
-                    const int4 gq = qg[q];
-                    const int cp = qcomp[q];
-                    nqi[w][idx] = qi;
-                    ngq[w][idx] = make_int2(gq.x, gq.y);
-                    ncomp[w][idx] = cp;  // tile component rep (a member of the set)
-                }
-            } else {
-                for (int j = 0; j < cnt; ++j) {
-                    const int idx = incl - cnt + j;
-                    nqi[w][idx] = qinfo[q0 + j];
-                    const int4 gq = qg[q0 + j];
-                    ngq[w][idx] = make_int2(gq.x, gq.y);
-                    ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
-                }
+            for (int j = 0; j < cnt; ++j) {
+                const int idx = incl - cnt + j;
+                nqi[w][idx] = qinfo[q0 + j];
+                const int4 gq = qg[q0 + j];
+                ngq[w][idx] = make_int2(gq.x, gq.y);
+                ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
             }
         }
         wave_sync();
