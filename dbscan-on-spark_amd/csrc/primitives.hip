@@ -581,15 +581,18 @@ __global__ __launch_bounds__(256) void bucket_table_kernel(const int32_t* __rest
 }
 
 // The pads: every padded slot no real key lands on gets the sentinel key.
+// Blocks 0..255: the pads after segment d's keys (< 2048 each); blocks 256.. share the tail after
+// the last segment (up to 256 tiles of 2048 keys: one block alone took ~29 us of every fit).
+constexpr int kPadTailBlocks = 64;
 __global__ __launch_bounds__(kBlock) void bucket_pad_kernel(const int32_t* __restrict__ seg,
                                                             int64_t np_max,
                                                             uint32_t* __restrict__ key) {
-    const int d = blockIdx.x;  // 0..256
+    const int d = blockIdx.x < 256 ? (int)blockIdx.x : 256;
     const int64_t a = (int64_t)seg[kSegPBase + d] + seg[kSegCnt + d];
     const int64_t b = d < 256 ? (int64_t)seg[kSegPBase + d + 1] : np_max;
-    for (int64_t j = a + threadIdx.x; j < b; j += kBlock) {
+    const int part = (int)blockIdx.x - d, parts = d < 256 ? 1 : kPadTailBlocks;
+    for (int64_t j = a + (int64_t)part * kBlock + threadIdx.x; j < b; j += (int64_t)parts * kBlock)
         key[j] = kSentinelKey;
-    }
 }
 
 // Per padded tile: (padded base - dense base of its segment, end of its real keys).
@@ -1064,7 +1067,7 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                 -1);
         klaunch(prof, "bucket_table", bucket_table_kernel, dim3(1), dim3(256), 0, s,
                 (const int32_t*)ho, n, np, bits_dev, seg, pshift);
-        klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(257), dim3(kBlock), 0, s,
+        klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(256 + kPadTailBlocks), dim3(kBlock), 0, s,
                 (const int32_t*)seg, np, ka);
         const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr, gp};
         klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),

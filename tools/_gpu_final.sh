@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out/fin
+VARIANTS="old main" ROUNDS=2 BENCH_ARGS="--steps 20 --warmup 5 --no-seam" bash tools/ab_bench.sh || exit 1
+grep -h -o '"bucket_pad": [0-9.]*' gpurun_out/ab/*.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/fin/gputest.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/fin/gputest.log; [ $rc -eq 0 ] || exit $rc
+TAG=round3_o bash tools/round_evidence.sh
