@@ -629,8 +629,19 @@ __global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __r
     const int64_t per = (t1 - t0 + G - 1) / G;
     const int64_t r0 = t0 + g * per < t1 ? t0 + g * per : t1;
     const int64_t r1 = r0 + per < t1 ? r0 + per : t1;
+    // the counts kOffBatch tiles at a time (their loads in flight together: a segment of
+    // config 5's share spans ~240 tiles, the tail segment up to 256)
+    constexpr int kOffBatch = 8;
     int agg = 0;
-    for (int64_t r = r0; r < r1; ++r) agg += cnt[r * RB + d];
+    int64_t r = r0;
+    for (; r + kOffBatch <= r1; r += kOffBatch) {
+        int v[kOffBatch];
+#pragma unroll
+        for (int u = 0; u < kOffBatch; ++u) v[u] = cnt[(r + u) * RB + d];
+#pragma unroll
+        for (int u = 0; u < kOffBatch; ++u) agg += v[u];
+    }
+    for (; r < r1; ++r) agg += cnt[r * RB + d];
     gsum[g][d] = agg;
     __syncthreads();
     if (g == 0) {  // the segment's digit totals, exclusive scan over the digits
@@ -645,7 +656,17 @@ __global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __r
     int run = seg[kSegPBase + s] + dex[d];
     for (int q = 0; q < (d >> 6); ++q) run += wsum[q];
     for (int q = 0; q < g; ++q) run += gsum[q][d];
-    for (int64_t r = r0; r < r1; ++r) {
+    for (r = r0; r + kOffBatch <= r1; r += kOffBatch) {
+        int v[kOffBatch];
+#pragma unroll
+        for (int u = 0; u < kOffBatch; ++u) v[u] = cnt[(r + u) * RB + d];
+#pragma unroll
+        for (int u = 0; u < kOffBatch; ++u) {
+            off[(r + u) * RB + d] = run;
+            run += v[u];
+        }
+    }
+    for (; r < r1; ++r) {
         const int c = cnt[r * RB + d];
         off[r * RB + d] = run;
         run += c;
