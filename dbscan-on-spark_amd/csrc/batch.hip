@@ -136,7 +136,11 @@ bool plan_batch_grid(const double* box, const int64_t* offs, int32_t n_parts, do
         widest = std::max(widest, tw[(size_t)p]);
         nf += (int64_t)b[4];
     }
-    if (nf == 0) return false;
+    if (nf == 0) {  // nothing to place: every partition (empty, all non-finite, sparse) alone
+        alone->clear();
+        for (int32_t p = 0; p < n_parts; ++p) alone->push_back(p);
+        return false;
+    }
     // shelves: rows of rectangles, a row as wide as the square root of the total area
     const int64_t W = std::max<int64_t>(widest, (int64_t)std::ceil(std::sqrt((double)area)));
     int64_t x = 0, y = 0, row_h = 0;

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
     const int32_t* __restrict__ offs,
     int32_t* __restrict__ cell, uint32_t* __restrict__ ckey, int32_t* __restrict__ cstart,
     int32_t* __restrict__ qidx, uint32_t* __restrict__ qkey, int32_t* __restrict__ qstart,
-    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart, int32_t* __restrict__ cq) {
+    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart) {
     __shared__ int wcnt[2][3][kBlock / 64];
     const int64_t nf = *nf_p;
     const int64_t base = (int64_t)blockIdx.x * kHeadTile;
@@ -445,7 +445,6 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
             if (h.c) {
                 ckey[ic] = k >> 2;
                 cstart[ic] = (int32_t)p;
-                if (cq) cq[ic] = iq;  // (a cell head heads a quarter)
             }
             if (qidx) {
                 qidx[p] = iq + h.q - 1;
@@ -461,7 +460,6 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
             if (p == nf - 1) {  // end sentinels
                 cstart[ic + h.c] = (int32_t)nf;
                 if (qidx) qstart[iq + h.q] = (int32_t)nf;
-                if (cq) cq[ic + h.c] = iq + h.q;
                 tstart[it + h.t] = (int32_t)nf;
             }
         }
@@ -488,9 +486,7 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
     const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ cell,
     const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
     const int32_t* __restrict__ ncells_p, const int32_t* __restrict__ qidx,
-    const int32_t* __restrict__ tmap, const GridParams* __restrict__ gp,
-    int32_t* __restrict__ tslot,
-    int32_t* __restrict__ tq, int4* __restrict__ tnb, const int32_t* __restrict__ cq) {
+    int32_t* __restrict__ tslot, int32_t* __restrict__ tq) {
     // one wave per tile, one lane per local cell
     const int lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
@@ -518,19 +514,10 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
         if (lane == 0) ts[64] = end;
         if (qidx) {
             int32_t* tqq = tq + (int64_t)t * kTslot;
-            // cq (heads_down): each cell's first quarter, cq[C] = Q, so the entry past the tile's
-            // last cell is the next tile's first quarter = qidx[end - 1] + 1; read next to
-            // cstart instead of gathering qidx at each cell's first slot
-            const int qend = cq ? cq[c0 + __popcll(occ)] : qidx[end - 1] + 1;
-            tqq[lane] = cq ? cq[c0 + rank] : (st < end ? qidx[st] : qend);
-            if (lane == 0) {
-                tqq[64] = qend;
-                const GridParams g = *gp;
-                const int ty = (int)(tk / g.ntx), tx = (int)(tk - (uint32_t)ty * g.ntx);
-                if (tnb)  // (else thalo_kernel writes it)
-                    tnb[t] = make_int4(tile_occ(tmap, g, tx + 1, ty), tile_occ(tmap, g, tx, ty + 1),
-                                   tile_occ(tmap, g, tx + 1, ty + 1), tile_occ(tmap, g, tx - 1, ty + 1));
-            }
+            // the entry past the tile's last cell is the next tile's first quarter
+            const int qend = qidx[end - 1] + 1;
+            tqq[lane] = st < end ? qidx[st] : qend;
+            if (lane == 0) tqq[64] = qend;
         }
     }
 }
@@ -605,54 +592,10 @@ struct TileStage {
 };
 
 // tstage[t][k] = (first slot, point count) of extended cell k of tile t: the staging table of
-// the per-tile kernels, so that staging a tile is one coalesced load per extended cell.  One
-// wave per tile (cells lane and lane + 64); tsz[t] = the stage's point count.
-__device__ __forceinline__ int2 tstage_entry(const GridParams& g, const int32_t* __restrict__ tmap,
-                                             const int32_t* __restrict__ tslot, int tx0,
-                                             int ty0, int k) {
-    const int ey = k / 10 - 1, ex = k % 10 - 1;
-    const int tx = tx0 + (ex < 0 ? -1 : (ex > 7 ? 1 : 0));
-    const int ty = ty0 + (ey < 0 ? -1 : (ey > 7 ? 1 : 0));
-    const int occ = tile_occ(tmap, g, tx, ty);
-    int b = 0, cnt = 0;
-    if (occ >= 0) {
-        const int l = (ey & 7) * 8 + (ex & 7);
-        b = tslot[(int64_t)occ * kTslot + l];
-        cnt = tslot[(int64_t)occ * kTslot + l + 1] - b;
-    }
-    return make_int2(b, cnt);
-}
-
-__global__ __launch_bounds__(kBlock) void tstage_kernel(const uint32_t* __restrict__ tkey,
-                                                        const int32_t* __restrict__ ntiles_p,
-                                                        const int32_t* __restrict__ tmap,
-                                                        const int32_t* __restrict__ tslot,
-                                                        const GridParams* __restrict__ gp,
-                                                        int2* __restrict__ tstage,
-                                                        int32_t* __restrict__ tsz) {
-    const int lane = threadIdx.x & 63;
-    const GridParams g = *gp;
-    const int ntiles = *ntiles_p;
-    for (int t = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t < ntiles;
-         t += gridDim.x * (kBlock / 64)) {
-        const uint32_t tk = tkey[t];
-        const int ty0 = (int)(tk / g.ntx), tx0 = (int)(tk - (uint32_t)ty0 * g.ntx);
-        const int2 e0 = tstage_entry(g, tmap, tslot, tx0, ty0, lane);
-        const int2 e1 = lane < 36 ? tstage_entry(g, tmap, tslot, tx0, ty0, 64 + lane)
-                                  : make_int2(0, 0);
-        tstage[(int64_t)t * 100 + lane] = e0;
-        if (lane < 36) tstage[(int64_t)t * 100 + 64 + lane] = e1;
-        int c = e0.y + e1.y;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) tsz[t] = c;
-    }
-}
-
-// tstage / tsz / tnb with more loads in flight per wave.  tstage_kernel walks the tiles one wave
-// per tile with a grid stride: at config 5's per-GPU share (1.46 M tiles, ~178 per resident
-// wave) each trip is a chain of 3 dependent loads (tile key -> neighbour's occupied index ->
-// its tslot row).
+// the per-tile kernels, so that staging a tile is one coalesced load per extended cell.
+// (One wave per tile with a grid stride was slower: at config 5's per-GPU share, 1.46 M tiles,
+// ~178 per resident wave, each trip a chain of 3 dependent loads: tile key -> neighbour's
+// occupied index -> its tslot row.)
 // thalo_kernel: the 100 staging entries of each tile (tstage_entry: the own tile's and the
 // neighbour tiles' tslot rows), tsz = their point count, and tnb (quarter grids).  One thread per
 // entry of kHaloTiles tiles per trip; each thread handles kHaloU trips' tiles with their loads
@@ -741,33 +684,15 @@ constexpr int kSmallCap = 192;
 // of capacity cap and its own counter.  Measured (round 2, 10^7 points): four small buckets
 // took count_wave from 0.127 to 0.094 ms; eight medium buckets slowed count_tile32 (0.308 ->
 // 0.316-0.331 ms: within a bucket the tiles lose the list's spatial order), so the medium tiles
-// stay one list in tile order (DBSCAN_AB_MED_BUCKETS: A/B builds).  Small-tile buckets hold
-// stage sizes (kSmallEdge[b + 1], kSmallEdge[b]]; count_wave_kernel runs in instances by lanes
-// per tile (kWaveSplit: 64 lanes above kTinyCap, 32 up to it; DBSCAN_AB_WAVE_SPLIT=3: 32 lanes up
-// to 64 points, measured even (10^7 0.092 -> 0.096 ms, config 3 share 0.254 -> 0.242); =2 also
-// 16 lanes up to 16 points).
-#ifndef DBSCAN_AB_MED_BUCKETS
-#define DBSCAN_AB_MED_BUCKETS 1
-#endif
-constexpr int kMedBuckets = DBSCAN_AB_MED_BUCKETS;
+// stay one list in tile order.  Small-tile buckets hold stage sizes (kSmallEdge[b + 1],
+// kSmallEdge[b]]; count_wave_kernel runs in two instances by lanes per tile: 64 lanes above
+// kTinyCap, 32 up to it (32 lanes up to 64 points measured even; 16 lanes up to 16 points no
+// gain).
+constexpr int kMedBuckets = 1;
 constexpr int kSmallBuckets = 5;
-#ifndef DBSCAN_AB_WAVE_SPLIT
-#define DBSCAN_AB_WAVE_SPLIT 1
-#endif
-constexpr int kWaveSplit = DBSCAN_AB_WAVE_SPLIT;  // 0: one instance; 1: 64 | 32; 2: 64 | 32 | 16
-#if DBSCAN_AB_WAVE_SPLIT == 2
-__device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 128, 64, 32, 16, 0};
-constexpr int kTinyCap = 64;     // the 32-lane instance: stages in (16, 64]
-constexpr int kTinyBucket0 = 2;  // its first bucket
-#elif DBSCAN_AB_WAVE_SPLIT == 3
-__device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 144, 96, 64, 32, 0};
-constexpr int kTinyCap = 64;     // the 32-lane instance: stages up to 64
-constexpr int kTinyBucket0 = 3;
-#else
 __device__ constexpr int kSmallEdge[kSmallBuckets + 1] = {kSmallCap, 144, 96, 64, 32, 0};
 constexpr int kTinyCap = 32;     // the 32-lane instance: stages up to 32
-constexpr int kTinyBucket0 = 4;
-#endif
+constexpr int kTinyBucket0 = 4;  // its first bucket
 static_assert(kSmallBuckets + kMedBuckets <= 16, "kStTileBuckets holds 16 counters");
 
 struct TileLists {
@@ -1230,7 +1155,6 @@ struct FuseArgs {
     const int32_t* perm;     // visit index per slot
     const uint32_t* tkey;    // occupied tile ids
     const GridParams* gp;
-    int f32;                 // clique grids are counted by count_tile32_kernel
     TileLists tl;            // f32: clique-grid tiles by stage size (tile_class_kernel)
     const uint8_t* zs;       // slab fits: zone per sorted slot (2: candidate only, never core)
     int4* qinfo;             // out: (begin, end, rep, core mask) per quarter
@@ -1288,27 +1212,21 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// b, e, key: this thread's quarter (threadIdx.x < nq), loaded before the count.
-template <bool STAGED>
-__device__ void fused_tile_union(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
-                                 const GridParams& g, const TileStage& st,
-                                 const double2* __restrict__ buf,
-                                 const uint32_t* __restrict__ lcore,
-                                 const double2* __restrict__ xy, const uint8_t* __restrict__ core,
-                                 double eps2, int32_t* __restrict__ parent, UnionLds& u,
-                                 int ablate) {
+// The tile-local quarter union of a big tile (big_union_kernel: its points are not staged, so
+// every range is a slot range and every core flag a global byte).  b, e, key: this thread's
+// quarter (threadIdx.x < nq).
+__device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, const FuseArgs& fa,
+                                  const GridParams& g, const double2* __restrict__ xy,
+                                  const uint8_t* __restrict__ core, double eps2,
+                                  int32_t* __restrict__ parent, UnionLds& u) {
     const int i = threadIdx.x;
-    const auto is_core = [&](int j) {  // j: LDS index (staged) or slot
-        if constexpr (STAGED) return ((lcore[j >> 5] >> (j & 31)) & 1u) != 0;
-        else return core[j] != 0;
-    };
+    const auto is_core = [&](int j) { return core[j] != 0; };
     u.qmap[i] = 0xFFFF;
     u.cmin[i] = ~0ull;
     lds_barrier();
-    // quarter records: quarter_init's rep and core mask.  The radix sort is stable and the
-    // visit index is the input index, so a quarter's slots are in visit order and its rep (the
-    // core with the smallest visit index) is simply its first core: one perm load, whose
-    // latency the pair tests below hide.
+    // quarter records: quarter rep and core mask.  The sort is stable and the visit index is the
+    // input index, so a quarter's slots are in visit order and its rep (the core with the
+    // smallest visit index) is simply its first core.
     int rep = -1, best = 0x7FFFFFFF, gx = 0, gy = 0;
     if (i < nq) {
         uint32_t cx, cy;
@@ -1317,74 +1235,47 @@ __device__ void fused_tile_union(int q0, int nq, int b, int e, uint32_t key, con
         gy = (int)(2 * cy + ((key >> 1) & 1u));
         const int lq = (gy & 15) * 16 + (gx & 15);
         const int len = e - b;
-        int jb = b;
-        if constexpr (STAGED) {
-            const int l = (int)((key >> 2) & 63u);
-            const int k = ((l >> 3) + 1) * 10 + (l & 7) + 1;
-            jb = st.off[k] + (b - st.cb[k]);
-        }
         uint32_t mask = 0;
         int first = -1;
-        if (STAGED && len <= 32) {  // the quarter's core bits straight from the bitmap
-            const int w = jb >> 5, o = jb & 31;
-            const uint64_t v = (uint64_t)lcore[w] | ((uint64_t)lcore[w + 1] << 32);
-            mask = (uint32_t)(v >> o) & (len == 32 ? ~0u : ((1u << len) - 1u));
-            first = mask ? __ffs(mask) - 1 : -1;
-        } else {
-            for (int j = 0; j < len && (j < 32 || first < 0); ++j)
-                if (is_core(jb + j)) {
-                    if (j < 32) mask |= 1u << j;
-                    if (first < 0) first = j;
-                }
-        }
+        for (int j = 0; j < len && (j < 32 || first < 0); ++j)
+            if (is_core(b + j)) {
+                if (j < 32) mask |= 1u << j;
+                if (first < 0) first = j;
+            }
         if (first >= 0) {
             rep = b + first;
             best = fa.perm[rep];
         }
         fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
         u.lp[i] = i;
-        u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) |
-                      (STAGED ? (uint32_t)jb | ((uint32_t)len << 11) : 0u);
+        u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22);
         u.lmask[i] = mask;
         u.qmap[lq] = (uint16_t)i;
     }
     lds_barrier();
-    // tile_union's pair tests, one (quarter, offset) item per thread, adjacent quarters first so
-    // that most distance-2 pairs are found joined and skipped
-    if (ablate != 3) {  // (ablate 3: time without the pair tests)
-        for (int sweep = 0; sweep < (ablate == 5 ? 1 : 2); ++sweep) {
-            const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
-            for (int k = i; k < nq * nofs; k += kBlock) {
-                const int o = k / nq, qi = k - o * nq;
-                const uint32_t ri = u.lrange[qi];
-                if (!(ri >> 31)) continue;
-                const int lq = (int)((ri >> 22) & 255u);
-                const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
-                if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
-                const int j = u.qmap[uy * 16 + ux];
-                if (j == 0xFFFF) continue;
-                const uint32_t rj = u.lrange[j];
-                if (!(rj >> 31)) continue;
-                // (adjacent items run all at once: a find before each would rarely prune)
-                if (sweep && ablate != 6 && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
-                int ab, ae, bb, be;
-                if constexpr (STAGED) {
-                    ab = (int)(ri & 2047u);
-                    ae = ab + (int)((ri >> 11) & 2047u);
-                    bb = (int)(rj & 2047u);
-                    be = bb + (int)((rj >> 11) & 2047u);
-                } else {
-                    ab = fa.qstart[q0 + qi];
-                    ae = fa.qstart[q0 + qi + 1];
-                    bb = fa.qstart[q0 + j];
-                    be = fa.qstart[q0 + j + 1];
-                }
-                if (quarters_touch(STAGED ? buf : xy, ab, ae, u.lmask[qi], bb, be, u.lmask[j],
-                                   is_core, eps2))
-                    lunite(u.lp, qi, j);
-            }
-            lds_barrier();
+    // pair tests, one (quarter, offset) item per thread, adjacent quarters first so that most
+    // distance-2 pairs are found joined and skipped
+    for (int sweep = 0; sweep < 2; ++sweep) {
+        const int o0 = sweep ? 4 : 0, nofs = sweep ? 8 : 4;
+        for (int k = i; k < nq * nofs; k += kBlock) {
+            const int o = k / nq, qi = k - o * nq;
+            const uint32_t ri = u.lrange[qi];
+            if (!(ri >> 31)) continue;
+            const int lq = (int)((ri >> 22) & 255u);
+            const int ux = (lq & 15) + kRingDx[o0 + o], uy = (lq >> 4) + kRingDy[o0 + o];
+            if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+            const int j = u.qmap[uy * 16 + ux];
+            if (j == 0xFFFF) continue;
+            const uint32_t rj = u.lrange[j];
+            if (!(rj >> 31)) continue;
+            // (adjacent items run all at once: a find before each would rarely prune)
+            if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+            const int ab = fa.qstart[q0 + qi], ae = fa.qstart[q0 + qi + 1];
+            const int bb = fa.qstart[q0 + j], be = fa.qstart[q0 + j + 1];
+            if (quarters_touch(xy, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, eps2))
+                lunite(u.lp, qi, j);
         }
+        lds_barrier();
     }
     // tile components: rep = the quarter rep with the smallest visit index
     int r = -1;
@@ -1401,54 +1292,34 @@ __device__ void fused_tile_union(int q0, int nq, int b, int e, uint32_t key, con
     }
 }
 
-// FUSE: also the tile-local quarter union (fused_tile_union) when the grid's quarter cells are
-// cliques; the parents are then written there, once.
-template <int CAP, int MINW, bool FUSE>
+// The fp64 count for grids whose quarter cells are not cliques of the predicate (grown cells;
+// the all-pairs grid): staged tiles count from LDS, the rest from global stencil pieces; every
+// point is its own parent for union_kernel.  Clique grids exit at once: the fp32 count kernels
+// (count_tile32 / count_wave / big_count) count them.
+template <int CAP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
     int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate,
-    FuseArgs fa) {
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k,
+    const GridParams* __restrict__ gp) {
     __shared__ TileStage st;
     __shared__ double2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
     __shared__ int rowoff[9];
     __shared__ __attribute__((aligned(16))) uint16_t lsts[kMaxNbr * kBlock];
-    __shared__ uint32_t lcore[FUSE ? (CAP + 31) / 32 + 1 : 1];  // core bits per LDS index
-    static_assert(!FUSE || CAP < 2048, "fused union packs LDS ranges in 11 bits");
     uint16_t* lst = lsts + threadIdx.x;
+    if (gp->clique) {
+        if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
+        return;
+    }
     const int ntiles = *ntiles_p;
     int mine = 0;
-    bool fuse = false;
-    GridParams g{};
-    if constexpr (FUSE) {
-        g = *fa.gp;
-        if (fa.f32 && g.clique && ablate != 4) {  // count_tile32_kernel + big_count_kernel's
-            if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
-            return;
-        }
-        fuse = g.clique != 0 && ablate != 4;  // (ablate 4: time the count alone)
-    }
-    const int32_t* tq = fuse ? fa.tq : nullptr;
-    StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart, tq);
+    StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart);
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        if (FUSE && threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
         const bool staged = stage_build<CAP>(meta, xy, st, buf);
-        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart, tq);  // in flight during the scans
-        // this thread's quarter record, in flight during the count (fused union)
-        int qb = 0, qe = 0, q0 = 0, nq = 0;
-        uint32_t qk = 0;
-        if (fuse) {
-            q0 = st.q0;
-            nq = st.nq;
-            if ((int)threadIdx.x < nq) {
-                qb = fa.qstart[q0 + threadIdx.x];
-                qe = fa.qstart[q0 + threadIdx.x + 1];
-                qk = fa.qkey[q0 + threadIdx.x];
-            }
-        }
+        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart);  // in flight during the scans
         if (staged) {
             if (threadIdx.x == 0) {  // own points per row of the tile: prefix over rows
                 int acc = 0;
@@ -1472,43 +1343,21 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
                 for (int s = 4; s > 0; s >>= 1)
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
-                bool is_core;
-                if (min_points <= 0) {
-                    is_core = true;
-                } else if (ablate == 1) {
-                    is_core = false;
-                } else {
-                    is_core = count_point<true>(st, buf, xy, cell, seg, j, r * 8 + ex, p, eps2,
-                                                min_points, lst, ablate == 2 ? nullptr : nbr,
-                                                nbr_k);
-                }
-                if (!fuse) parent[p] = p;
-                if (FUSE && is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
+                const bool is_core =
+                    min_points <= 0 || count_point<true>(st, buf, xy, cell, seg, j, r * 8 + ex, p,
+                                                         eps2, min_points, lst, nbr, nbr_k);
+                parent[p] = p;
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
-            }
-            if (fuse) {
-                __syncthreads();
-                fused_tile_union<true>(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, core, eps2,
-                                       parent, *reinterpret_cast<UnionLds*>(lsts), ablate);
             }
         } else {
             for (int p = st.ts + (int)threadIdx.x; p < st.te; p += kBlock) {
-                bool is_core;
-                if (min_points <= 0) {
-                    is_core = true;
-                } else {
-                    is_core = count_point<false>(st, buf, xy, cell, seg, 0, 0, p, eps2,
-                                                 min_points, lst, nbr, nbr_k);
-                }
-                if (!fuse) parent[p] = p;
+                const bool is_core =
+                    min_points <= 0 || count_point<false>(st, buf, xy, cell, seg, 0, 0, p, eps2,
+                                                          min_points, lst, nbr, nbr_k);
+                parent[p] = p;
                 core[p] = is_core ? 1 : 0;
                 mine += is_core ? 1 : 0;
-            }
-            if (fuse) {
-                __syncthreads();  // (workgroup scope: this block's core[] writes are visible)
-                fused_tile_union<false>(q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, core, eps2,
-                                        parent, *reinterpret_cast<UnionLds*>(lsts), ablate);
             }
         }
         __syncthreads();
@@ -1628,11 +1477,8 @@ __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy
 // minPoints has at most minPoints - 1 hits, so its records are complete.
 // Candidates per batch: 4, the batch's tail clamped and masked once (round 2: against 8 with
 // a per-candidate select, count_wave + count_tiny 0.092 -> 0.087 ms at 10^7, 0.256 -> 0.236
-// on config 3's share; 8 in this form spilled at 80 VGPRs).  DBSCAN_AB_SCAN_BATCH: A/B builds.
-#ifndef DBSCAN_AB_SCAN_BATCH
-#define DBSCAN_AB_SCAN_BATCH 4
-#endif
-constexpr int kScanBatch = DBSCAN_AB_SCAN_BATCH;
+// on config 3's share; 8 in this form spilled at 80 VGPRs).
+constexpr int kScanBatch = 4;
 template <bool REC, int STRIDE = kBlock, class ExactF>
 __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
                                              float2 me, F32Cut cut, int min_points, int& cnt,
@@ -1750,7 +1596,7 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
                                    const float2* __restrict__ buf,
                                    const uint32_t* __restrict__ lcore,
                                    const double2* __restrict__ xy, double eps2, F32Cut cut,
-                                   int32_t* __restrict__ parent, UnionLds& u, int ablate) {
+                                   int32_t* __restrict__ parent, UnionLds& u) {
     const int i = threadIdx.x;
     const auto is_core = [&](int j) { return ((lcore[j >> 5] >> (j & 31)) & 1u) != 0; };
     const auto exact = [&](int qa, int qb) {
@@ -1811,7 +1657,7 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
     lds_barrier();
     if (i == 0) fa.tcore[t] = (uint8_t)s_tflags;
     AB_STAMP(5);
-    if (ablate != 3) {
+    {
         // adjacent quarters (the 4 backward offsets) from each core quarter's own thread
         if (i < nq && rep >= 0)
             unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, i, buf, is_core, cut, exact);
@@ -1863,14 +1709,12 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
 // count_tile_kernel<.., true> runs the other grids; each exits at once on the other's).
 template <int CAP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ cell,
-    const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
+    const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
     int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, int ablate,
-    FuseArgs fa) {
+    int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k, FuseArgs fa) {
     const GridParams g = *fa.gp;
-    if (!g.clique || ablate == 4) {  // count_tile_kernel counts this grid
+    if (!g.clique) {  // count_tile_kernel counts this grid
         if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
         return;
     }
@@ -1933,7 +1777,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core = true;
-                if (min_points > 0 && ablate != 1) {
+                if (min_points > 0) {
                     const int l = r * 8 + ex;
                     const float2 me = buf[j];
                     const LdsRanges rg = lds_ranges(st, l);
@@ -1942,7 +1786,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                         return within_eps(a.x, a.y, o.x, o.y, eps2);
                     };
                     int cnt = 0, nrec = 0;
-                    const int k_rec = ablate == 2 ? 0 : nbr_k;
+                    const int k_rec = nbr_k;
                     bool done = scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points, cnt,
                                                    lst, nrec, k_rec, 0, exact);
 #pragma unroll
@@ -1987,7 +1831,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
             __syncthreads();
             AB_STAMP(4);
             fused_tile_union32(t, q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
-                               *reinterpret_cast<UnionLds*>(lsts), ablate);
+                               *reinterpret_cast<UnionLds*>(lsts));
         }
         __syncthreads();
         AB_STAMP(9);
@@ -2375,11 +2219,10 @@ __global__ __launch_bounds__(kBlock) void big_union_kernel(const double2* __rest
                                                            const uint8_t* __restrict__ core,
                                                            double eps2,
                                                            int32_t* __restrict__ parent,
-                                                           FuseArgs fa, int ablate) {
+                                                           FuseArgs fa) {
     const GridParams g = *fa.gp;
     if (!g.clique) return;
     __shared__ UnionLds u;
-    __shared__ TileStage st;  // (unused by the global-memory union)
     const int nb = fa.tl.n[kTileBig];
     for (int k = blockIdx.x; k < nb; k += gridDim.x) {
         const int t = fa.tl.big[k];
@@ -2391,8 +2234,7 @@ __global__ __launch_bounds__(kBlock) void big_union_kernel(const double2* __rest
             qe = fa.qstart[q0 + threadIdx.x + 1];
             qk = fa.qkey[q0 + threadIdx.x];
         }
-        fused_tile_union<false>(q0, nq, qb, qe, qk, fa, g, st, nullptr, nullptr, xy, core, eps2,
-                                parent, u, ablate);
+        global_tile_union(q0, nq, qb, qe, qk, fa, g, xy, core, eps2, parent, u);
         __syncthreads();
     }
 }
@@ -2550,120 +2392,13 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 // if their quarter-grid offsets are <= 2 (inside the 3x3 eps-cell stencil); ONE core-core
 // edge per such pair suffices.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void quarter_init_kernel(
-    const int32_t* __restrict__ qstart, const uint32_t* __restrict__ qkey,
-    const int32_t* __restrict__ nq_p, const GridParams* __restrict__ gp,
-    const int32_t* __restrict__ perm,
-    const uint8_t* __restrict__ core, int4* __restrict__ qinfo, int4* __restrict__ qg,
-    int32_t* __restrict__ parent) {
-    if (!gp->clique) return;
-    const int q = blockIdx.x * kBlock + threadIdx.x;
-    if (q >= *nq_p) return;
-    const GridParams g = *gp;
-    const int b = qstart[q], e = qstart[q + 1];
-    int rep = -1, best = 0x7FFFFFFF;
-    uint32_t mask = 0;  // cores among the first 32 slots (quarters rarely hold more)
-    for (int j = b; j < e; ++j)
-        if (core[j]) {
-            if (j - b < 32) mask |= 1u << (j - b);
-            if (perm[j] < best) {
-                best = perm[j];
-                rep = j;
-            }
-        }
-    const uint32_t k = qkey[q];
-    uint32_t cx, cy;
-    cell_xy(k >> 2, g.ntx, cx, cy);
-    qinfo[q] = make_int4(b, e, rep, (int)mask);
-    qg[q] = make_int4((int)(2 * cx + (k & 1u)), (int)(2 * cy + ((k >> 1) & 1u)),
-                      rep >= 0 ? best : 0x7FFFFFFF, 0);
-    if (rep < 0) return;
-    for (int j = b; j < e; ++j)
-        if (core[j]) parent[j] = rep;
-}
-
-// One tile per loop trip: quarter records and their quarter-grid neighbours in LDS, the
-// pair tests read the (L2-resident) coordinates directly -- staging them measured slower
-// (fewer resident workgroups; tools/tile_variants.sh, r02).
-template <int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void tile_union_kernel(
-    const double2* __restrict__ xy, const int32_t* __restrict__ tq,
-    const int32_t* __restrict__ ntiles_p, const int4* __restrict__ qinfo,
-    const int4* __restrict__ qg, double eps2, const int32_t* __restrict__ perm,
-    const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    int32_t* __restrict__ qcomp, const GridParams* __restrict__ gp) {
-    if (!gp->clique) return;
-    __shared__ int lp[kMaxTileQ];
-    __shared__ int4 lqi[kMaxTileQ];
-    __shared__ int qmap[kMaxTileQ];  // 16x16 local quarter grid -> local quarter index
-    __shared__ int cmin[kMaxTileQ];
-    __shared__ int crep[kMaxTileQ];
-    const int ntiles = *ntiles_p;
-    const int i = threadIdx.x;
-    const auto gcore = [core](int j) { return core[j] != 0; };
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int q0 = tq[(int64_t)t * kTslot], nq = tq[(int64_t)t * kTslot + 64] - q0;
-        qmap[i] = -1;
-        cmin[i] = 0x7FFFFFFF;
-        __syncthreads();
-        int lqx = 0, lqy = 0, prio = 0x7FFFFFFF;
-        int4 me = make_int4(0, 0, -1, 0);
-        if (i < nq) {
-            me = qinfo[q0 + i];
-            const int4 gq = qg[q0 + i];
-            lqx = gq.x & 15;
-            lqy = gq.y & 15;
-            prio = gq.z;
-            lqi[i] = me;
-            lp[i] = i;
-            qmap[lqy * 16 + lqx] = i;
-        }
-        __syncthreads();
-        if (i < nq && me.z >= 0) {
-            double px[kQReg], py[kQReg];
-            const int na = load_own(xy, me, 0, px, py);
-            // adjacent quarters first (merges happen early), then the distance-2 ring
-#pragma unroll
-            for (int sweep = 1; sweep <= 2; ++sweep)
-                for (int dy = -2; dy <= 2; ++dy)
-                    for (int dx = -2; dx <= 2; ++dx) {
-                        if (max(abs(dx), abs(dy)) != sweep) continue;
-                        const int ux = lqx + dx, uy = lqy + dy;
-                        if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
-                        const int j = qmap[uy * 16 + ux];
-                        if (j < 0 || j >= i) continue;  // each pair once, from the larger index
-                        const int4 o = lqi[j];
-                        if (o.z < 0) continue;
-                        if (lfind(lp, i) == lfind(lp, j)) continue;
-                        const bool f = na >= 0 ? pair_found(px, py, na, xy, o.x, o.y,
-                                                            (uint32_t)o.w, gcore, 0, eps2)
-                                               : pair_found_generic(xy, 0, me, o, gcore, eps2);
-                        if (f) lunite(lp, i, j);
-                    }
-        }
-        __syncthreads();
-        int r = -1;
-        if (i < nq && me.z >= 0) {
-            r = lfind(lp, i);
-            atomicMin(&cmin[r], prio);
-        }
-        __syncthreads();
-        if (r >= 0 && prio == cmin[r]) crep[r] = me.z;
-        __syncthreads();
-        // quarter reps (roots after quarter_init) now point at their tile component's rep
-        if (r >= 0 && crep[r] != me.z) parent[me.z] = crep[r];
-        if (i < nq) qcomp[q0 + i] = r >= 0 ? crep[r] : -1;
-        __syncthreads();
-    }
-}
-
 // Quarter pairs that cross a tile edge.  One wave per (tile, side), each wave looping on its
 // own (no block barriers): side 0 pairs the tile's
 // east cell column with the E tile's west column plus the SE tile's corner cell; side 1 its
 // south row with the S tile's north row plus the SW tile's corner cell.  With the mirrored
 // sides of the other tiles, every pair of adjacent cells in different tiles is covered once.
 // The wave loads the quarter cells of the facing strips (<= 32 + 36) into LDS, tags each with
-// its tile component (qcomp, from tile_union), pre-joins equal tags in an LDS union-find, then
+// its tile component (qcomp, from the count kernels' tile unions), pre-joins equal tags in an LDS union-find, then
 // pair-tests facing quarters within quarter distance 2 (adjacent first) only while the two are
 // not yet joined in LDS.  A found edge is one global union of the two tile components, so the
 // global union-find sees about one operation per component pair per tile side.
@@ -3257,37 +2992,10 @@ __global__ __launch_bounds__(kBlock) void box_label_kernel(
     packed[place ? place[p] : p] = v;  // (bucketed sort: at the slot's padded place)
 }
 
-// Two-part slab label (dbscan_slab_roots_prepare_device + dbscan_slab_label_finish_device_async):
-// the ROOTS-packed labels moved to slab order before the roots are numbered (zone 1/2 entries
-// 0), so the part that waits for the numbering is one coalesced pass.
-__global__ __launch_bounds__(kBlock) void slab_permute_kernel(int64_t n,
-                                                              const int32_t* __restrict__ inv,
-                                                              const uint32_t* __restrict__ packed,
-                                                              const uint8_t* __restrict__ zone,
-                                                              uint32_t* __restrict__ spacked) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    spacked[i] = zone[i] == 0 ? packed[inv[i]] : 0u;
-}
-
-// Slab order: cluster = label_of_root[root], flag Core / Border / Noise as permute_out_kernel.
-__global__ __launch_bounds__(kBlock) void slab_map_kernel(int64_t n,
-                                                          const uint32_t* __restrict__ spacked,
-                                                          const uint8_t* __restrict__ zone,
-                                                          const int32_t* __restrict__ label_of_root,
-                                                          int32_t* __restrict__ cluster_out,
-                                                          uint8_t* __restrict__ flag_out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n || zone[i] != 0) return;
-    const uint32_t v = spacked[i];
-    cluster_out[i] = v == 0 ? 0 : label_of_root[(v >> 1) - 1u];
-    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
-}
-
-// slab_permute_kernel + slab_map_kernel in one pass (the finish of a prepared slab label):
-// each zone-0 point reads its packed label through to_packed (its sorted slot or padded place)
-// and maps its local root to the cluster id, so the packed labels are not copied to slab order
-// first (config 3's share at N = 1: 0.076 + 0.038 ms).
+// The finish of a prepared slab label: each zone-0 point reads its packed label through
+// to_packed (its sorted slot or padded place) and maps its local root to the cluster id
+// (label_of_root), flag Core / Border / Noise as permute_out_kernel.  (Copying the packed
+// labels to slab order first and mapping them there cost 0.076 + 0.038 ms on config 3's share.)
 __global__ __launch_bounds__(kBlock) void slab_map_packed_kernel(
     int64_t n, const int32_t* __restrict__ to_packed, const uint32_t* __restrict__ packed,
     const uint8_t* __restrict__ zone, const int32_t* __restrict__ label_of_root,
@@ -3455,70 +3163,10 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 // Host orchestration
 // ---------------------------------------------------------------------------------------
 
-// A/B experiment options.  They are COMPILE-TIME only (-D on the hipcc line of an A/B build
-// loaded through DBSCAN_LIB_PATH, tools/build_ab.sh): no environment variable can change what
-// the shipped library computes.  The product build uses the defaults below.
-// DBSCAN_AB_COUNT_CAP: LDS staging capacity of the fp64 count pass (2048 or 1024 instead of
-//   1536; results identical for every choice).
-// DBSCAN_AB_COUNT_ABLATE (timing experiments only; results are WRONG): 1 = staging only, no
-//   neighbour scans; 2 = scans without neighbour lists; 4 = count32 returns at once.
-// DBSCAN_AB_UNION_W: register budget (waves/SIMD) of the tile/edge union kernels, 6 by default
-//   (tile_union 88 -> 78 VGPRs, edge_union 100 -> 80: blobs 0.35 / 0.31 -> 0.31 / 0.23 ms;
-//   8 spills and is slower, tools/union_w_sweep.sh, r05); 5 and 7 for measurements.
-// DBSCAN_AB_F32=0: count clique grids with the fp64 staging.
-// DBSCAN_AB_FUSE=0: run quarter_init and tile_union as their own kernels.
-// DBSCAN_AB_TINY_W: waves per SIMD of the packed count_wave instances.
-#ifndef DBSCAN_AB_TINY_W
-#define DBSCAN_AB_TINY_W 5
-#endif
-static constexpr int kTinyWaves = DBSCAN_AB_TINY_W;
-#ifndef DBSCAN_AB_COUNT_ABLATE
-#define DBSCAN_AB_COUNT_ABLATE 0
-#endif
-#ifndef DBSCAN_AB_UNION_W
-#define DBSCAN_AB_UNION_W 0
-#endif
-#ifndef DBSCAN_AB_COUNT_CAP
-#define DBSCAN_AB_COUNT_CAP 0
-#endif
-#ifndef DBSCAN_AB_F32
-#define DBSCAN_AB_F32 1
-#endif
-#ifndef DBSCAN_AB_FUSE
-#define DBSCAN_AB_FUSE 1
-#endif
-static constexpr int count_ablate() { return DBSCAN_AB_COUNT_ABLATE; }
-static constexpr int union_w() { return DBSCAN_AB_UNION_W; }
-static constexpr int count_cap() { return DBSCAN_AB_COUNT_CAP; }
-static constexpr bool f32_count() { return DBSCAN_AB_F32 != 0; }
-static constexpr bool fuse_union() { return DBSCAN_AB_FUSE != 0; }
-// DBSCAN_AB_CAP32: staging capacity of count_tile32 (tiles over it take the big-tile path)
-// Staging tables by thalo_kernel (1) or tstage_kernel (0, A/B builds)
-#ifndef DBSCAN_AB_TABLES
-#define DBSCAN_AB_TABLES 1
-#endif
-constexpr bool kTablesHalo = DBSCAN_AB_TABLES != 0;
-// tslot_kernel's quarter table from a per-cell first-quarter array written by heads_down (1) or
-// by gathering qidx at each cell's first slot (0, A/B builds)
-#ifndef DBSCAN_AB_CQ
-#define DBSCAN_AB_CQ 0
-#endif
-constexpr bool kCellQuarter = DBSCAN_AB_CQ != 0;
-// Bucketed sort: the MSD pass bins the points itself (1) or reads bin_kernel's keys (0, A/B)
-#ifndef DBSCAN_AB_BIN_MSD
-#define DBSCAN_AB_BIN_MSD 1
-#endif
-constexpr bool kBinInMsd = DBSCAN_AB_BIN_MSD != 0;
-// Prepared slab labels: the finish maps the packed labels straight from their sorted slots (1)
-// or the prepare first copies them to slab order (0, A/B)
-#ifndef DBSCAN_AB_SLABMAP
-#define DBSCAN_AB_SLABMAP 1
-#endif
-constexpr bool kSlabMapPacked = DBSCAN_AB_SLABMAP != 0;
-#ifndef DBSCAN_AB_CAP32
-#define DBSCAN_AB_CAP32 1536
-#endif
-constexpr int kCap32 = DBSCAN_AB_CAP32;
+// Waves per SIMD of the packed count_wave instance (count_tiny) and the staging capacity of
+// count_tile32 (tiles over it take the big-tile path; 1024 / 1280 / 1792 measured slower).
+static constexpr int kTinyWaves = 5;
+constexpr int kCap32 = 1536;
 
 // Archery float32 box, after the rank scan: the one-way core-core pairs decide which component
 // a cluster's expansion claims beyond its own.  Usually there are none (returns nullptr: the
@@ -3662,7 +3310,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "grid", grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
-        if (!bucketed || !kBinInMsd) {
+        if (!bucketed) {  // (bucketed: the MSD pass bins x, y itself)
             StageTimer t(prof, s, "bin");
             klaunch(prof, "bin", bin_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, a.x, a.y, n, gp, key);
             DBSCAN_HIP_CHECK(hipGetLastError());
@@ -3675,7 +3323,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "shared_mark", shared_mark_kernel, dim3(nblk(a.n_shared)),
                         dim3(kBlock), 0, s, a.n_shared, a.shared_idx, shm);
             }
-            bucket_sort(s, a.x, a.y, kBinInMsd ? nullptr : key, n, &st[kStBits], ws.bucket,
+            bucket_sort(s, a.x, a.y, nullptr, n, &st[kStBits], ws.bucket,
                         ws.hist, ws.scan, prof, a.zone, shm, gp);
             key = ws.bucket.key_fin;  // (perm: written by scatter_bucket_kernel below)
         } else {
@@ -3718,9 +3366,6 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* qidx = static_cast<int32_t*>(ws.qidx.ensure(n * sizeof(int32_t)));
     uint32_t* qkey = static_cast<uint32_t*>(ws.qkey.ensure(n * sizeof(uint32_t)));
     int32_t* qstart = static_cast<int32_t*>(ws.qstart.ensure((n + 1) * sizeof(int32_t)));
-    // each cell's first quarter (+ the quarter count), for tslot_kernel's quarter table
-    int32_t* cq = kCellQuarter ? static_cast<int32_t*>(ws.cq.ensure((n + 1) * sizeof(int32_t)))
-                               : nullptr;
     int4* qinfo = static_cast<int4*>(ws.qrep.ensure(n * sizeof(int4)));
     int4* qg = static_cast<int4*>(ws.qmask.ensure(n * sizeof(int4)));
     // the tile-local quarter union runs inside the count kernels (slab fits: the fp32 count
@@ -3728,13 +3373,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     // archery's float32 search box (mode 2): its own count / union / label kernels over the
     // global stencil pieces; none of the clique-quarter or fp32-record paths
     const bool box = a.mode == kModeArcheryBox;
-    const bool fuse = !box && mode == kGridEps && fuse_union() && count_cap() == 0 &&
-                      (!a.zone || f32_count());
+    const bool fuse = !box && mode == kGridEps;
     uint8_t* zs =
         (a.zone && (fuse || bucketed)) ? static_cast<uint8_t*>(ws.zs.ensure(n)) : nullptr;
-    // clique grids: the fp32-record count kernels by tile class (tile_class_kernel);
-    // DBSCAN_F32=0 keeps the fp64 count_tile_kernel for A/B measurements
-    const bool f32 = mode != kGridNoPairs && fuse && f32_count() && count_cap() == 0;
+    // eps grids: the fp32-record count kernels by tile class (tile_class_kernel) when the
+    // grid's quarter cells are cliques, count_tile_kernel (fp64) when not
+    const bool f32 = fuse;
     const int nbr_k =
         (!box && a.min_points >= 2 && a.min_points - 1 <= kMaxNbr) ? a.min_points - 1 : 0;
     TileLists tl{};
@@ -3790,7 +3434,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan);
             exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
-                    offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart, cq);
+                    offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
             if (tpart)
                 klaunch(prof, "tile_part", tile_part_kernel, dim3(nblk(ntile_bound)),
@@ -3803,30 +3447,16 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            if (kTablesHalo) {  // (tnb: thalo_kernel)
-                klaunch(prof, "tslot", tslot_kernel,
-                        dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
-                        dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
-                        &st[kStCells], qidx, tmap, gp, tslot, tq, (int4*)nullptr, cq);
-                DBSCAN_HIP_CHECK(hipGetLastError());
-                klaunch(prof, "tstage", thalo_kernel,
-                        dim3((unsigned)std::min<int64_t>(
-                            (ntile_bound + kHaloTiles * kHaloU - 1) / (kHaloTiles * kHaloU),
-                            kTileGrid)),
-                        dim3(kBlock), 0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz,
-                        qidx ? tnb : nullptr);
-                DBSCAN_HIP_CHECK(hipGetLastError());
-            } else {
-                klaunch(prof, "tslot", tslot_kernel,
-                        dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
-                        dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
-                        &st[kStCells], qidx, tmap, gp, tslot, tq, tnb, cq);
-                DBSCAN_HIP_CHECK(hipGetLastError());
-                klaunch(prof, "tstage", tstage_kernel,
-                        dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
-                        dim3(kBlock), 0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz);
-                DBSCAN_HIP_CHECK(hipGetLastError());
-            }
+            klaunch(prof, "tslot", tslot_kernel,
+                    dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
+                    dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
+                    &st[kStCells], qidx, tslot, tq);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+            klaunch(prof, "tstage", thalo_kernel,
+                    dim3((unsigned)std::min<int64_t>(
+                        (ntile_bound + kHaloTiles * kHaloU - 1) / (kHaloTiles * kHaloU), kTileGrid)),
+                    dim3(kBlock), 0, s, tkey, &st[kStTiles], tmap, tslot, gp, tstage, tsz, tnb);
+            DBSCAN_HIP_CHECK(hipGetLastError());
             if (f32)  // clique grids: small / medium / big tile lists
                 klaunch(prof, "tile_class", tile_class_kernel<kCap32>,
                         dim3((unsigned)std::min<int64_t>(
@@ -3858,75 +3488,44 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     {
         StageTimer t(prof, s, "count");
         if (mode != kGridNoPairs) {
-            auto kern = fuse ? count_tile_kernel<1536, 5, true> : count_tile_kernel<1536, 5, false>;
-            switch (count_cap()) {
-                case 2048: kern = count_tile_kernel<2048, 1, false>; break;
-                case 1024: kern = count_tile_kernel<1024, 5, false>; break;
-                default: break;
-            }
-            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, f32 ? 1 : 0, tl, zs, qinfo, qg, qcomp,
-                              tcore, tpart};
+            const FuseArgs fa{tq, qstart, qkey, perm, tkey, gp, tl, zs, qinfo, qg, qcomp, tcore,
+                              tpart};
             if (box) {
                 klaunch(prof, "box_count", box_count_kernel, dim3(tile_grid), dim3(kBlock), 0, s,
                         xy, cell, seg, nf_p, a.eps, eps2, a.min_points, core, parent,
                         block_cores);
             } else if (f32) {
-                // clique grids by tile stage size: small tiles one wave each (count_wave),
+                // clique grids by tile stage size: small tiles one wave each (count_wave: 64
+                // lanes per tile over kTinyCap points; count_tiny: tiles packed 2 to a wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
-                // big_union); other grids: count (fp64)
-                // small tiles: 64 lanes per tile over kTinyCap points, then tiles packed 2 (and
-                // 4) to a wave
-                {
-                    int32_t* bc = block_cores + 3 * tile_grid;
-                    if constexpr (kWaveSplit == 0)
-                        klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kSmallBuckets>,
-                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                                a.min_points, core, parent, bc, nbr, nbr_k, fa);
-                    else
-                        klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0>,
-                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                                a.min_points, core, parent, bc, nbr, nbr_k, fa);
-                    if constexpr (kWaveSplit == 1 || kWaveSplit == 3)
-                        klaunch(prof, "count_tiny",
-                                count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0,
-                                                  kSmallBuckets - kTinyBucket0>,
-                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                                a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
-                    if constexpr (kWaveSplit == 2) {
-                        klaunch(prof, "count_tiny",
-                                count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0, 2>,
-                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                                a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
-                        klaunch(prof, "count_tiny16",
-                                count_wave_kernel<kTinyWaves, 16, 16, kTinyBucket0 + 2, 1>,
-                                dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                                a.min_points, core, parent, bc + 2 * tile_grid, nbr, nbr_k, fa);
-                    }
-                    if constexpr (kWaveSplit != 2) {
-                        constexpr int used = kWaveSplit == 0 ? 1 : 2;
-                        DBSCAN_HIP_CHECK(hipMemsetAsync(bc + used * tile_grid, 0,
-                                                        (3 - used) * tile_grid * sizeof(int32_t), s));
-                    }
-                }
-                auto k32 =
-                    union_w() == 5 ? count_tile32_kernel<kCap32, 5> : count_tile32_kernel<kCap32, 6>;
-                klaunch(prof, "count32", k32, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
-                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
-                        block_cores, nbr, nbr_k, count_ablate(), fa);
+                // big_union); other eps grids: count (fp64, exits at once on clique grids)
+                int32_t* bc = block_cores + 3 * tile_grid;
+                klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0>,
+                        dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                        a.min_points, core, parent, bc, nbr, nbr_k, fa);
+                klaunch(prof, "count_tiny",
+                        count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0,
+                                          kSmallBuckets - kTinyBucket0>,
+                        dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                        a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
+                DBSCAN_HIP_CHECK(hipMemsetAsync(bc + 2 * tile_grid, 0, tile_grid * sizeof(int32_t), s));
+                klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
+                        dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
+                        a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
                 klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,
                         s, xy, cell, seg, tstart, qidx, eps2, a.min_points, core,
                         block_cores + tile_grid, nbr, nbr_k, fa);
                 // one workgroup per big tile up to kTileGrid (a grid of 2048 gave the tiles past
                 // it a second serial turn)
                 klaunch(prof, "big_union", big_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
-                        (const uint8_t*)core, eps2, parent, fa, count_ablate());
-                klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
-                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
-                        block_cores + 2 * tile_grid, nbr, nbr_k, count_ablate(), fa);
+                        (const uint8_t*)core, eps2, parent, fa);
+                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid), dim3(kBlock),
+                        0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2, a.min_points,
+                        core, parent, block_cores + 2 * tile_grid, nbr, nbr_k, (const GridParams*)gp);
             } else {
-                klaunch(prof, "count", kern, dim3(tile_grid), dim3(kBlock), 0, s, xy, cell, seg,
-                        tstart, tstage, &st[kStTiles], eps2, a.min_points, core, parent,
-                        block_cores, nbr, nbr_k, count_ablate(), fa);
+                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid), dim3(kBlock),
+                        0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2, a.min_points,
+                        core, parent, block_cores, nbr, nbr_k, (const GridParams*)gp);
             }
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
@@ -3946,31 +3545,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     // direct fits with fused quarter unions: quarter_root_kernel flags the roots (root bits)
     uint64_t* qlab_bits =
-        (!a.zone && fuse && mode == kGridEps && !box)
+        (!a.zone && fuse)
             ? static_cast<uint64_t*>(ws.is_root.ensure(((n + 63) / 64) * sizeof(uint64_t)))
             : nullptr;
-    if (mode == kGridEps && !box) {  // quarter-cell unions (no-ops unless the grid made them cliques)
-        if (!fuse) {
-            StageTimer t(prof, s, "quarter_init");
-            klaunch(prof, "quarter_init", quarter_init_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qstart,
-                               qkey, &st[kStQuarters], gp, perm, core, qinfo, qg, parent);
-            DBSCAN_HIP_CHECK(hipGetLastError());
-        }
-        if (!fuse) {
-            StageTimer t(prof, s, "union_tile");
-            auto tu = tile_union_kernel<6>;
-            if (union_w() == 5) tu = tile_union_kernel<5>;
-            if (union_w() == 7) tu = tile_union_kernel<7>;
-            klaunch(prof, "tile_union", tu, dim3(tile_grid), dim3(kBlock), 0, s, xy, tq,
-                    &st[kStTiles], qinfo, qg, eps2, perm, core, parent, qcomp, gp);
-            DBSCAN_HIP_CHECK(hipGetLastError());
-        }
+    if (fuse) {  // quarter-cell unions across tiles (no-ops unless the grid made them cliques)
         {
             StageTimer t(prof, s, "union_edge");
-            auto eu = edge_union_kernel<6>;
-            if (union_w() == 5) eu = edge_union_kernel<5>;
-            if (union_w() == 7) eu = edge_union_kernel<7>;
-            klaunch(prof, "edge_union", eu, dim3(tile_grid), dim3(kBlock), 0, s, xy,
+            klaunch(prof, "edge_union", edge_union_kernel<6>, dim3(tile_grid), dim3(kBlock), 0, s, xy,
                     &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
                     (const uint8_t*)tcore);
             DBSCAN_HIP_CHECK(hipGetLastError());
@@ -4203,11 +3784,6 @@ void enqueue_slab_label_prepare(hipStream_t s, Workspace& ws, Profiler* prof,
             static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
             (const uint64_t*)nullptr, (const int32_t*)nullptr, zone, gid, gs_of_root,
             (const int32_t*)nullptr, packed, st.place);
-    if (!kSlabMapPacked) {
-        uint32_t* spacked = static_cast<uint32_t*>(ws.spacked.ensure(st.n * sizeof(uint32_t)));
-        klaunch(prof, "slab_permute", slab_permute_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
-                st.n, st.to_packed, packed, zone, spacked);
-    }
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
@@ -4230,13 +3806,10 @@ void run_slab_label_finish(hipStream_t s, Workspace& ws, Profiler* prof, const S
                 static_cast<const uint8_t*>(ws.core.p), static_cast<const int32_t*>(ws.lab.p),
                 gs_of_root, all_roots, n_roots, label_of_root);
     }
-    if (kSlabMapPacked)  // (the packed labels of the prepare, still in the workspace)
-        klaunch(prof, "slab_map", slab_map_packed_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s,
-                st.n, st.to_packed, static_cast<const uint32_t*>(ws.packed.p), zone,
-                label_of_root, cluster, flag);
-    else
-        klaunch(prof, "slab_map", slab_map_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-                static_cast<const uint32_t*>(ws.spacked.p), zone, label_of_root, cluster, flag);
+    // (the packed labels of the prepare, still in the workspace)
+    klaunch(prof, "slab_map", slab_map_packed_kernel, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
+            st.to_packed, static_cast<const uint32_t*>(ws.packed.p), zone, label_of_root, cluster,
+            flag);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 

@@ -154,11 +154,9 @@ struct ScanState {
 // input index) moved to its padded place, then LSD passes inside the segments.  Outputs:
 // key_fin[n] sorted keys, slot_place[n] the padded place of each sorted slot, rec[place] the
 // record there, pos[i] the padded place of input i; np padded places.
-// DBSCAN_AB_BUCKET_LOG2: A/B builds only (tools/build_ab.sh), never the shipped library
-#ifndef DBSCAN_AB_BUCKET_LOG2
-#define DBSCAN_AB_BUCKET_LOG2 23
-#endif
-constexpr int64_t kBucketMinPoints = int64_t(1) << DBSCAN_AB_BUCKET_LOG2;
+// Threshold 2^23 (A/B against 2^20 and 2^24: at 10^7 points a wash, at config 3's share
+// 2.63 -> 2.52 ms).
+constexpr int64_t kBucketMinPoints = int64_t(1) << 23;
 struct BucketSort {
     DevBuf ka, kb, jb, kc, jc, recb, posb, kf, jf, tab;
     uint32_t* key_fin = nullptr;
@@ -175,7 +173,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, spacked, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, cq;
+        key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm;
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
@@ -189,8 +187,8 @@ struct Workspace {
                           &seg, &core, &parent, &lab, &is_root, &rank, &misc, &qidx, &qkey,
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
-                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &spacked, &lroots,
-                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm, &cq})
+                          &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &lroots,
+                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm})
             b->release();
     }
 };
@@ -273,7 +271,7 @@ struct FitArgs {
     int64_t n_shared = 0;
     // full fits of n <= small_max points (and a mode / eps the one-workgroup kernel serves) run
     // small.hip's single-launch fit; 0 keeps every fit on the tiled pipeline
-    int64_t small_max = kSmallMaxPoints;
+    int64_t small_max = 0;  // (0: the tiled pipeline; entry points opt in from the handle)
     // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
     const BatchFit* batch = nullptr;
 };

@@ -63,10 +63,18 @@ def fit_batch_tensors_async(x: torch.Tensor, y: torch.Tensor, offsets, eps: floa
     import numpy as np
 
     offs = np.ascontiguousarray(offsets, dtype=np.int64)
-    assert x.is_cuda and y.is_cuda and x.dtype == torch.float64 and y.dtype == torch.float64
-    assert cluster.dtype == torch.int32 and flag.dtype == torch.uint8
-    assert n_clusters.dtype == torch.int32 and n_clusters.numel() >= offs.size - 1
-    assert offs[-1] <= x.numel() and x.numel() == y.numel()
+    if offs.ndim != 1 or offs.size < 1 or offs[0] < 0 or np.any(np.diff(offs) < 0):
+        raise ValueError("offsets: n_parts + 1 non-decreasing values from >= 0")
+    total = int(offs[-1])
+    for name, t, dt, need in (("x", x, torch.float64, total), ("y", y, torch.float64, total),
+                              ("cluster", cluster, torch.int32, total),
+                              ("flag", flag, torch.uint8, total),
+                              ("n_clusters", n_clusters, torch.int32, offs.size - 1)):
+        if not (t.is_cuda and t.is_contiguous() and t.dtype == dt and t.device == x.device
+                and t.numel() >= need):
+            raise ValueError(f"{name}: contiguous {dt} tensor of >= {need} values on {x.device}")
+    if x.numel() != y.numel():
+        raise ValueError("x and y differ in length")
     _lib.check(_lib.load().dbscan_fit_batch_device_async(
         handle.ptr, _p(x), _p(y), offs.ctypes.data_as(ctypes.c_void_p), offs.size - 1,
         float(eps), int(min_points), int(mode), _p(cluster), _p(flag), _p(n_clusters)))

@@ -124,10 +124,13 @@ def fit_batch(x, y, offsets, eps: float, min_points: int, mode: int = _lib.MODE_
     if x.shape != y.shape or x.ndim != 1 or offs.ndim != 1 or offs.size < 1:
         raise ValueError("x, y: equal 1-D arrays; offsets: n_parts + 1 values")
     n = x.size
-    if offs[-1] > n:
-        raise ValueError("offsets exceed the arrays")
+    if offs[0] < 0 or np.any(np.diff(offs) < 0) or offs[-1] > n:
+        raise ValueError("offsets: non-decreasing, from >= 0, within the arrays")
     cl = cluster_out if cluster_out is not None else np.zeros(n, np.int32)
     fl = flag_out if flag_out is not None else np.zeros(n, np.uint8)
+    if cl.dtype != np.int32 or fl.dtype != np.uint8 or cl.shape != (n,) or fl.shape != (n,) \
+            or not (cl.flags.c_contiguous and fl.flags.c_contiguous):
+        raise ValueError("cluster_out / flag_out: contiguous int32[n] / uint8[n]")
     nk = np.zeros(max(1, offs.size - 1), np.int32)
     h = handle or default_handle()
     vp = ctypes.c_void_p

@@ -108,3 +108,24 @@ def test_cpp_mirror_compiles_against_the_library(tmp_path):
     subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                     str(exe), "-L", libdir, "-ldbscan_hip", f"-Wl,-rpath,{libdir}"], check=True)
     assert subprocess.run([str(exe)]).returncode == 0
+
+
+def test_fit_batch_rejects_bad_outputs_and_offsets():
+    """dbscan_amd.fit_batch validates the caller's output arrays and offsets before any native
+    call (round-3 ADVICE: an int64, short or strided cluster_out was a host overrun)."""
+    import numpy as np
+
+    x = np.zeros(10)
+    offs = np.array([0, 4, 10])
+    bad_outputs = [
+        dict(cluster_out=np.zeros(10, np.int64)),
+        dict(cluster_out=np.zeros(9, np.int32)),
+        dict(cluster_out=np.zeros(20, np.int32)[::2]),
+        dict(flag_out=np.zeros(10, np.int32)),
+    ]
+    for kw in bad_outputs:
+        with pytest.raises(ValueError):
+            dbscan_amd.fit_batch(x, x, offs, 0.3, 3, **kw)
+    for o in ([-1, 4, 10], [0, 6, 4, 10], [0, 11]):
+        with pytest.raises(ValueError):
+            dbscan_amd.fit_batch(x, x, np.array(o), 0.3, 3)

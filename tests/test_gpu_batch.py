@@ -176,3 +176,27 @@ def test_reference_partitions_of_blobs(dm, handle):
     assert np.array_equal(dnk.cpu().numpy(), got[2])
     assert len(offs) - 1 > 200
     _check_parts(px, py, offs, 2.55, 10, 0, got, "blobs")
+
+
+def test_only_sparse_and_empty_partitions(dm, handle):
+    """A tiled batch (a partition over the one-workgroup capacity) in which NO partition is
+    placed in the virtual grid: every finite partition has a sparse extent (a far outlier), the
+    rest are empty or all-NaN.  Every partition must still be fitted (round-3 ADVICE: the empty
+    and NaN ones were once left with stale outputs)."""
+    rng = np.random.default_rng(8)
+    xs, ys = [], []
+    for m in (9000, 3000):
+        x, y = _blob_part(rng, m, 0.25 * 10, np.array([0.0, 0.0]))
+        x[5] = 1e9  # sparse extent: the partition is fitted alone
+        xs.append(x)
+        ys.append(y)
+    xs += [np.array([]), np.full(30, np.nan), np.array([])]
+    ys += [np.array([]), np.zeros(30), np.array([])]
+    offs = np.concatenate([[0], np.cumsum([a.size for a in xs])]).astype(np.int64)
+    x, y = np.concatenate(xs), np.concatenate(ys)
+    for mp in (1, 5):
+        cl = np.full(x.size, 12345, np.int32)
+        fl = np.full(x.size, 7, np.uint8)
+        got = dm.fit_batch(x, y, offs, 0.25, mp, 0, handle=handle, cluster_out=cl, flag_out=fl)
+        _check_parts(x, y, offs, 0.25, mp, 0, got, f"sparse/empty minPoints {mp}")
+        assert not np.any(fl == 7) and not np.any(cl == 12345)
