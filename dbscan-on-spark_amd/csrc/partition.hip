@@ -13,14 +13,18 @@
 // pointsInRectangle counts the cells CONTAINED in a rectangle (DBSCANRectangle.scala:28-30) with
 // the reference's exact fp comparisons, so the split-line/cell-corner defect (a
 // split line an ulp off a cell corner drops that cell's points) is reproduced, not repaired.
-// Ties between equal-cost splits: first candidate in (x splits, then y splits) order; the
-// reference iterates a Scala HashSet there (:161), an order that is not reproducible.
+// Ties between equal-cost splits (split's reduceLeft over `splits.toSet`, :111-119, :161): the
+// first minimum in the iteration order of a Scala 2.10 immutable Set -- candidate order (x
+// splits, then y splits) for at most four candidates (Set1..Set4), else a HashTrieSet, which
+// iterates by the improved hash of each DBSCANRectangle (split_rank below).  Two candidates
+// whose 32-bit hashes collide would iterate in ListSet order: not modelled (never observed).
 #include "../../include/dbscan_hip.h"
 #include "internal.h"
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -160,6 +164,64 @@ private:
     std::vector<int64_t> sat_;
 };
 
+// ---- Scala 2.10.4 hashing of a DBSCANRectangle (a case class of four Doubles) -------------
+// scala.runtime.BoxesRunTime.hashFromDouble: a boxed Double's ## -- the Int value when exact,
+// else the Long's hashCode when exact, else the Float's (floatToIntBits), else the Double's.
+uint32_t boxed_double_hash(double d) {
+    if (d == d && d > -2147483649.0 && d < 2147483648.0) {
+        const int32_t i = (int32_t)d;  // (truncation: in range)
+        if ((double)i == d) return (uint32_t)i;
+    }
+    if (d == d && d >= -9223372036854775808.0 && d < 9223372036854775808.0) {
+        const int64_t l = (int64_t)d;
+        if ((double)l == d) {
+            const uint64_t u = (uint64_t)l;
+            return (uint32_t)(u ^ (u >> 32));
+        }
+    }
+    // Java's (long) saturates: 2^63 becomes Long.MaxValue, which compares equal to 2^63 as a
+    // double (NaN: Java's (int) / (long) give 0, which is not == NaN: falls through too)
+    if (d == 9223372036854775808.0) return 0x80000000u;  // Long.MaxValue.hashCode
+    const float f = (float)d;
+    if ((double)f == d) {
+        uint32_t b;
+        memcpy(&b, &f, 4);
+        return b;
+    }
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    if (d != d) u = 0x7FF8000000000000ull;  // Double.doubleToLongBits: canonical NaN
+    return (uint32_t)(u ^ (u >> 32));
+}
+// scala.util.hashing.MurmurHash3.productHash(rect, 0xcafebabe): mix per field, finalize
+uint32_t rect_case_hash(const Rect& r) {
+    const auto rotl = [](uint32_t v, int k) { return (v << k) | (v >> (32 - k)); };
+    uint32_t h = 0xCAFEBABEu;
+    const double f[4] = {r.x, r.y, r.x2, r.y2};
+    for (double v : f) {
+        uint32_t k = boxed_double_hash(v) * 0xCC9E2D51u;
+        k = rotl(k, 15) * 0x1B873593u;
+        h = rotl(h ^ k, 13) * 5u + 0xE6546B64u;
+    }
+    h ^= 4u;  // finalizeHash(h, productArity)
+    h = (h ^ (h >> 16)) * 0x85EBCA6Bu;
+    h = (h ^ (h >> 13)) * 0xC2B2AE35u;
+    return h ^ (h >> 16);
+}
+// Iteration rank of a rectangle in a Scala 2.10 immutable.HashSet (HashTrieSet): the element's
+// hash goes through HashSet.improve, then the trie indexes 5-bit groups from the low bits up and
+// iterates children in index order -- i.e. ascending order of the groups read low group first.
+uint32_t split_rank(const Rect& r) {
+    uint32_t h = rect_case_hash(r);
+    h += ~(h << 9);
+    h ^= h >> 14;
+    h += h << 4;
+    h ^= h >> 10;
+    uint32_t key = 0;
+    for (int lvl = 0; lvl < 6; ++lvl) key = (key << 5) | ((h >> (5 * lvl)) & 31u);
+    return (key << 2) | (h >> 30);
+}
+
 // Number of elements of the Scala 2.10 Double range `start until end by step`
 // (EvenSplitPartitioner.scala:150-152): NumericRange.count, restated exactly in javanum.hip;
 // the elements themselves come by repeated addition from start (NumericRange.foreach).
@@ -177,10 +239,14 @@ bool best_split(const CellGrid& g, const Rect& box, double mrs, Rect* s1, Rect* 
     bool have = false;
     int64_t best_cost = 0;
     Rect best = box;
+    int64_t lens[2];
+    for (int axis = 0; axis < 2; ++axis)
+        lens[axis] = range_len((axis == 0 ? box.x : box.y) + mrs, axis == 0 ? box.x2 : box.y2, mrs);
+    const bool trie = lens[0] + lens[1] > 4;  // the candidate Set is a HashTrieSet
+    uint32_t best_rank = 0;
     for (int axis = 0; axis < 2; ++axis) {
         const double start = (axis == 0 ? box.x : box.y) + mrs;
-        const double end = axis == 0 ? box.x2 : box.y2;
-        const int64_t len = range_len(start, end, mrs);
+        const int64_t len = lens[axis];
         const int64_t base = axis == 0 ? g.imin() : g.jmin();
         const int64_t lim = base + (axis == 0 ? g.W() : g.H());
         int64_t last = (axis == 0 ? c0 : r0) - 1;  // last contained column/row so far
@@ -189,10 +255,18 @@ bool best_split(const CellGrid& g, const Rect& box, double mrs, Rect* s1, Rect* 
             while (last + 1 < lim && g.hi(last + 1) <= v) ++last;
             const int64_t cnt = axis == 0 ? g.count(c0, last, r0, r1) : g.count(c0, c1, r0, last);
             const int64_t cost = std::llabs(half - cnt);
+            const Rect cand = axis == 0 ? Rect{box.x, box.y, v, box.y2} : Rect{box.x, box.y, box.x2, v};
             if (!have || cost < best_cost) {
                 best_cost = cost;
-                best = axis == 0 ? Rect{box.x, box.y, v, box.y2} : Rect{box.x, box.y, box.x2, v};
+                best = cand;
                 have = true;
+                if (trie) best_rank = split_rank(cand);
+            } else if (trie && cost == best_cost) {
+                const uint32_t rk = split_rank(cand);
+                if (rk < best_rank) {
+                    best = cand;
+                    best_rank = rk;
+                }
             }
         }
     }

@@ -28,6 +28,8 @@ import subprocess
 
 import numpy as np
 
+import jvm  # noqa: E402  (oracle/jvm.py: JDK 7/8 Double.toString, Scala 2.10 hashing)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
@@ -49,8 +51,8 @@ def scala_range_count(start: float, end: float, step: float, inclusive: bool = F
     decimal module: diff = end - start in double arithmetic; quot = (BigDecimal(diff) /
     BigDecimal(step)) at DECIMAL128 (34 digits, HALF_EVEN), doubleValue, toLong; rem =
     BigDecimal remainder (zero iff the decimals divide exactly); BigDecimal(d) is the decimal
-    of Double.toString(d), taken here as the shortest round-trip digits (repr) -- JDK 7/8
-    print longer digits for ~0.3% of doubles (csrc/javanum.hip has that form)."""
+    of Double.toString(d) as JDK 7/8 print it (oracle/jvm.py jdk8_double_string; longer than
+    the shortest round-trip digits for ~0.3% of doubles)."""
     import decimal
     from fractions import Fraction
 
@@ -62,7 +64,8 @@ def scala_range_count(start: float, end: float, step: float, inclusive: bool = F
         return 0
     start, end, step = float(start), float(end), float(step)
     diff = end - start
-    d, s = decimal.Decimal(repr(diff)), decimal.Decimal(repr(step))
+    d = decimal.Decimal(jvm.jdk8_double_string(diff))
+    s = decimal.Decimal(jvm.jdk8_double_string(step))
     ctx = decimal.Context(prec=34, rounding=decimal.ROUND_HALF_EVEN)
     q = float(ctx.divide(d, s))  # float(Decimal) is correctly rounded
     jumps = int(q) if q == q else 0
@@ -85,6 +88,10 @@ def _range_count_py(a, b, c):
 
 
 _range_count_cb = _RANGE_COUNT_FN(_range_count_py)
+
+_SPLIT_KEY_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double)
+_split_key_cb = _SPLIT_KEY_FN(lambda a, b, c, d: jvm.split_order_key(a, b, c, d))
 
 
 def lib() -> ctypes.CDLL:
@@ -120,6 +127,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_set_range_count.argtypes = [_RANGE_COUNT_FN]
         L.oracle_set_range_count.restype = None
         L.oracle_set_range_count(_range_count_cb)
+        L.oracle_set_split_key.argtypes = [_SPLIT_KEY_FN]
+        L.oracle_set_split_key.restype = None
+        L.oracle_set_split_key(_split_key_cb)
         _lib = L
     return _lib
 

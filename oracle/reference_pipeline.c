@@ -19,8 +19,12 @@
  *   - pointsInRectangle is answered with a summed-area table; the contained cell-index
  *     range is found by binary search with the reference's exact fp comparisons, so the
  *     answer equals the linear scan (:175-181), including the split-line/cell-corner defect.
- *   - Ties in split cost are broken by candidate order (x splits, then y splits); the
- *     reference breaks them by Scala HashSet iteration order (:161, :111-119): unpinned.
+ *   - Ties in split cost: `splits.toSet.reduceLeft` (:111-119, :161) keeps the first
+ *     minimum in the Set's iteration order -- candidate order (x splits, then y splits) for at
+ *     most 4 candidates (Set1..Set4), else the HashTrieSet order of the candidates' hashes,
+ *     which the Python side of the oracle computes (oracle/jvm.py split_order_key: Scala 2.10
+ *     MurmurHash3.productHash + HashSet.improve) and hands in as a callback, like the range
+ *     count.  Full 32-bit hash collisions (ListSet order) are not modelled.
  *   - Scala's Double NumericRange (:150-152) is restated as repeated addition from the
  *     start with its length from quotient/remainder in extended precision.
  *   - Spark shuffle order inside groupByKey is taken as map-partition order, then the
@@ -111,6 +115,11 @@ static int64_t range_count(double start, double end, double step) {
 
 typedef struct { rect_t r; int64_t c; } rc_t;
 
+/* HashTrieSet iteration rank of a candidate rectangle (smaller first): oracle/jvm.py */
+typedef uint32_t (*split_key_fn)(double x, double y, double x2, double y2);
+static split_key_fn g_split_key = NULL;
+void oracle_set_split_key(split_key_fn fn) { g_split_key = fn; }
+
 /* EvenSplitPartitioner.scala:105-123 split + :128-143 complement. Returns 0 on error. */
 static int split_rect(const grid_t* g, rect_t box, double mrs, rect_t* s1, rect_t* s2) {
     int64_t total = points_in(g, box);
@@ -118,12 +127,18 @@ static int split_rect(const grid_t* g, rect_t box, double mrs, rect_t* s1, rect_
     int have = 0;
     rect_t best = box;
     int64_t best_cost = 0;
+    int64_t cnts[2];
+    for (int axis = 0; axis < 2; ++axis)
+        cnts[axis] = range_count((axis == 0 ? box.x : box.y) + mrs, axis == 0 ? box.x2 : box.y2,
+                                 mrs);
+    /* more than 4 candidates: a HashTrieSet, ties go to the smaller trie rank */
+    const int hashed = cnts[0] + cnts[1] > 4;
+    int have_key = 0;
+    uint32_t best_key = 0;
     for (int axis = 0; axis < 2; ++axis) {
         double start = (axis == 0 ? box.x : box.y) + mrs;
-        double end = axis == 0 ? box.x2 : box.y2;
-        int64_t cnt = range_count(start, end, mrs);
         double v = start;
-        for (int64_t k = 0; k < cnt; ++k, v += mrs) {
+        for (int64_t k = 0; k < cnts[axis]; ++k, v += mrs) {
             rect_t cand = axis == 0 ? (rect_t){box.x, box.y, v, box.y2}
                                     : (rect_t){box.x, box.y, box.x2, v};
             int64_t cost = llabs(half - points_in(g, cand));
@@ -131,6 +146,18 @@ static int split_rect(const grid_t* g, rect_t box, double mrs, rect_t* s1, rect_
                 best = cand;
                 best_cost = cost;
                 have = 1;
+                have_key = 0;
+            } else if (cost == best_cost && hashed) {
+                if (!g_split_key) return 0;
+                if (!have_key) {
+                    best_key = g_split_key(best.x, best.y, best.x2, best.y2);
+                    have_key = 1;
+                }
+                uint32_t key = g_split_key(cand.x, cand.y, cand.x2, cand.y2);
+                if (key < best_key) {
+                    best = cand;
+                    best_key = key;
+                }
             }
         }
     }

@@ -112,3 +112,84 @@ def test_duplicate_into_outer_rectangles(seed):
     for p in range(len(rects)):
         want = np.flatnonzero((ox[p] <= x) & (x <= ox2[p]) & (oy[p] <= y) & (y <= oy2[p]))
         np.testing.assert_array_equal(idx[offs[p]:offs[p + 1]], want)
+
+
+def test_murmur3_primitives_known_vectors():
+    """The oracle's MurmurHash3 mix / finalization (oracle/jvm.py, restating Scala 2.10's
+    scala.util.hashing.MurmurHash3 that DBSCANRectangle.hashCode goes through) against the
+    published MurmurHash3_x86_32 verification values (4-byte blocks, byte length mixed in)."""
+    import jvm
+
+    def x86_32(blocks, seed):
+        h = seed
+        for k in blocks:
+            h = jvm._mix(h, k)
+        return jvm._avalanche(h ^ (4 * len(blocks)))
+
+    assert x86_32([], 0) == 0
+    assert x86_32([], 1) == 0x514E28B7
+    assert x86_32([0xFFFFFFFF], 0) == 0x76293B50
+    assert x86_32([0x87654321], 0) == 0xF55B516B
+    assert x86_32([0x87654321], 0x5082EDEE) == 0x2362F9DE
+    assert x86_32([0x61616161], 0x9747B28C) == 0x5A97808A
+    # BoxesRunTime.hashFromDouble: Int, Long, Float and Double cases
+    assert jvm.hash_from_double(3.0) == 3 and jvm.hash_from_double(-1.0) == 0xFFFFFFFF
+    assert jvm.hash_from_double(2.0 ** 40) == (2 ** 40 ^ 0) >> 32 ^ (2 ** 40 & 0xFFFFFFFF)
+    assert jvm.hash_from_double(0.5) == 0x3F000000
+    assert jvm.hash_from_double(0.1) == 0x9999999A ^ 0x3FB99999
+
+
+def _first_split_candidates(spec, mrs):
+    """The first split of the bounding rectangle, restated directly over the cells: every
+    candidate (x splits, then y splits) with its cost |count/2 - pointsIn(candidate)|."""
+    import jvm
+
+    x0 = min(c[0] for c in spec)
+    y0 = min(c[1] for c in spec)
+    x2 = max(c[2] for c in spec)
+    y2 = max(c[3] for c in spec)
+    total = sum(c[4] for c in spec)
+
+    def pin(r):
+        return sum(c[4] for c in spec
+                   if r[0] <= c[0] and c[2] <= r[2] and r[1] <= c[1] and c[3] <= r[3])
+
+    cands = []
+    for axis in (0, 1):
+        start = (x0 if axis == 0 else y0) + mrs
+        end = x2 if axis == 0 else y2
+        v = start
+        for _ in range(O.scala_range_count(start, end, mrs)):
+            r = (x0, y0, v, y2) if axis == 0 else (x0, y0, x2, v)
+            cands.append((r, abs(total // 2 - pin(r)), jvm.split_order_key(*r)))
+            v += mrs
+    return cands
+
+
+@pytest.mark.parametrize("shape", ["square", "gaps", "stripes"])
+def test_tie_heavy_lattices_vs_oracle(shape):
+    """Cell sets built so that equal-cost split candidates are the rule: the product
+    (csrc/partition.hip) and the oracle (reference_pipeline.c with oracle/jvm.py's ranks), two
+    independent restatements of Scala 2.10's `splits.toSet` order, must pick the same splits.
+    The first split is checked to be a tie that the HashTrieSet order decides differently from
+    plain candidate order, so the case discriminates."""
+    mrs, o = 1.0, 9  # (o: an x offset at which every shape's first tie is decided by rank)
+    if shape == "square":  # 16 x 16 unit cells of one point: x = 8 and y = 8 both halve it
+        spec = [(i + o, j, i + o + 1, j + 1, 1) for i in range(16) for j in range(16)]
+        maxpp = 5
+    elif shape == "gaps":  # two blocks with an empty band between them: every x in the band ties
+        spec = [(i + o, j, i + o + 1, j + 1, 2) for i in list(range(0, 6)) + list(range(14, 20))
+                for j in range(10)]
+        maxpp = 7
+    else:  # vertical stripes of equal weight with empty columns between them
+        spec = [(i + o, j, i + o + 1, j + 1, 3) for i in range(0, 24, 3) for j in range(12)]
+        maxpp = 10
+    cands = _first_split_candidates(spec, mrs)
+    best = min(c[1] for c in cands)
+    ties = [c for c in cands if c[1] == best]
+    assert len(cands) > 4 and len(ties) > 1
+    by_rank = min(ties, key=lambda c: c[2])[0]
+    assert by_rank != ties[0][0], "the tie order must matter for this case"
+    got = EvenSplitPartitioner.partition(_cells(spec), maxpp, mrs)
+    ref = O.ref_partition_cells(spec, maxpp, mrs)
+    assert [(tuple(r), c) for r, c in got] == [(tuple(map(float, r)), c) for r, c in ref]

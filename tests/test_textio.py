@@ -150,3 +150,27 @@ def test_scala_double_range_count_vs_oracle():
         step = abs(rng.normal()) * 10.0 ** rng.integers(-3, 1)
         if end > start and (end - start) / step < 1e6:
             assert scala_range_count(start, end, step) == O.scala_range_count(start, end, step)
+
+
+def test_double_to_string_two_restatements_agree():
+    """java.lang.Double.toString as JDK 7/8 print it, restated twice: the product's
+    csrc/javanum.hip (C++ bigints) and the oracle's oracle/jvm.py (Python ints), over random bit
+    patterns, decimals of few digits, integers past 2^53 and tiny / huge magnitudes -- the digits
+    BigDecimal(Double.toString(_)) sees in the partitioner's NumericRange count."""
+    import random
+    import struct
+
+    import jvm
+
+    from dbscan_amd.textio import format_double
+
+    rng = random.Random(7)
+    gens = [lambda: struct.unpack("<d", struct.pack("<Q", rng.getrandbits(64)))[0],
+            lambda: round(rng.uniform(-100, 100), rng.randint(0, 6)),
+            lambda: rng.randint(-2 ** 62, 2 ** 62) * 1.0,
+            lambda: rng.uniform(0, 1) * 10.0 ** rng.randint(-30, 30),
+            lambda: 0.1 * rng.randint(-10000, 10000) + 2.0 * 0.30000001192092896]
+    for g in gens:
+        for _ in range(4000):
+            v = g()
+            assert format_double(v) == jvm.jdk8_double_string(v), repr(v)
