@@ -152,19 +152,6 @@ std::vector<double> make_cuts(const double* x, int64_t n, int world, double eps)
     return cuts;
 }
 
-struct Shard {
-    HostVec<int64_t> gid;  // slab points, increasing global visit index
-    HostVec<double> x, y;
-    HostVec<uint8_t> zone;
-    HostVec<int32_t> shared;  // slab indices of points in zones 0/1 of another shard too
-    HostVec<int32_t> root;    // slab fit output (-1: not core)
-    HostVec<int64_t> gs;      // global s(K) per local root (only the roots' entries are read)
-    HostVec<int32_t> cluster;
-    HostVec<uint8_t> flag;
-    std::string err;
-    int32_t rc = DBSCAN_OK;
-};
-
 // node.py zones(): zone of x for shard r (0 owned, 1 inner halo, 2 outer halo, kOut) and
 // whether the point is shared (in zone 0/1 of an adjacent shard as well).  The margins depend on
 // the cut values alone, so they are computed once per shard (ZoneCut), not per point.
@@ -193,9 +180,10 @@ std::vector<ZoneCut> zone_cuts(int world, const std::vector<double>& cuts, doubl
     return zc;
 }
 
-uint8_t zone_of(double x, int r, int world, const ZoneCut& c, bool* shared) {
+__host__ __device__ inline uint8_t zone_of(double x, int r, int world, const ZoneCut& c,
+                                           bool* shared) {
     bool own = (!c.has_lo || x >= c.lo) && (!c.has_hi || x < c.hi);
-    if (r == 0 && world > 1 && std::isnan(x)) own = true;
+    if (r == 0 && world > 1 && x != x) own = true;
     bool in1 = false, in2 = false, sh = false;
     if (c.has_lo) {
         in1 = in1 || (x >= c.lo - c.m1lo && x < c.lo);
@@ -212,148 +200,174 @@ uint8_t zone_of(double x, int r, int world, const ZoneCut& c, bool* shared) {
     return z;
 }
 
-// Uploads a shard and runs its slab fit on handle h (device buffers returned in *dev, freed by
-// the caller).  Phase 1 reads the roots back; phase 2 re-fits on a handle that held other
-// shards meanwhile (the fit is deterministic) and then labels.
-struct ShardDev {
+// ---- the slab plan on the device -------------------------------------------------------
+// Shard r's points (zone != kOut for r) in increasing global visit order, by an ordered
+// three-kernel compaction over all n points: per-block counts of the shard's points and of its
+// shared points, an exclusive scan of each, a ballot-ranked write.  kPlanTile points per block.
+constexpr int kPlanTile = 8192;  // 32 rounds of 256
+
+__global__ __launch_bounds__(kBlock) void plan_count_kernel(const double* __restrict__ x,
+                                                            int64_t n, int r, int world,
+                                                            ZoneCut zc,
+                                                            int32_t* __restrict__ cnt_sel,
+                                                            int32_t* __restrict__ cnt_sh) {
+    __shared__ int ws[2][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    int c = 0, h = 0;
+    for (int k = 0; k < kPlanTile / kBlock; ++k) {
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        if (i >= n) break;
+        bool sh = false;
+        const uint8_t z = zone_of(x[i], r, world, zc, &sh);
+        c += z != kOut ? 1 : 0;
+        h += (z != kOut && sh) ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, 64);
+        h += __shfl_xor(h, o, 64);
+    }
+    if (__lane_id() == 0) {
+        ws[0][threadIdx.x >> 6] = c;
+        ws[1][threadIdx.x >> 6] = h;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += ws[threadIdx.x][w];
+        (threadIdx.x ? cnt_sh : cnt_sel)[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void plan_write_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, int64_t n, int r, int world,
+    ZoneCut zc, const int32_t* __restrict__ off_sel, const int32_t* __restrict__ off_sh,
+    double* __restrict__ sx, double* __restrict__ sy, uint8_t* __restrict__ sz,
+    int64_t* __restrict__ sgid, int64_t* __restrict__ sshared) {
+    __shared__ int wc[2][2][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int o = off_sel[blockIdx.x], oh = off_sh[blockIdx.x];
+    for (int k = 0; k < kPlanTile / kBlock; ++k) {
+        if (base + k * kBlock >= n) break;  // (block-uniform)
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        bool sh = false;
+        uint8_t z = kOut;
+        double xi = 0;
+        if (i < n) {
+            xi = x[i];
+            z = zone_of(xi, r, world, zc, &sh);
+        }
+        const bool in = z != kOut;
+        sh = sh && in;
+        const uint64_t b = __ballot(in), bh = __ballot(sh);
+        if (lane == 0) {
+            wc[k & 1][0][w] = __popcll(b);
+            wc[k & 1][1][w] = __popcll(bh);
+        }
+        __syncthreads();
+        int before = 0, total = 0, beforeh = 0, totalh = 0;
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+            const int c = wc[k & 1][0][v], ch = wc[k & 1][1][v];
+            before += v < w ? c : 0;
+            total += c;
+            beforeh += v < w ? ch : 0;
+            totalh += ch;
+        }
+        if (in) {
+            const int64_t q = (int64_t)o + before + __popcll(b & lt);
+            sx[q] = xi;
+            sy[q] = y[i];
+            sz[q] = z;
+            sgid[q] = i;
+            if (sh) sshared[oh + beforeh + __popcll(bh & lt)] = q;
+        }
+        o += total;
+        oh += totalh;
+    }
+}
+
+// The merge records of a shard: (gid of a shared point, gid of its local root, or -1 when the
+// point is not core here) -- node.py NodeJob.run's records.
+__global__ __launch_bounds__(kBlock) void plan_records_kernel(
+    const int64_t* __restrict__ sshared, int64_t ns, const int64_t* __restrict__ sgid,
+    const uint8_t* __restrict__ score, const int32_t* __restrict__ sroot, int64_t* __restrict__ a,
+    int64_t* __restrict__ b) {
+    const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= ns) return;
+    const int64_t p = sshared[k];
+    const int32_t r = sroot[p];
+    a[k] = sgid[p];
+    b[k] = (score[p] != 0 && r >= 0) ? sgid[r] : -1;
+}
+
+// The zone-0 labels of a shard (slab order) into the whole job's output arrays (input order).
+__global__ __launch_bounds__(kBlock) void plan_scatter_kernel(
+    int64_t m, const uint8_t* __restrict__ sz, const int64_t* __restrict__ sgid,
+    const int32_t* __restrict__ cl, const uint8_t* __restrict__ fl, int32_t* __restrict__ out_cl,
+    uint8_t* __restrict__ out_fl) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= m || sz[p] != 0) return;
+    const int64_t g = sgid[p];
+    out_cl[g] = cl[p];
+    out_fl[g] = fl[p];
+}
+
+unsigned nblocks(int64_t m) { return (unsigned)std::max<int64_t>(1, (m + kBlock - 1) / kBlock); }
+
+// A shard on its device: the slab (x, y, zone, gid in increasing gid), its shared points, the
+// slab fit's outputs and each local root's global s(K).
+struct DevShard {
+    int64_t m = 0, ns = 0;
     double *x = nullptr, *y = nullptr;
     uint8_t *zone = nullptr, *core = nullptr;
+    int64_t *gid = nullptr, *shared = nullptr, *gs = nullptr;
     int32_t* root = nullptr;
+    std::vector<int64_t> a, b, own;  // host: merge records, owned global roots
+    int32_t rc = DBSCAN_OK;
+    std::string err;
     void release() {
-        for (void* p : {(void*)x, (void*)y, (void*)zone, (void*)core, (void*)root}) (void)hipFree(p);
-        *this = ShardDev();
+        for (void* p : {(void*)x, (void*)y, (void*)zone, (void*)core, (void*)gid, (void*)shared,
+                        (void*)gs, (void*)root})
+            (void)hipFree(p);
+        x = y = nullptr;
+        zone = core = nullptr;
+        gid = shared = gs = nullptr;
+        root = nullptr;
     }
 };
 
-bool shard_upload_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points,
-                      ShardDev* d) {
-    const int64_t m = (int64_t)s.gid.size();
-    auto fail = [&](hipError_t e, const char* what) {
-        s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
-        s.err = std::string(what) + ": " + hipGetErrorString(e);
-        return false;
-    };
-    hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&d->x, m * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&d->y, m * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&d->zone, m);
-    if (e == hipSuccess) e = hipMalloc(&d->core, m);
-    if (e == hipSuccess) e = hipMalloc(&d->root, m * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMemcpy(d->x, s.x.data(), m * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d->y, s.y.data(), m * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d->zone, s.zone.data(), m, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return fail(e, "shard upload");
-    s.rc = dbscan_slab_fit_device(h, d->x, d->y, d->zone, m, eps, min_points, d->core, d->root);
-    if (s.rc != DBSCAN_OK) {
-        s.err = dbscan_last_error();
-        return false;
-    }
-    return true;
-}
-
-// Phase 1 of one shard: slab fit, roots back to the host.
-void shard_fit(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points) {
-    const int64_t m = (int64_t)s.gid.size();
-    s.root.resize(m);  // (downloaded whole)
-    if (m == 0) return;
-    ShardDev d;
-    if (shard_upload_fit(s, h, device, eps, min_points, &d)) {
-        const hipError_t e =
-            hipMemcpy(s.root.data(), d.root, m * sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e != hipSuccess) {
-            s.rc = DBSCAN_EHIP;
-            s.err = std::string("shard download: ") + hipGetErrorString(e);
-        }
-    }
-    d.release();
-}
-
-// Phase 2: labels of the shard's zone-0 points from the merged component ids.  refit: the
-// handle's last slab fit was another shard's (shards sharing a device run one after another on
-// one handle, so a device holds one workspace, not one per shard).
-void shard_label(Shard& s, dbscan_handle* h, int device, double eps, int32_t min_points,
-                 const std::vector<int64_t>& all_roots, int32_t mode, bool refit) {
-    const int64_t m = (int64_t)s.gid.size();
-    s.cluster.resize(m);  // (downloaded whole; only zone-0 entries are used)
-    s.flag.resize(m);
-    if (m == 0) return;
-    ShardDev fitd;
-    if (refit && !shard_upload_fit(s, h, device, eps, min_points, &fitd)) {
-        fitd.release();
-        return;
-    }
-    uint8_t *dz = nullptr, *dfl = nullptr;
-    int64_t *dgid = nullptr, *dgs = nullptr, *droots = nullptr;
-    int32_t* dcl = nullptr;
-    const int64_t nr = (int64_t)all_roots.size();
-    hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&dz, m);
-    if (e == hipSuccess) e = hipMalloc(&dfl, m);
-    if (e == hipSuccess) e = hipMalloc(&dgid, m * sizeof(int64_t));
-    if (e == hipSuccess) e = hipMalloc(&dgs, m * sizeof(int64_t));
-    if (e == hipSuccess) e = hipMalloc(&droots, std::max<int64_t>(1, nr) * sizeof(int64_t));
-    if (e == hipSuccess) e = hipMalloc(&dcl, m * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMemcpy(dz, s.zone.data(), m, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dgid, s.gid.data(), m * sizeof(int64_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dgs, s.gs.data(), m * sizeof(int64_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess && nr > 0)
-        e = hipMemcpy(droots, all_roots.data(), nr * sizeof(int64_t), hipMemcpyHostToDevice);
-    // zone 1/2 entries are not labelled here (the output takes zone-0 entries only)
-    if (e == hipSuccess) e = hipMemset(dcl, 0, m * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMemset(dfl, DBSCAN_FLAG_NOT_FLAGGED, m);
-    if (e != hipSuccess) {
-        s.rc = e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
-        s.err = std::string("shard label upload: ") + hipGetErrorString(e);
-    } else {
-        s.rc = dbscan_slab_label_device(h, dz, dgid, dgs, droots, nr, mode, dcl, dfl);
-        if (s.rc != DBSCAN_OK) {
-            s.err = dbscan_last_error();
-        } else {
-            e = hipMemcpy(s.cluster.data(), dcl, m * sizeof(int32_t), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(s.flag.data(), dfl, m, hipMemcpyDeviceToHost);
-            if (e != hipSuccess) {
-                s.rc = DBSCAN_EHIP;
-                s.err = std::string("shard label download: ") + hipGetErrorString(e);
-            }
-        }
-    }
-    for (void* p : {(void*)dz, (void*)dfl, (void*)dgid, (void*)dgs, (void*)droots, (void*)dcl})
-        (void)hipFree(p);
-    fitd.release();
-}
-
-// Min-root union-find over global visit indices (host; the records are few).
-struct GidUnion {
-    std::unordered_map<int64_t, int64_t> up;
-    int64_t find(int64_t v) {
-        auto it = up.find(v);
-        if (it == up.end()) return v;
-        int64_t r = v;
-        while (true) {
-            auto jt = up.find(r);
-            if (jt == up.end() || jt->second == r) break;
-            r = jt->second;
-        }
-        while (v != r) {  // compress
-            int64_t& nx = up[v];
-            const int64_t t = nx;
-            nx = r;
-            v = t;
-        }
-        return r;
-    }
-    void unite(int64_t a, int64_t b) {
-        a = find(a);
-        b = find(b);
-        if (a == b) return;
-        if (a < b) std::swap(a, b);
-        up[a] = b;  // the larger index hangs under the smaller: a root is s(K)
-        up.emplace(b, b);
-    }
+// HIP failures inside a device worker: thrown, caught per worker
+struct HipFail {
+    hipError_t e;
+    const char* what;
 };
+inline void hcheck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipFail{e, what};
+}
+inline void ccheck(int32_t rc) {
+    if (rc != DBSCAN_OK) throw rc;
+}
 
 }  // namespace
 
+// dbscan_train_node: the slab plan, the slab fits, the merge and the labels all on the
+// devices (round 4; rounds 1-3 built the plan and merged on the host: 16.9 s for 10^9 points on
+// one GPU, 7.3 s of it the host plan).  Per device (one host thread and one handle each; shard
+// s on device s % device_count):
+//   A  upload x, y; for each of its shards: zone + ordered compaction (plan_*_kernel), the lean
+//      slab fit (dbscan_slab_fit_shared_device_async: roots at the shared points only), the
+//      merge records (gid, root gid) -> host
+//   B  (host) every shard's records, concatenated
+//   C  union of all records on each device (dbscan_merge_union_device: the same lock-free
+//      union as node.py's ranks), each shard's local roots -> global s(K) and its owned global
+//      roots (dbscan_slab_merge_roots_device) -> host
+//   D  (host) the owned roots of all shards, sorted: cluster id = 1 + rank of s(K)
+//   E  per shard: re-fit when its device held other shards since (one workspace per device),
+//      label (dbscan_slab_label_device), scatter the zone-0 labels into the output by gid;
+//      one device: the whole output on the device, one copy back; several: each device's
+//      labels copied back and scattered by host threads.
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
                    int64_t* n_clusters_out, std::string* err) {
@@ -379,85 +393,15 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         *n_clusters_out = k;
         return rc;
     }
-    const int world = (int)cuts.size() + 1;
-    const double R = reach(eps);
-    const std::vector<ZoneCut> zc = zone_cuts(world, cuts, R);
-    std::vector<Shard> sh(world);
-    // slab plan: every shard's points in increasing global visit order, built by host threads
-    // over contiguous chunks of the input (count, then fill at the chunk's offsets)
-    const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / 65536 + 1));
-    std::vector<int64_t> cnt((size_t)nth * world * 2, 0);  // [thread][shard]{points, shared}
-    const auto chunk = [&](int t) {
-        return std::make_pair(n * t / nth, n * (t + 1) / nth);
-    };
-    // only the owner and shards whose halo can reach x need a look: scan neighbours of the
-    // owner until both directions fall out of reach
-    const auto visit = [&](int64_t i, auto&& f) {
-        const int own = std::isnan(x[i])  // NaN x is owned by shard 0 (node.py zones)
-                            ? 0
-                            : (int)(std::upper_bound(cuts.begin(), cuts.end(), x[i]) -
-                                    cuts.begin());
-        for (int dir = -1; dir <= 1; dir += 2) {
-            for (int r = (dir < 0 ? own : own + 1); r >= 0 && r < world; r += dir) {
-                // a shard past the owner's is reached only through its outer halo margin
-                // (zone_of would say kOut; NaN included): most points stop here at once
-                if (r != own && (dir < 0 ? !(x[i] <= zc[r].hi + zc[r].m2hi)
-                                         : !(x[i] >= zc[r].lo - zc[r].m2lo)))
-                    break;
-                bool shared = false;
-                const uint8_t z = zone_of(x[i], r, world, zc[r], &shared);
-                if (z == kOut) {
-                    if (r != own) break;
-                    continue;
-                }
-                f(r, z, shared);
-            }
-        }
-    };
-    parallel_for(nth, [&](int t) {
-        int64_t* c = &cnt[(size_t)t * world * 2];
-        const auto [i0, i1] = chunk(t);
-        for (int64_t i = i0; i < i1; ++i)
-            visit(i, [&](int r, uint8_t, bool shared) {
-                ++c[2 * r];
-                c[2 * r + 1] += shared ? 1 : 0;
-            });
-    });
-    tr.mark("plan count");
-    std::vector<int64_t> at((size_t)nth * world * 2, 0);
-    for (int r = 0; r < world; ++r) {
-        int64_t np = 0, ns = 0;
-        for (int t = 0; t < nth; ++t) {
-            at[((size_t)t * world + r) * 2] = np;
-            at[((size_t)t * world + r) * 2 + 1] = ns;
-            np += cnt[((size_t)t * world + r) * 2];
-            ns += cnt[((size_t)t * world + r) * 2 + 1];
-        }
-        sh[r].gid.resize((size_t)np);
-        sh[r].x.resize((size_t)np);
-        sh[r].y.resize((size_t)np);
-        sh[r].zone.resize((size_t)np);
-        sh[r].shared.resize((size_t)ns);
+    if (n >= (int64_t)INT32_MAX) {
+        *err = "dbscan_train_node: more than 2^31 - 1 points";
+        return DBSCAN_EARG;
     }
-    tr.mark("plan alloc");
-    parallel_for(nth, [&](int t) {
-        int64_t* a = &at[(size_t)t * world * 2];
-        const auto [i0, i1] = chunk(t);
-        for (int64_t i = i0; i < i1; ++i)
-            visit(i, [&](int r, uint8_t z, bool shared) {
-                Shard& s = sh[r];
-                const int64_t k = a[2 * r]++;
-                if (shared) s.shared[(size_t)a[2 * r + 1]++] = (int32_t)k;
-                s.gid[(size_t)k] = i;
-                s.x[(size_t)k] = x[i];
-                s.y[(size_t)k] = y[i];
-                s.zone[(size_t)k] = z;
-            });
-    });
-    tr.mark("plan fill");
-    // one host thread and one handle per device; the shards of a device run one after another
-    // on its handle (one workspace per device: 8 shards of a 10^9-point job on one GPU)
+    const int world = (int)cuts.size() + 1;
+    const std::vector<ZoneCut> zc = zone_cuts(world, cuts, reach(eps));
     const int nworkers = std::min(world, ndev);
+    const bool shared_dev = world > nworkers;
+    std::vector<DevShard> sh(world);
     std::vector<dbscan_handle*> hs(nworkers, nullptr);
     for (int w = 0; w < nworkers; ++w) {
         hs[w] = dbscan_create(w);
@@ -468,77 +412,292 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
             return DBSCAN_EHIP;
         }
     }
-    const bool shared_dev = world > nworkers;
+    struct Dev {  // per device: the union's parent array and records, output arrays
+        int32_t* parent = nullptr;
+        int64_t *ra = nullptr, *rb = nullptr, *roots = nullptr;
+        int32_t* out_cl = nullptr;
+        uint8_t* out_fl = nullptr;
+        int32_t rc = DBSCAN_OK;
+        std::string err;
+    };
+    std::vector<Dev> dv(nworkers);
+    // runs f(w) on one host thread per device; a failure is recorded per device
     auto each_device = [&](auto&& f) {
         std::vector<std::thread> th;
         for (int w = 0; w < nworkers; ++w)
             th.emplace_back([&, w]() {
-                for (int r = w; r < world; r += nworkers) f(r, w);
+                try {
+                    hcheck(hipSetDevice(w), "hipSetDevice");
+                    f(w);
+                } catch (const HipFail& e) {
+                    dv[w].rc = e.e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
+                    dv[w].err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+                } catch (int32_t rc) {
+                    dv[w].rc = rc;
+                    dv[w].err = dbscan_last_error();
+                }
             });
         for (auto& t : th) t.join();
+        for (auto& d : dv)
+            if (d.rc != DBSCAN_OK) return false;
+        return true;
     };
-    each_device([&](int r, int w) { shard_fit(sh[r], hs[w], w, eps, min_points); });
-    tr.mark("slab fits");
+    auto lean_fit = [&](int r, int w) {
+        DevShard& s = sh[r];
+        ccheck(dbscan_slab_fit_shared_device_async(hs[w], s.x, s.y, s.zone, s.m, eps, min_points,
+                                                   s.shared, s.ns, s.core, s.root));
+    };
     int32_t rc = DBSCAN_OK;
-    for (auto& s : sh)
-        if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
-            rc = s.rc;
-            *err = s.err;
-        }
+    int64_t nroots = 0;
     std::vector<int64_t> all_roots;
-    if (rc == DBSCAN_OK) {
-        GidUnion uf;  // records: shared core point -- its local root
-        for (auto& s : sh)
-            for (int32_t p : s.shared) {
-                const int32_t r = s.root[p];
-                if (r >= 0) uf.unite(s.gid[p], s.gid[r]);
-            }
-        for (auto& s : sh) {
-            const int64_t m = (int64_t)s.gid.size();
-            s.gs.resize(m);  // (only the local roots' entries are read)
-            // the local roots by host threads (per-thread lists in slab order), then their global
-            // s(K) on this thread (the union-find compresses paths as it goes)
-            std::vector<std::vector<int32_t>> lr(nth);
-            parallel_for(nth, [&](int t) {
-                for (int64_t p = m * t / nth, p1 = m * (t + 1) / nth; p < p1; ++p)
-                    if (s.root[(size_t)p] == (int32_t)p) lr[t].push_back((int32_t)p);
-            });
-            for (auto& l : lr)
-                for (int32_t p : l) {
-                    const int64_t g = s.gid[(size_t)p], gs = uf.find(g);
-                    s.gs[(size_t)p] = gs;
-                    if (s.zone[(size_t)p] == 0 && gs == g) all_roots.push_back(g);
-                }
-            HostVec<int32_t>().swap(s.root);
-        }
-        std::sort(all_roots.begin(), all_roots.end());
-        tr.mark("merge + numbering");
-        each_device([&](int r, int w) {
-            shard_label(sh[r], hs[w], w, eps, min_points, all_roots, mode, shared_dev);
-        });
-        tr.mark("slab labels");
-        for (auto& s : sh)
-            if (s.rc != DBSCAN_OK && rc == DBSCAN_OK) {
-                rc = s.rc;
-                *err = s.err;
-            }
-    }
-    if (rc == DBSCAN_OK) {
-        // zone-0 points: each input point is owned by exactly one shard (disjoint writes)
-        parallel_for(nth, [&](int t) {
-            for (auto& s : sh) {
-                const int64_t m = (int64_t)s.gid.size(), p0 = m * t / nth, p1 = m * (t + 1) / nth;
-                for (int64_t p = p0; p < p1; ++p)
-                    if (s.zone[(size_t)p] == 0) {
-                        cluster_out[s.gid[(size_t)p]] = s.cluster[(size_t)p];
-                        flag_out[s.gid[(size_t)p]] = s.flag[(size_t)p];
+    const bool ok = [&]() {
+        // ---- A: plan + lean slab fits + records ----
+        if (!each_device([&](int w) {
+                hipStream_t st = static_cast<hipStream_t>(dbscan_stream(hs[w]));
+                double *dx = nullptr, *dy = nullptr;
+                int32_t* cnt = nullptr;
+                const int64_t nb = (n + kPlanTile - 1) / kPlanTile;
+                try {
+                    hcheck(hipMalloc(&dx, n * sizeof(double)), "upload");
+                    hcheck(hipMalloc(&dy, n * sizeof(double)), "upload");
+                    hcheck(hipMalloc(&cnt, (4 * nb + 4) * sizeof(int32_t)), "plan");
+                    hcheck(hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, st),
+                           "upload");
+                    hcheck(hipMemcpyAsync(dy, y, n * sizeof(double), hipMemcpyHostToDevice, st),
+                           "upload");
+                    int32_t* cs = cnt;
+                    int32_t* ch = cnt + nb;
+                    int32_t* os = cnt + 2 * nb;
+                    int32_t* oh = cnt + 3 * nb;
+                    int32_t* tot = cnt + 4 * nb;
+                    dbscan::Workspace scratch;  // (the scans' look-back state)
+                    for (int r = w; r < world; r += nworkers) {
+                        DevShard& s = sh[r];
+                        hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0,
+                                           st, dx, n, r, world, zc[r], cs, ch);
+                        hcheck(hipGetLastError(), "plan count");
+                        exclusive_scan(st, 0, cs, os, nb, tot, scratch.scan);
+                        exclusive_scan(st, 0, ch, oh, nb, tot + 1, scratch.scan);
+                        int32_t t2[2];
+                        hcheck(hipMemcpyAsync(t2, tot, sizeof(t2), hipMemcpyDeviceToHost, st),
+                               "plan");
+                        hcheck(hipStreamSynchronize(st), "plan");
+                        s.m = t2[0];
+                        s.ns = t2[1];
+                        const int64_t m = std::max<int64_t>(1, s.m);
+                        hcheck(hipMalloc(&s.x, m * sizeof(double)), "shard");
+                        hcheck(hipMalloc(&s.y, m * sizeof(double)), "shard");
+                        hcheck(hipMalloc(&s.zone, m), "shard");
+                        hcheck(hipMalloc(&s.core, m), "shard");
+                        hcheck(hipMalloc(&s.gid, m * sizeof(int64_t)), "shard");
+                        hcheck(hipMalloc(&s.gs, m * sizeof(int64_t)), "shard");
+                        hcheck(hipMalloc(&s.root, m * sizeof(int32_t)), "shard");
+                        hcheck(hipMalloc(&s.shared, std::max<int64_t>(1, s.ns) * sizeof(int64_t)),
+                               "shard");
+                        hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0,
+                                           st, dx, dy, n, r, world, zc[r], os, oh, s.x, s.y,
+                                           s.zone, s.gid, s.shared);
+                        hcheck(hipGetLastError(), "plan write");
+                        if (s.m == 0) continue;
+                        lean_fit(r, w);
+                        s.a.resize((size_t)s.ns);
+                        s.b.resize((size_t)s.ns);
+                        if (s.ns > 0) {
+                            int64_t* rec = nullptr;
+                            hcheck(hipMalloc(&rec, 2 * s.ns * sizeof(int64_t)), "records");
+                            hipLaunchKernelGGL(plan_records_kernel, dim3(nblocks(s.ns)),
+                                               dim3(kBlock), 0, st, s.shared, s.ns, s.gid, s.core,
+                                               s.root, rec, rec + s.ns);
+                            hcheck(hipMemcpyAsync(s.a.data(), rec, s.ns * sizeof(int64_t),
+                                                  hipMemcpyDeviceToHost, st), "records");
+                            hcheck(hipMemcpyAsync(s.b.data(), rec + s.ns, s.ns * sizeof(int64_t),
+                                                  hipMemcpyDeviceToHost, st), "records");
+                            hcheck(hipStreamSynchronize(st), "records");
+                            (void)hipFree(rec);
+                        }
+                        ccheck(dbscan_sync(hs[w]));
                     }
+                } catch (...) {
+                    (void)hipFree(dx);
+                    (void)hipFree(dy);
+                    (void)hipFree(cnt);
+                    throw;
+                }
+                (void)hipFree(dx);
+                (void)hipFree(dy);
+                (void)hipFree(cnt);
+            }))
+            return false;
+        tr.mark("plan + slab fits");
+        // ---- B: all records ----
+        std::vector<int64_t> A, B;
+        for (auto& s : sh) {
+            A.insert(A.end(), s.a.begin(), s.a.end());
+            B.insert(B.end(), s.b.begin(), s.b.end());
+            std::vector<int64_t>().swap(s.a);
+            std::vector<int64_t>().swap(s.b);
+        }
+        const int64_t nrec = (int64_t)A.size();
+        // ---- C: the union on every device, global s(K) per local root, owned roots ----
+        if (!each_device([&](int w) {
+                hipStream_t st = static_cast<hipStream_t>(dbscan_stream(hs[w]));
+                Dev& d = dv[w];
+                hcheck(hipMalloc(&d.parent, n * sizeof(int32_t)), "merge");
+                hcheck(hipMemsetAsync(d.parent, 0xFF, n * sizeof(int32_t), st), "merge");
+                hcheck(hipMalloc(&d.ra, std::max<int64_t>(1, nrec) * sizeof(int64_t)), "merge");
+                hcheck(hipMalloc(&d.rb, std::max<int64_t>(1, nrec) * sizeof(int64_t)), "merge");
+                if (nrec > 0) {
+                    hcheck(hipMemcpyAsync(d.ra, A.data(), nrec * sizeof(int64_t),
+                                          hipMemcpyHostToDevice, st), "merge");
+                    hcheck(hipMemcpyAsync(d.rb, B.data(), nrec * sizeof(int64_t),
+                                          hipMemcpyHostToDevice, st), "merge");
+                    ccheck(dbscan_merge_union_device(d.ra, d.rb, nrec, d.parent, st));
+                }
+                for (int r = w; r < world; r += nworkers) {
+                    DevShard& s = sh[r];
+                    if (s.m == 0) continue;
+                    int64_t* own = nullptr;
+                    hcheck(hipMalloc(&own, s.m * sizeof(int64_t)), "roots");
+                    int64_t k = 0;
+                    const int32_t rc2 = dbscan_slab_merge_roots_device(
+                        hs[w], s.m, s.zone, s.gid, s.root, d.parent, s.gs, own, &k);
+                    if (rc2 == DBSCAN_OK) {
+                        s.own.resize((size_t)k);
+                        const hipError_t e = k > 0 ? hipMemcpyAsync(s.own.data(), own,
+                                                                    k * sizeof(int64_t),
+                                                                    hipMemcpyDeviceToHost, st)
+                                                   : hipSuccess;
+                        const hipError_t e2 = hipStreamSynchronize(st);
+                        (void)hipFree(own);
+                        hcheck(e, "roots");
+                        hcheck(e2, "roots");
+                    } else {
+                        (void)hipFree(own);
+                        throw rc2;
+                    }
+                }
+                (void)hipFree(d.ra);
+                (void)hipFree(d.rb);
+                (void)hipFree(d.parent);
+                d.ra = d.rb = nullptr;
+                d.parent = nullptr;
+            }))
+            return false;
+        // ---- D: numbering ----
+        for (auto& s : sh) all_roots.insert(all_roots.end(), s.own.begin(), s.own.end());
+        std::sort(all_roots.begin(), all_roots.end());
+        nroots = (int64_t)all_roots.size();
+        tr.mark("merge + numbering");
+        // ---- E: labels ----
+        const bool one = nworkers == 1;
+        std::vector<std::vector<int32_t>> hcl(world);
+        std::vector<std::vector<uint8_t>> hfl(world);
+        std::vector<std::vector<int64_t>> hgid(world);
+        if (!each_device([&](int w) {
+                hipStream_t st = static_cast<hipStream_t>(dbscan_stream(hs[w]));
+                Dev& d = dv[w];
+                hcheck(hipMalloc(&d.roots, std::max<int64_t>(1, nroots) * sizeof(int64_t)), "label");
+                if (nroots > 0)
+                    hcheck(hipMemcpyAsync(d.roots, all_roots.data(), nroots * sizeof(int64_t),
+                                          hipMemcpyHostToDevice, st), "label");
+                if (one) {
+                    hcheck(hipMalloc(&d.out_cl, n * sizeof(int32_t)), "output");
+                    hcheck(hipMalloc(&d.out_fl, n), "output");
+                }
+                for (int r = w; r < world; r += nworkers) {
+                    DevShard& s = sh[r];
+                    if (s.m == 0) continue;
+                    if (shared_dev) lean_fit(r, w);  // (the handle's last fit was another shard's)
+                    int32_t* cl = nullptr;
+                    uint8_t* fl = nullptr;
+                    hcheck(hipMalloc(&cl, s.m * sizeof(int32_t)), "label");
+                    hcheck(hipMalloc(&fl, s.m), "label");
+                    const int32_t rc2 = dbscan_slab_label_device(hs[w], s.zone, s.gid, s.gs,
+                                                                 d.roots, nroots, mode, cl, fl);
+                    if (rc2 != DBSCAN_OK) {
+                        (void)hipFree(cl);
+                        (void)hipFree(fl);
+                        throw rc2;
+                    }
+                    if (one) {
+                        hipLaunchKernelGGL(plan_scatter_kernel, dim3(nblocks(s.m)), dim3(kBlock),
+                                           0, st, s.m, s.zone, s.gid, cl, fl, d.out_cl, d.out_fl);
+                        hcheck(hipGetLastError(), "label scatter");
+                    } else {  // several devices: the slab-order labels and gids back to the host
+                        hcl[r].resize((size_t)s.m);
+                        hfl[r].resize((size_t)s.m);
+                        hgid[r].resize((size_t)s.m);
+                        hcheck(hipMemcpyAsync(hcl[r].data(), cl, s.m * sizeof(int32_t),
+                                              hipMemcpyDeviceToHost, st), "label");
+                        hcheck(hipMemcpyAsync(hfl[r].data(), fl, s.m, hipMemcpyDeviceToHost, st),
+                               "label");
+                        hcheck(hipMemcpyAsync(hgid[r].data(), s.gid, s.m * sizeof(int64_t),
+                                              hipMemcpyDeviceToHost, st), "label");
+                    }
+                    hcheck(hipStreamSynchronize(st), "label");
+                    (void)hipFree(cl);
+                    (void)hipFree(fl);
+                    if (!one) {  // zone-0 flags of the slab for the host scatter
+                        std::vector<uint8_t> z((size_t)s.m);
+                        hcheck(hipMemcpy(z.data(), s.zone, s.m, hipMemcpyDeviceToHost), "label");
+                        for (int64_t p = 0; p < s.m; ++p)
+                            if (z[(size_t)p] != 0) hgid[r][(size_t)p] = -1;
+                    }
+                    s.release();
+                }
+                if (one) {
+                    hcheck(hipMemcpyAsync(cluster_out, d.out_cl, n * sizeof(int32_t),
+                                          hipMemcpyDeviceToHost, st), "output");
+                    hcheck(hipMemcpyAsync(flag_out, d.out_fl, n, hipMemcpyDeviceToHost, st),
+                           "output");
+                    hcheck(hipStreamSynchronize(st), "output");
+                }
+                (void)hipFree(d.roots);
+                (void)hipFree(d.out_cl);
+                (void)hipFree(d.out_fl);
+                d.roots = nullptr;
+                d.out_cl = nullptr;
+                d.out_fl = nullptr;
+            }))
+            return false;
+        tr.mark("slab labels + output");
+        if (!one) {  // host scatter of every shard's zone-0 labels (disjoint writes)
+            const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / 65536 + 1));
+            parallel_for(nth, [&](int t) {
+                for (int r = 0; r < world; ++r) {
+                    const int64_t m = (int64_t)hgid[r].size(), p0 = m * t / nth,
+                                  p1 = m * (t + 1) / nth;
+                    for (int64_t p = p0; p < p1; ++p) {
+                        const int64_t g = hgid[r][(size_t)p];
+                        if (g < 0) continue;
+                        cluster_out[g] = hcl[r][(size_t)p];
+                        flag_out[g] = hfl[r][(size_t)p];
+                    }
+                }
+            });
+            tr.mark("output scatter");
+        }
+        return true;
+    }();
+    if (!ok) {
+        for (auto& d : dv)
+            if (d.rc != DBSCAN_OK) {
+                rc = d.rc;
+                *err = d.err;
+                break;
             }
-        });
-        *n_clusters_out = (int64_t)all_roots.size();
-        tr.mark("output scatter");
+        if (rc == DBSCAN_OK) rc = DBSCAN_EHIP;
+    }
+    for (int w = 0; w < nworkers; ++w) {
+        (void)hipSetDevice(w);
+        Dev& d = dv[w];
+        for (void* p : {(void*)d.parent, (void*)d.ra, (void*)d.rb, (void*)d.roots,
+                        (void*)d.out_cl, (void*)d.out_fl})
+            (void)hipFree(p);
+        for (int r = w; r < world; r += nworkers) sh[r].release();
     }
     for (auto* h : hs) dbscan_destroy(h);
+    if (rc == DBSCAN_OK) *n_clusters_out = nroots;
     tr.mark("teardown");
     return rc;
 }
