@@ -1389,14 +1389,28 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
 // ~10^5 takes the exact path).
 // ---------------------------------------------------------------------------------------
 struct F32Cut {
-    float lo, hi;
+    float lo, hi;  // F <= lo: a neighbour; F > hi: not; otherwise the exact fp64 predicate
+    float ne2;     // -fl32(e2), for the count's signed form (count_d below)
 };
 
 __device__ __forceinline__ F32Cut f32_cut(const GridParams& g, double eps2) {
     const double s = 0.5 * g.invx;  // 1 / h
     const double e2 = eps2 * s * s;
-    return {__double2float_rd(e2 - 0x1p-14), __double2float_ru(e2 + 0x1p-14)};
+    return {__double2float_rd(e2 - 0x1p-14), __double2float_ru(e2 + 0x1p-14), -(float)e2};
 }
+
+// The count's signed form of the same test (count_tile32_kernel): D = fl(dx*dx + fl(dy*dy -
+// fl32(e2))), two fused steps.  D differs from F - e2 by at most the two roundings (|dx|, |dy|
+// <= 3 cells inside the stencil: 2^-21 each) plus |fl32(e2) - e2| <= 2^-24 (e2 ~ 1 on clique
+// grids), all far below the margin M = 2^-14 around the F bound of 1.6e-5: |D| > M means F is
+// outside [lo, hi] on the same side, so D < 0 <=> a neighbour, exactly as F <= lo; |D| <= M
+// takes the exact fp64 predicate (a superset of the F band).
+constexpr float kCountBand = 0x1p-14f;
+__device__ __forceinline__ float count_d(float2 me, float2 q, float ne2) {
+    const float dx = q.x - me.x, dy = q.y - me.y;
+    return __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, ne2));
+}
+__device__ __forceinline__ uint32_t sign_of(float d) { return __float_as_uint(d) >> 31; }
 
 // LDS index -> global slot of a staged tile (largest extended cell k with off[k] <= q)
 __device__ __forceinline__ int stage_slot(const TileStage& st, int q) {
@@ -1682,26 +1696,19 @@ __device__ __forceinline__ bool stage_build_own32(const StageMeta& m,
 }
 
 // One LDS range [b, e) of candidates for the count, in batches of 4 (the last one masked), early
-// exit at minPoints.  Per candidate: F <= lo counts (a sure hit), F <= hi counts into a second
-// sum; a batch whose two sums differ holds an ambiguous candidate and is recounted with the
-// exact fp64 predicate (exact(q), LDS index q).  REC: each batch with hits is noted as ONE 16-bit
-// record (first LDS index | range tag << 11 | (candidates - 1) << 13) in the thread's column of
-// lst while fewer than nbr_k records exist; a point that ends below minPoints has at most
-// minPoints - 1 hits, so its records are complete.  The hits themselves are re-derived from the
-// records (the same tests) only for the non-cores' neighbour lists.
-__device__ __forceinline__ int hits_of(float F, F32Cut cut) { return F <= cut.lo ? 1 : 0; }
-__device__ __forceinline__ int maybe_of(float F, F32Cut cut) { return F <= cut.hi ? 1 : 0; }
-
-// a batch's hits when one of its candidates is ambiguous (F0..F3: its first nin candidates)
+// exit at minPoints.  Per candidate the signed distance D (count_d): the batch's hits are the
+// sign bits of its D's, and a batch whose smallest |D| is inside the band is recounted with the
+// exact fp64 predicate on its band members (exact(q), LDS index q).  REC: each batch with hits
+// is noted as ONE 16-bit record (first LDS index | range tag << 11 | (candidates - 1) << 13) in
+// the thread's column of lst while fewer than nbr_k records exist; a point that ends below
+// minPoints has at most minPoints - 1 hits, so its records are complete.  The hits themselves are
+// re-derived from the records (the same tests) only for the non-cores' neighbour lists.
+// (Per candidate: one packed subtract and two FMAs; per batch: the band test and the sign-bit
+// sum -- about half the VALU of a compare / select per bound, the count phase being VALU-bound
+// while every wave of a CU scans.)
 template <class ExactF>
-__device__ __forceinline__ int exact_hits(float F0, float F1, float F2, float F3, int nin, int j,
-                                       F32Cut cut, ExactF exact) {
-    const float F[4] = {F0, F1, F2, F3};
-    int h = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-        if (u < nin) h += (F[u] <= cut.lo || (F[u] <= cut.hi && exact(j + u))) ? 1 : 0;
-    return h;
+__device__ __forceinline__ bool hit_of(float d, int q, ExactF exact) {
+    return fabsf(d) > kCountBand ? d < 0.0f : exact(q);
 }
 
 template <class ExactF>
@@ -1711,16 +1718,13 @@ __device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int 
                                             ExactF exact) {
     int j = b;
     for (; j + 4 <= e; j += 4) {
-        float F[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) F[u] = f32_d2(me, buf[j + u]);
-        int h = 0, a = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            h += hits_of(F[u], cut);
-            a += maybe_of(F[u], cut);
-        }
-        if (__builtin_expect(a != h, 0)) h = exact_hits(F[0], F[1], F[2], F[3], 4, j, cut, exact);
+        const float d0 = count_d(me, buf[j], cut.ne2), d1 = count_d(me, buf[j + 1], cut.ne2);
+        const float d2 = count_d(me, buf[j + 2], cut.ne2), d3 = count_d(me, buf[j + 3], cut.ne2);
+        int h = (int)(sign_of(d0) + sign_of(d1) + sign_of(d2) + sign_of(d3));
+        const float mn = fminf(fminf(fabsf(d0), fabsf(d1)), fminf(fabsf(d2), fabsf(d3)));
+        if (__builtin_expect(mn <= kCountBand, 0))
+            h = (int)hit_of(d0, j, exact) + (int)hit_of(d1, j + 1, exact) +
+                (int)hit_of(d2, j + 2, exact) + (int)hit_of(d3, j + 3, exact);
         if (h && nrec < nbr_k) {
             lst[nrec * kBlock] = (uint16_t)(j | (tag << 11) | (3 << 13));
             ++nrec;
@@ -1730,16 +1734,16 @@ __device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int 
     }
     if (j < e) {  // the last 1-3 candidates: the batch reads past e (inside LDS), masked
         const int nin = e - j;
-        float F[4];
+        float d[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) F[u] = f32_d2(me, buf[j + u]);
-        int h = 0, a = 0;
+        for (int u = 0; u < 4; ++u) d[u] = u < nin ? count_d(me, buf[j + u], cut.ne2) : 1.0f;
+        int h = (int)(sign_of(d[0]) + sign_of(d[1]) + sign_of(d[2]) + sign_of(d[3]));
+        const float mn = fminf(fminf(fabsf(d[0]), fabsf(d[1])), fminf(fabsf(d[2]), fabsf(d[3])));
+        if (__builtin_expect(mn <= kCountBand, 0)) {
+            h = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            h += u < nin ? hits_of(F[u], cut) : 0;
-            a += u < nin ? maybe_of(F[u], cut) : 0;
+            for (int u = 0; u < 4; ++u) h += (u < nin && hit_of(d[u], j + u, exact)) ? 1 : 0;
         }
-        if (__builtin_expect(a != h, 0)) h = exact_hits(F[0], F[1], F[2], F[3], nin, j, cut, exact);
         if (h && nrec < nbr_k) {
             lst[nrec * kBlock] = (uint16_t)(j | (tag << 11) | ((nin - 1) << 13));
             ++nrec;
@@ -1799,6 +1803,7 @@ __device__ __forceinline__ int pairs44(const Cores4& a, const Cores4& b, F32Cut 
 
 struct UnionLds32 {  // aliases the count's neighbour records (the two never overlap in time)
     int lp[kMaxTileQ];           // LDS union-find over the tile's quarters
+    uint8_t comp[kMaxTileQ];     // each core quarter's component after the adjacent unions
     uint32_t lrange[kMaxTileQ];  // LDS begin | length << 11 | local quarter (16 y + x) << 22;
                                  // bit 31: holds cores
     uint32_t lmask[kMaxTileQ];   // cores among the first 32 points
@@ -1912,10 +1917,18 @@ __device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e
     }
     lds_barrier();
     AB_STAMP(6);
-    // the adjacent pairs joined every core of the tile: no distance-2 pair can add an edge
+    // each core quarter's component after the adjacent pairs, once; if they joined every core
+    // of the tile, no distance-2 pair can add an edge
     const int f = s_first;
-    const bool split = i < nq && rep >= 0 && lfind(u.lp, i) != lfind(u.lp, f);
+    int ci = -1;
+    if (i < nq && rep >= 0) {
+        ci = lfind(u.lp, i);
+        u.comp[i] = ci;
+    }
+    const bool split = ci >= 0 && ci != lfind(u.lp, f);
     if (__syncthreads_or(split)) {
+        // distance-2 pairs between quarters of different components (the snapshot above: a
+        // pair joined meanwhile by another distance-2 union is only tested again)
         for (int k = i; k < nq * 8; k += kBlock) {
             const int o = k / nq, qi = k - o * nq;
             const uint32_t ri = u.lrange[qi];
@@ -1927,7 +1940,7 @@ __device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e
             if (j == 0xFFFF) continue;
             const uint32_t rj = u.lrange[j];
             if (!(rj >> 31)) continue;
-            if (lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+            if (u.comp[qi] == u.comp[j]) continue;
             const uint32_t mi = u.lmask[qi];
             if (touch(cores4(buf, ri, mi, 1.0f), ri, mi, rj, u.lmask[j])) lunite(u.lp, qi, j);
         }
@@ -2050,8 +2063,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                         const int k0 = (ly + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + lx;
                         for (int uu = 0; uu < nin; ++uu) {
                             const int qq = q + uu;
-                            const float F = f32_d2(me, buf[qq]);
-                            if (!(F <= cut.lo || (F <= cut.hi && exact(qq)))) continue;
+                            if (!hit_of(count_d(me, buf[qq], cut.ne2), qq, exact)) continue;
                             const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
                                           (qq >= st.off[k0 + 2] ? 1 : 0);
                             const int sq = st.cb[c] + (qq - st.off[c]);
