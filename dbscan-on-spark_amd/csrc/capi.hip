@@ -499,6 +499,29 @@ int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double ep
     });
 }
 
+int64_t dbscan_route_slabs_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                                  int64_t m, int64_t start, const double* cuts, int32_t n_cuts,
+                                  double eps, int64_t* d_rows, int64_t capacity,
+                                  int64_t* counts_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    int64_t total = 0;
+    const int32_t rc = guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (m < 0 || start < 0 || n_cuts < 0 || !counts_out || (n_cuts > 0 && !cuts) ||
+            (m > 0 && (!d_x || !d_y)) || capacity < 0)
+            throw dbscan::ArgError{"bad routing arguments"};
+        if (!std::isfinite(eps * eps)) throw dbscan::ArgError{"eps*eps must be finite to shard"};
+        settle(h);
+        total = dbscan::route_slabs(h->stream, h->ws.route, h->ws.route_tab, d_x, d_y, m, start,
+                                    cuts, n_cuts, eps, d_rows, capacity, counts_out);
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? total : rc;
+}
+
 }  // extern "C"
 
 namespace {

@@ -173,7 +173,7 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm;
+        key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, route, route_tab;
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
@@ -188,7 +188,8 @@ struct Workspace {
                           &qstart, &qrep, &qmask, &blockcnt, &heads, &tkey, &tstart, &tmap, &tslot,
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &lroots,
-                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm})
+                          &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm, &route,
+                          &route_tab})
             b->release();
     }
 };
@@ -363,6 +364,10 @@ int64_t scala_range_count(double start, double end, double step, bool inclusive)
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
                    int64_t* n_clusters_out, std::string* err);
+// Node-path routing (node.hip, dbscan_route_slabs_device): see include/dbscan_hip.h.
+int64_t route_slabs(hipStream_t s, DevBuf& scratch, DevBuf& tabbuf, const double* x,
+                    const double* y, int64_t m, int64_t start, const double* cuts, int32_t n_cuts,
+                    double eps, int64_t* rows, int64_t capacity, int64_t* counts_out);
 // Node-path merge (merge.hip): every local root's global s(K) (gs_of_root, slab index) and the
 // zone-0 global roots owned here, compacted in slab (= gid) order; returns their count (syncs).
 int64_t run_slab_merge_roots(hipStream_t s, Workspace& ws, int64_t n, const uint8_t* zone,

@@ -316,6 +316,86 @@ __global__ __launch_bounds__(kBlock) void plan_scatter_kernel(
 
 unsigned nblocks(int64_t m) { return (unsigned)std::max<int64_t>(1, (m + kBlock - 1) / kBlock); }
 
+// ---- the node path's host-to-slab routing (node.py NodeJob.from_chunk) ------------------
+// Every point of a rank's input chunk goes to each slab whose zones 0/1/2 hold it, as a 24-B row
+// (x bits, y bits, gid * 8 + zone * 2 + shared), rows grouped by destination rank, ascending gid
+// within each.  One count pass (per block and destination), one scan over the [dest][block]
+// counts, one ballot-ranked write pass: every destination's rows in one kernel pass each.
+constexpr int kRouteTile = 4096;  // points per block (16 rounds of 256)
+constexpr int kRouteMaxWorld = 64;
+
+__global__ __launch_bounds__(kBlock) void route_count_kernel(const double* __restrict__ x,
+                                                             int64_t m, int world,
+                                                             const ZoneCut* __restrict__ zc,
+                                                             int32_t* __restrict__ cnt) {
+    __shared__ int c[kRouteMaxWorld];
+    for (int d = threadIdx.x; d < world; d += kBlock) c[d] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kRouteTile;
+    for (int k = 0; k < kRouteTile / kBlock; ++k) {
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        if (i >= m) break;
+        const double xi = x[i];
+        for (int d = 0; d < world; ++d) {
+            bool sh = false;
+            if (zone_of(xi, d, world, zc[d], &sh) != kOut) atomicAdd(&c[d], 1);
+        }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < world; d += kBlock) cnt[(int64_t)d * gridDim.x + blockIdx.x] = c[d];
+}
+
+__global__ __launch_bounds__(kBlock) void route_write_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, int64_t m, int64_t start,
+    int world, const ZoneCut* __restrict__ zc, const int32_t* __restrict__ off,
+    int64_t* __restrict__ rows) {
+    __shared__ int wc[2][kRouteMaxWorld][kBlock / 64];
+    __shared__ int base_d[kRouteMaxWorld];
+    const int nb = gridDim.x;
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int d = threadIdx.x; d < world; d += kBlock) base_d[d] = off[(int64_t)d * nb + blockIdx.x];
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kRouteTile;
+    for (int k = 0; k < kRouteTile / kBlock; ++k) {
+        if (base + k * kBlock >= m) break;  // (block-uniform)
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        double xi = 0, yi = 0;
+        if (i < m) {
+            xi = x[i];
+            yi = y[i];
+        }
+        for (int d = 0; d < world; ++d) {
+            bool sh = false;
+            const uint8_t z = i < m ? zone_of(xi, d, world, zc[d], &sh) : kOut;
+            const uint64_t b = __ballot(z != kOut);
+            if (lane == 0) wc[k & 1][d][w] = __popcll(b);
+        }
+        __syncthreads();
+        for (int d = 0; d < world; ++d) {
+            bool sh = false;
+            const uint8_t z = i < m ? zone_of(xi, d, world, zc[d], &sh) : kOut;
+            const uint64_t b = __ballot(z != kOut);
+            int before = 0, total = 0;
+#pragma unroll
+            for (int v = 0; v < kBlock / 64; ++v) {
+                const int c = wc[k & 1][d][v];
+                before += v < w ? c : 0;
+                total += c;
+            }
+            if (z != kOut) {
+                const int64_t q = (int64_t)base_d[d] + before + __popcll(b & lt);
+                rows[3 * q] = (int64_t)__double_as_longlong(xi);
+                rows[3 * q + 1] = (int64_t)__double_as_longlong(yi);
+                rows[3 * q + 2] = (start + i) * 8 + (int64_t)z * 2 + (sh ? 1 : 0);
+            }
+            __syncthreads();  // (every thread has read base_d[d] before it advances)
+            if (threadIdx.x == 0) base_d[d] += total;
+        }
+        __syncthreads();
+    }
+}
+
 // A shard on its device: the slab (x, y, zone, gid in increasing gid), its shared points, the
 // slab fit's outputs and each local root's global s(K).
 struct DevShard {
@@ -351,6 +431,54 @@ inline void ccheck(int32_t rc) {
 }
 
 }  // namespace
+
+// Routing of one chunk (see route_write_kernel): counts_out[d] = rows for rank d; rows written
+// when rows != nullptr and capacity (rows) suffices.  Returns the total row count.
+int64_t route_slabs(hipStream_t s, DevBuf& scratch, DevBuf& tabbuf, const double* x,
+                    const double* y, int64_t m, int64_t start, const double* cuts, int32_t n_cuts,
+                    double eps, int64_t* rows, int64_t capacity, int64_t* counts_out) {
+    const int world = n_cuts + 1;
+    if (world > kRouteMaxWorld) throw ArgError{"route: more than 64 slabs"};
+    for (int d = 0; d < world; ++d) counts_out[d] = 0;
+    if (m == 0) return 0;
+    const std::vector<double> cv(cuts, cuts + n_cuts);
+    const std::vector<ZoneCut> zc = zone_cuts(world, cv, reach(eps));
+    ZoneCut* dzc = static_cast<ZoneCut*>(tabbuf.ensure(world * sizeof(ZoneCut)));
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(dzc, zc.data(), world * sizeof(ZoneCut), hipMemcpyHostToDevice, s));
+    const int64_t nb = (m + kRouteTile - 1) / kRouteTile;
+    int32_t* cnt = static_cast<int32_t*>(scratch.ensure((2 * nb * world + 8) * sizeof(int32_t)));
+    int32_t* off = cnt + nb * world;
+    hipLaunchKernelGGL(route_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, x, m, world,
+                       dzc, cnt);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    // per destination: the sum of its blocks (host), then one scan for the offsets
+    std::vector<int32_t> hc((size_t)(nb * world));
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(hc.data(), cnt, hc.size() * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    int64_t total = 0;
+    for (int d = 0; d < world; ++d) {
+        int64_t c = 0;
+        for (int64_t b = 0; b < nb; ++b) c += hc[(size_t)(d * nb + b)];
+        counts_out[d] = c;
+        total += c;
+    }
+    if (!rows || capacity < total) return total;
+    if (total >= (int64_t)INT32_MAX) throw ArgError{"route: more than 2^31 rows"};
+    std::vector<int32_t> ho((size_t)(nb * world));
+    int64_t run = 0;
+    for (size_t k = 0; k < ho.size(); ++k) {
+        ho[k] = (int32_t)run;
+        run += hc[k];
+    }
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(off, ho.data(), ho.size() * sizeof(int32_t),
+                                    hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(route_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, x, y, m, start,
+                       world, dzc, off, rows);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));  // (the host vectors go out of scope)
+    return total;
+}
 
 // dbscan_train_node: the slab plan, the slab fits, the merge and the labels all on the
 // devices (round 4; rounds 1-3 built the plan and merged on the host: 16.9 s for 10^9 points on

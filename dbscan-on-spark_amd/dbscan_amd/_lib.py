@@ -68,6 +68,8 @@ SIGNATURES = [
     ("dbscan_fit_batch_device_async", _i32,
      [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_duplicate", _i64, [_vp, _vp, _i64, _vp, _i64, _d, _vp, _vp, _i64]),
+    ("dbscan_route_slabs_device", _i64, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _d, _vp, _i64,
+                                         _vp]),
 ]
 SMALL_MAX_POINTS = 8192  # DBSCAN_SMALL_MAX_POINTS
 

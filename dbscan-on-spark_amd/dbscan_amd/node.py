@@ -264,6 +264,28 @@ class HipSlabOps:
         self._from_handle()
         return core, root
 
+    def route(self, x, y, start, cuts, eps):
+        """from_chunk's rows (dbscan_route_slabs_device): (rows int64[k, 3], counts per rank)."""
+        import numpy as np
+
+        L = _lib.load()
+        m = x.numel()
+        c = np.ascontiguousarray(cuts, dtype=np.float64)
+        counts = np.zeros(len(cuts) + 1, np.int64)
+        self._to_handle()
+        vp = ctypes.c_void_p
+        args = (self.h.ptr, _p(x), _p(y), m, int(start), c.ctypes.data_as(vp), len(cuts),
+                float(eps))
+        total = L.dbscan_route_slabs_device(*args, None, 0, counts.ctypes.data_as(vp))
+        if total < 0:
+            _lib.check(int(total))
+        rows = torch.empty((max(1, total), 3), dtype=torch.int64, device=x.device)
+        got = L.dbscan_route_slabs_device(*args, _p(rows), total, counts.ctypes.data_as(vp))
+        if got < 0:
+            _lib.check(int(got))
+        self._from_handle()
+        return rows[:total], [int(v) for v in counts]
+
     @staticmethod
     def _stream():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -325,7 +347,7 @@ class NodeJob:
     """One rank's share of a whole-node fit.  run() is one step (timed by bench.py)."""
 
     def __init__(self, x, y, zone, gid, shared, eps, min_points, mode, comm: Comm, ops,
-                 n_total: int):
+                 n_total: int, sh_idx=None):
         self.x, self.y, self.zone, self.gid, self.shared = x, y, zone, gid, shared
         self.eps, self.min_points, self.mode = float(eps), int(min_points), int(mode)
         self.comm, self.ops = comm, ops
@@ -335,7 +357,7 @@ class NodeJob:
         # Static per job: the shared points (slab indices), the a-side of every rank's records
         # and the record counts, so each step exchanges only the b-side at known sizes.
         dev = x.device
-        self.sh_idx = torch.nonzero(shared).flatten()
+        self.sh_idx = torch.nonzero(shared).flatten() if sh_idx is None else sh_idx
         a = gid[self.sh_idx]
         self.rec_sizes = comm.sizes(a.numel())
         self.all_a = comm.allgather_fixed(a, self.rec_sizes)
@@ -381,11 +403,38 @@ class NodeJob:
         world = comm.world
         m = x.numel()
         dev = x.device
+        if comm._local():  # one rank, nothing to route: the chunk is the whole slab, all owned
+            job = cls(x.contiguous(), y.contiguous(), torch.zeros(m, dtype=torch.uint8, device=dev),
+                      torch.arange(start, start + m, dtype=torch.int64, device=dev),
+                      torch.zeros(m, dtype=torch.bool, device=dev), eps, min_points, mode, comm,
+                      ops, n_total, sh_idx=torch.zeros(0, dtype=torch.int64, device=dev))
+            job.cuts = []
+            return job
         xf = x[torch.isfinite(x)]
         per = max(1, sample // world)
         smp = xf[::max(1, xf.numel() // per)][:per].contiguous()
         allx = comm.allgather_varlen(smp)
         cuts = make_cuts(allx, world, eps, sample=max(1, allx.numel()))
+        if x.is_cuda and cuts and hasattr(ops, "route"):
+            # one kernel pass per direction: every destination's rows, grouped and ordered
+            rows, counts = ops.route(x, y, start, cuts, eps)
+        else:
+            rows, counts = cls._route_torch(x, y, start, cuts, eps, world)
+        recv = comm.alltoall_rows(rows, counts)
+        code = recv[:, 2].contiguous()
+        job = cls(recv[:, 0].contiguous().view(torch.float64),
+                  recv[:, 1].contiguous().view(torch.float64),
+                  ((code >> 1) & 3).to(torch.uint8), code >> 3, (code & 1) != 0, eps,
+                  min_points, mode, comm, ops, n_total)
+        job.cuts = cuts
+        return job
+
+    @staticmethod
+    def _route_torch(x, y, start, cuts, eps, world):
+        """from_chunk's rows by torch ops (host tensors: the gloo tests' path; device tensors go
+        through ops.route, the HIP kernels of dbscan_route_slabs_device)."""
+        m = x.numel()
+        dev = x.device
         gid = torch.arange(start, start + m, dtype=torch.int64, device=dev)
         xb, yb = x.contiguous().view(torch.int64), y.contiguous().view(torch.int64)
         recs, counts = [], []
@@ -399,19 +448,14 @@ class NodeJob:
             code = gid[idx] * 8 + z[idx].long() * 2 + sh[idx].long()
             recs.append(torch.stack([xb[idx], yb[idx], code], 1))
             counts.append(int(idx.numel()))
-        recv = comm.alltoall_rows(torch.cat(recs), counts)
-        code = recv[:, 2].contiguous()
-        job = cls(recv[:, 0].contiguous().view(torch.float64),
-                  recv[:, 1].contiguous().view(torch.float64),
-                  ((code >> 1) & 3).to(torch.uint8), code >> 3, (code & 1) != 0, eps,
-                  min_points, mode, comm, ops, n_total)
-        job.cuts = cuts
-        return job
+        return torch.cat(recs), counts
 
     def chunk_labels(self, start: int, m: int, bounds: List[int]):
         """The labels of the chunk [start, start + m) this rank holds, in input order: every
         rank sends its owned (gid, cluster, flag) to the chunk owner (one all_to_all), which
         scatters them into place.  Returns (cluster int32[m], flag uint8[m]) on the device."""
+        if self.comm._local():  # one rank: the slab is the chunk, in order, every point owned
+            return self.cluster, self.flag
         gid, cl, fl = self.owned()
         dev = gid.device
         b = torch.tensor(bounds[1:-1], dtype=torch.int64, device=dev)

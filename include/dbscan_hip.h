@@ -329,6 +329,20 @@ int32_t dbscan_slab_label_finish_device_async(dbscan_handle* h, const uint8_t* d
                                               const int64_t* d_all_roots, int64_t n_all_roots,
                                               int32_t* d_cluster, uint8_t* d_flag);
 
+/* Host-to-slab routing of the node path (dbscan_amd/node.py NodeJob.from_chunk; the point
+ * duplication of DBSCAN.scala:116-137 for x-slabs): a rank holds the chunk [start, start + m)
+ * of the global input (device arrays, global visit order); every point goes to each of the
+ * n_cuts + 1 slabs (x < cuts[0], [cuts[0], cuts[1]), ...; at most 64) whose zone 0/1/2 holds it
+ * (node.py zones(): owned, within eps-reach of the slab, within twice that).  Rows of three
+ * int64: (x bits, y bits, gid * 8 + zone * 2 + shared), grouped by destination slab, ascending
+ * gid within each.  counts_out[d] (host, n_cuts + 1 entries) = rows for slab d.  d_rows NULL or
+ * capacity (rows) below the total: counts only.  Returns the total row count (< 0: error).
+ * Synchronizes the handle's stream. */
+int64_t dbscan_route_slabs_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                                  int64_t m, int64_t start, const double* cuts, int32_t n_cuts,
+                                  double eps, int64_t* d_rows, int64_t capacity,
+                                  int64_t* counts_out);
+
 /* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
  * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the
  * visit order.  Writes d_x, d_y (device).  Used by bench.py so 10^7..10^9 points need no PCIe. */

@@ -327,3 +327,46 @@ def test_two_part_slab_label_matches_one_part(mode):
         h.ptr, node._p(sz), node._p(gs), node._p(roots), 1, node._p(cl), node._p(fl))
     assert rc == _lib.DBSCAN_EARG
     h.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_route_kernel_equals_torch_zones(world):
+    """dbscan_route_slabs_device (HipSlabOps.route, the HIP routing of NodeJob.from_chunk) against
+    the torch restatement of node.py zones() (_route_torch): the same rows (x bits, y bits,
+    gid * 8 + zone * 2 + shared) in the same order and the same per-rank counts, on a chunk with
+    NaN / inf coordinates, points exactly on the cuts and within ulps of the halo margins, and
+    cuts that coincide (empty slabs)."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import node
+
+    rng = np.random.default_rng(world)
+    n, start, eps = 300_000, 12_345, 2.55
+    x, y = gen_blobs(n, noise=0.2, seed=world)
+    xs = np.sort(x[np.isfinite(x)])
+    cuts = [float(np.floor(xs[k * xs.size // world] / (2 * eps)) * 2 * eps) for k in range(1, world)]
+    if world == 8:
+        cuts[3] = cuts[2]  # an empty slab
+    R = node.reach(eps)
+    special = []
+    for c in cuts:
+        m1, m2 = node.margin1(c, R), node.margin2(c, R)
+        for v in (c, c - m1, c + m1, c - m2, c + m2):
+            special += [v, np.nextafter(v, -np.inf), np.nextafter(v, np.inf)]
+    k = len(special)
+    x[:k] = special
+    x[k:k + 5] = [np.nan, np.inf, -np.inf, np.nan, 0.0]
+    y[k + 5] = np.nan
+    x = x[rng.permutation(n)]
+    h = dbscan_amd.Handle(0)
+    ops = node.HipSlabOps(h)
+    try:
+        tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+        rows, counts = ops.route(tx, ty, start, cuts, eps)
+        trows, tcounts = node.NodeJob._route_torch(tx, ty, start, cuts, eps, world)
+        assert counts == tcounts
+        assert torch.equal(rows, trows)
+    finally:
+        ops.close()
+        h.close()
