@@ -248,6 +248,17 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
 // (cache-resident while the launch sweeps the bands in order), coalesced writes.
 // Slab fits: zs[p] = the slot's zone (from the record), and for the listed shared points
 // sinv[i] = their slot (a scattered write per shared point only).
+#ifndef DBSCAN_AB_XCD_GATHER
+#define DBSCAN_AB_XCD_GATHER 0
+#endif
+// (A/B) block index with each XCD given a contiguous range of the grid (see xcd_block below)
+__device__ __forceinline__ int64_t gather_block() {
+    if (!DBSCAN_AB_XCD_GATHER) return blockIdx.x;
+    const int G = gridDim.x, b = blockIdx.x;
+    const int x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
+    return x * q + (x < r ? x : r) + j;
+}
+
 __global__ __launch_bounds__(kBlock) void gather_bucket_kernel(int64_t n,
                                                                const int32_t* __restrict__ place,
                                                                const double4* __restrict__ rec,
@@ -256,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void gather_bucket_kernel(int64_t n,
                                                                double2* __restrict__ xy,
                                                                uint8_t* __restrict__ zs,
                                                                int32_t* __restrict__ sinv) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t p = gather_block() * kBlock + threadIdx.x;
     if (p >= n) return;
     const double4 r = rec[place[p]];
     const int32_t i = (int32_t)__double_as_longlong(r.z);
@@ -1484,51 +1495,6 @@ __device__ bool stage_build32(const StageMeta& m, const double2* __restrict__ xy
     return st.ok;
 }
 
-// One LDS range of candidates in batches of kScanBatch (the last batch masked).  Sure hits by F <= lo,
-// ambiguous ones by the exact fp64 predicate (exact(q) for LDS index q).  REC: each batch with
-// hits is noted as ONE record (first LDS index | range tag << 11 | hit bits << 16) in the
-// thread's column of lst while fewer than nbr_k records exist; a point that ends below
-// minPoints has at most minPoints - 1 hits, so its records are complete.
-// Candidates per batch: 4, the batch's tail clamped and masked once (round 2: against 8 with
-// a per-candidate select, count_wave + count_tiny 0.092 -> 0.087 ms at 10^7, 0.256 -> 0.236
-// on config 3's share; 8 in this form spilled at 80 VGPRs).
-constexpr int kScanBatch = 4;
-template <bool REC, int STRIDE = kBlock, class ExactF>
-__device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
-                                             float2 me, F32Cut cut, int min_points, int& cnt,
-                                             uint32_t* lst, int& nrec, int nbr_k, int tag,
-                                             ExactF exact) {
-    for (int j = b; j < e; j += kScanBatch) {
-        const int nin = e - j;
-        float2 qq[kScanBatch];
-#pragma unroll
-        for (int u = 0; u < kScanBatch; ++u) qq[u] = buf[min(j + u, e - 1)];  // tail masked below
-        uint32_t hm = 0, am = 0;
-#pragma unroll
-        for (int u = 0; u < kScanBatch; ++u) {
-            const float F = f32_d2(me, qq[u]);
-            hm |= F <= cut.lo ? (1u << u) : 0u;
-            am |= F <= cut.hi ? (1u << u) : 0u;
-        }
-        const uint32_t valid = nin >= kScanBatch ? (1u << kScanBatch) - 1u : (1u << nin) - 1u;
-        hm &= valid;
-        am = (am & valid) ^ hm;
-        if (__builtin_expect(am != 0, 0)) {
-            for (uint32_t m = am; m; m &= m - 1) {
-                const int u = __ffs(m) - 1;
-                if (exact(j + u)) hm |= 1u << u;
-            }
-        }
-        if (REC && hm && nrec < nbr_k) {
-            lst[nrec * STRIDE] = (uint32_t)j | ((uint32_t)tag << 11) | (hm << 16);
-            ++nrec;
-        }
-        cnt += __popc(hm);
-        if (cnt >= min_points) return true;
-    }
-    return cnt >= min_points;
-}
-
 // Is there an eps pair between a core of quarter A and a core of quarter B (LDS ranges)?
 template <class CoreF, class ExactF>
 __device__ __forceinline__ bool quarters_touch32(const float2* __restrict__ buf, int ab, int ae,
@@ -1711,10 +1677,10 @@ __device__ __forceinline__ bool hit_of(float d, int q, ExactF exact) {
     return fabsf(d) > kCountBand ? d < 0.0f : exact(q);
 }
 
-template <class ExactF>
+template <int STRIDE = kBlock, class RecT = uint16_t, class ExactF>
 __device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int b, int e,
                                             float2 me, F32Cut cut, int min_points, int& cnt,
-                                            uint16_t* lst, int& nrec, int nbr_k, int tag,
+                                            RecT* lst, int& nrec, int nbr_k, int tag,
                                             ExactF exact) {
     int j = b;
     for (; j + 4 <= e; j += 4) {
@@ -1726,7 +1692,7 @@ __device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int 
             h = (int)hit_of(d0, j, exact) + (int)hit_of(d1, j + 1, exact) +
                 (int)hit_of(d2, j + 2, exact) + (int)hit_of(d3, j + 3, exact);
         if (h && nrec < nbr_k) {
-            lst[nrec * kBlock] = (uint16_t)(j | (tag << 11) | (3 << 13));
+            lst[nrec * STRIDE] = (RecT)(j | (tag << 11) | (3 << 13));
             ++nrec;
         }
         cnt += h;
@@ -1745,7 +1711,7 @@ __device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int 
             for (int u = 0; u < 4; ++u) h += (u < nin && hit_of(d[u], j + u, exact)) ? 1 : 0;
         }
         if (h && nrec < nbr_k) {
-            lst[nrec * kBlock] = (uint16_t)(j | (tag << 11) | ((nin - 1) << 13));
+            lst[nrec * STRIDE] = (RecT)(j | (tag << 11) | ((nin - 1) << 13));
             ++nrec;
         }
         cnt += h;
@@ -2252,20 +2218,15 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                     };
                     uint32_t* lst = wt[w].rec + lane;
                     int cnt = 0, nrec = 0;
-                    bool done = scan_count32<true, 64>(T.buf, rg.cs, rg.ce, me, cut, min_points,
-                                                       cnt, lst, nrec, nbr_k, 0, exact);
-#pragma unroll
-                    for (int kk = 0; kk < 3 && !done; ++kk) {
-                        const int lo = rg.b[kk], hi = rg.e[kk];
-                        if (lo <= rg.cs && rg.ce <= hi) {
-                            done = scan_count32<true, 64>(T.buf, lo, rg.cs, me, cut, min_points,
-                                                          cnt, lst, nrec, nbr_k, kk, exact) ||
-                                   scan_count32<true, 64>(T.buf, rg.ce, hi, me, cut, min_points,
-                                                          cnt, lst, nrec, nbr_k, kk, exact);
-                        } else {
-                            done = scan_count32<true, 64>(T.buf, lo, hi, me, cut, min_points, cnt,
-                                                          lst, nrec, nbr_k, kk, exact);
-                        }
+                    bool done = false;
+#pragma unroll 1
+                    for (int kk = 0; kk < 5 && !done; ++kk) {  // (as count_tile32_kernel)
+                        const int b = kk == 0 ? rg.cs : kk == 1 ? rg.b[0] : kk == 2 ? rg.ce
+                                    : kk == 3 ? rg.b[1] : rg.b[2];
+                        const int e = kk == 0 ? rg.ce : kk == 1 ? rg.cs : kk == 2 ? rg.e[0]
+                                    : kk == 3 ? rg.e[1] : rg.e[2];
+                        done = scan_lean32<64>(T.buf, b, e, me, cut, min_points, cnt, lst, nrec,
+                                               nbr_k, kk < 3 ? 0 : kk - 2, exact);
                     }
                     is_core = cnt >= min_points;
                     if (!is_core && nbr_k > 0) {
@@ -2274,9 +2235,11 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                         for (int rr = 0; rr < nrec; ++rr) {
                             const uint32_t v = lst[rr * 64];
                             const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
+                            const int nin = (int)((v >> 13) & 3u) + 1;
                             const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
-                            for (uint32_t mm = v >> 16; mm; mm &= mm - 1) {
-                                const int qq = q + __ffs(mm) - 1;
+                            for (int uu = 0; uu < nin; ++uu) {
+                                const int qq = q + uu;
+                                if (!hit_of(count_d(me, T.buf[qq], cut.ne2), qq, exact)) continue;
                                 const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
                                               (qq >= st.off[k0 + 2] ? 1 : 0);
                                 const int sq = st.cb[c] + (qq - st.off[c]);
@@ -2919,7 +2882,11 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
     const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed,
     const int32_t* __restrict__ place) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+#ifndef DBSCAN_AB_XCD_LABEL
+#define DBSCAN_AB_XCD_LABEL 0
+#endif
+    const int64_t blk = (DBSCAN_AB_XCD_LABEL && place) ? (int64_t)xcd_block() : (int64_t)blockIdx.x;
+    const int64_t p = blk * kBlock + threadIdx.x;
     if (p >= n) return;
     const int64_t nf = *nf_p;
     uint32_t v = 0;  // Noise
