@@ -1641,7 +1641,10 @@ __device__ __forceinline__ bool stage_build_own32(const StageMeta& m,
     if (st.ok) {
         constexpr int kPer = (CAP + kBlock - 1) / kBlock;
         const int total = st.total;
-#pragma unroll
+#ifndef DBSCAN_AB_STAGE_UNROLL
+#define DBSCAN_AB_STAGE_UNROLL 6
+#endif
+#pragma unroll DBSCAN_AB_STAGE_UNROLL
         for (int u = 0; u < kPer; ++u) {
             const int i = tid + u * kBlock;
             if (i < total) {
@@ -3727,7 +3730,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                         a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
                 DBSCAN_HIP_CHECK(hipMemsetAsync(bc + 2 * tile_grid, 0, tile_grid * sizeof(int32_t), s));
-                klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
+#ifndef DBSCAN_AB_C32W
+#define DBSCAN_AB_C32W 6
+#endif
+                klaunch(prof, "count32", count_tile32_kernel<kCap32, DBSCAN_AB_C32W>, dim3(tile_grid),
                         dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
                         a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
                 klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,

@@ -103,7 +103,12 @@ def load() -> ctypes.CDLL:
                     f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
                     "g.build()'` (hipcc --offload-arch=gfx950)")
             L = ctypes.CDLL(LIB_PATH)
+            ab = bool(os.environ.get("DBSCAN_LIB_PATH"))
             for name, res, args in SIGNATURES:
+                # (an A/B build of an older revision, loaded through DBSCAN_LIB_PATH, may lack
+                # entry points added since: bind what it has; the in-tree library has them all)
+                if ab and not hasattr(L, name):
+                    continue
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -286,6 +286,20 @@ class HipSlabOps:
         self._from_handle()
         return rows[:total], [int(v) for v in counts]
 
+    def fit_whole(self, x, y, eps, min_points, mode):
+        """One rank, nothing to merge: the slab is the whole data set, so the node step is the
+        direct fit (dbscan_fit_device_async) -- labels in slab order, the cluster count."""
+        n = x.numel()
+        cl = torch.empty(n, dtype=torch.int32, device=x.device)
+        fl = torch.empty(n, dtype=torch.uint8, device=x.device)
+        nk = torch.zeros(1, dtype=torch.int32, device=x.device)
+        self._to_handle()
+        _lib.check(_lib.load().dbscan_fit_device_async(
+            self.h.ptr, _p(x), _p(y), n, float(eps), int(min_points), int(mode), _p(cl), _p(fl),
+            _p(nk)))
+        self._from_handle()
+        return cl, fl, int(nk.item())
+
     @staticmethod
     def _stream():
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -489,6 +503,12 @@ class NodeJob:
         """One step.  tick(name), if given, is called after each phase (tools/node_breakdown.py
         synchronizes and times there)."""
         tick = tick or (lambda name: None)
+        if self.comm._local() and not getattr(self, "cuts", None) and hasattr(self.ops, "fit_whole"):
+            # one rank and one slab (every point owned): the direct fit IS the node step
+            self.cluster, self.flag, self.n_clusters = self.ops.fit_whole(
+                self.x, self.y, self.eps, self.min_points, self.mode)
+            tick("slab_fit")
+            return self.n_clusters
         core, root = self.ops.fit(self.x, self.y, self.zone, self.eps, self.min_points,
                                   shared=self.sh_idx)
         tick("slab_fit")
