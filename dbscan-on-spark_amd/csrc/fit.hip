@@ -248,12 +248,12 @@ __global__ __launch_bounds__(kBlock) void scatter_xy_kernel(const double* __rest
 // (cache-resident while the launch sweeps the bands in order), coalesced writes.
 // Slab fits: zs[p] = the slot's zone (from the record), and for the listed shared points
 // sinv[i] = their slot (a scattered write per shared point only).
-#ifndef DBSCAN_AB_XCD_GATHER
-#define DBSCAN_AB_XCD_GATHER 0
-#endif
-// (A/B) block index with each XCD given a contiguous range of the grid (see xcd_block below)
+// Block index giving each XCD a contiguous range of the grid (as xcd_block below), for the
+// bucketed gathers: the slots of one tile-row band then run under one L2, so each band's
+// records (a random order inside the band) are fetched into one L2, not eight.  gather_bucket
+// 0.167 -> 0.154 ms and label_sorted (its packed[place] writes) 0.128 -> 0.106 ms per 10^7
+// points (A/B on one box).
 __device__ __forceinline__ int64_t gather_block() {
-    if (!DBSCAN_AB_XCD_GATHER) return blockIdx.x;
     const int G = gridDim.x, b = blockIdx.x;
     const int x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
     return x * q + (x < r ? x : r) + j;
@@ -1569,256 +1569,93 @@ __device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// count_tile32_kernel: the medium clique-grid tiles, ONE WORKGROUP PER TILE (stage <= CAP
-// points).  Per tile: stage (float2 cell-unit records, the own-cell table), count (own points
-// over 256 threads), the tile-local quarter union, all from LDS.
-// ---------------------------------------------------------------------------------------
-
-// Own-point tables of a staged tile, written by wave 0 before the records are loaded: for own
-// point i (own points in slot order: the tile's cells row-major, so own point i is slot ts + i)
-// its local cell ocell[i], and per tile row r the LDS offset of its first own point minus the
-// own points before it (hb[r]): own point i of row r sits at LDS index i + hb[r].  Replaces the
-// two dependent 3-step searches per own point (own index -> row -> cell).
-struct OwnTable {
-    int hb[8];
-    int own;             // own points
-    uint8_t ocell[1536];  // local cell (ly * 8 + lx) of each own point
-};
-
-// stage_build32 + the own tables (one more output per staged record: its own-cell byte)
-template <int CAP>
-__device__ __forceinline__ bool stage_build_own32(const StageMeta& m,
-                                                  const double2* __restrict__ xy, TileStage& st,
-                                                  float2* buf, OwnTable& ot, double invx,
-                                                  double invy, const TileOrg& o) {
-    const int tid = threadIdx.x;
-    if (tid < 100) {
-        st.cb[tid] = m.b;
-        st.cn[tid] = m.cnt;
-    }
-    if (tid == 0) {
-        st.ts = m.ts;
-        st.te = m.te;
-        st.q0 = m.q0;
-        st.nq = m.q1 - m.q0;
-    }
-    __syncthreads();
-    if (tid < 64) {
-        int carry = 0;
-        for (int base = 0; base < 100; base += 64) {
-            const int i = base + tid;
-            const int v = i < 100 ? st.cn[i] : 0;
-            int incl = v;
-#pragma unroll
-            for (int o2 = 1; o2 < 64; o2 <<= 1) {
-                const int u = __shfl_up(incl, o2, 64);
-                if (tid >= o2) incl += u;
-            }
-            if (i < 100) st.off[i] = carry + incl - v;
-            carry += __shfl(incl, 63, 64);
-        }
-        if (tid == 0) {
-            st.off[100] = carry;
-            st.total = carry;
-            st.ok = carry <= CAP;
-        }
-        // own points per tile row (extended cells (r+1)*10+1 .. +8), their prefix, and hb[r]
-        wave_sync();
-        const int r = tid & 7;
-        const int first = st.off[(r + 1) * 10 + 1];
-        const int cntr = st.off[(r + 1) * 10 + 9] - first;
-        int incl = cntr;
-#pragma unroll
-        for (int o2 = 1; o2 < 8; o2 <<= 1) {
-            const int u = __shfl_up(incl, o2, 64);
-            if (r >= o2) incl += u;
-        }
-        if (tid < 8) ot.hb[r] = first - (incl - cntr);
-        if (tid == 7) ot.own = incl;
-    }
-    __syncthreads();
-    if (st.ok) {
-        constexpr int kPer = (CAP + kBlock - 1) / kBlock;
-        const int total = st.total;
-#ifndef DBSCAN_AB_STAGE_UNROLL
-#define DBSCAN_AB_STAGE_UNROLL 6
-#endif
-#pragma unroll DBSCAN_AB_STAGE_UNROLL
-        for (int u = 0; u < kPer; ++u) {
-            const int i = tid + u * kBlock;
-            if (i < total) {
-                int lo = 0;
-#pragma unroll
-                for (int s = 64; s > 0; s >>= 1)
-                    if (lo + s < 100 && st.off[lo + s] <= i) lo += s;
-                const double2 v = xy[st.cb[lo] + (i - st.off[lo])];
-                buf[i] = make_float2((float)((v.x * 0.5 - o.xmin2) * invx - o.ox),
-                                     (float)((v.y * 0.5 - o.ymin2) * invy - o.oy));
-                const int ey = lo / 10 - 1, ex = lo - (ey + 1) * 10 - 1;
-                if ((unsigned)ey < 8u && (unsigned)ex < 8u) ot.ocell[i - ot.hb[ey]] = (uint8_t)(ey * 8 + ex);
-            }
-        }
-    }
-    __syncthreads();
-    return st.ok;
-}
-
-// One LDS range [b, e) of candidates for the count, in batches of 4 (the last one masked), early
-// exit at minPoints.  Per candidate the signed distance D (count_d): the batch's hits are the
-// sign bits of its D's, and a batch whose smallest |D| is inside the band is recounted with the
-// exact fp64 predicate on its band members (exact(q), LDS index q).  REC: each batch with hits
-// is noted as ONE 16-bit record (first LDS index | range tag << 11 | (candidates - 1) << 13) in
-// the thread's column of lst while fewer than nbr_k records exist; a point that ends below
-// minPoints has at most minPoints - 1 hits, so its records are complete.  The hits themselves are
-// re-derived from the records (the same tests) only for the non-cores' neighbour lists.
-// (Per candidate: one packed subtract and two FMAs; per batch: the band test and the sign-bit
-// sum -- about half the VALU of a compare / select per bound, the count phase being VALU-bound
-// while every wave of a CU scans.)
-template <class ExactF>
-__device__ __forceinline__ bool hit_of(float d, int q, ExactF exact) {
-    return fabsf(d) > kCountBand ? d < 0.0f : exact(q);
-}
-
-template <int STRIDE = kBlock, class RecT = uint16_t, class ExactF>
-__device__ __forceinline__ bool scan_lean32(const float2* __restrict__ buf, int b, int e,
-                                            float2 me, F32Cut cut, int min_points, int& cnt,
-                                            RecT* lst, int& nrec, int nbr_k, int tag,
-                                            ExactF exact) {
-    int j = b;
-    for (; j + 4 <= e; j += 4) {
-        const float d0 = count_d(me, buf[j], cut.ne2), d1 = count_d(me, buf[j + 1], cut.ne2);
-        const float d2 = count_d(me, buf[j + 2], cut.ne2), d3 = count_d(me, buf[j + 3], cut.ne2);
-        int h = (int)(sign_of(d0) + sign_of(d1) + sign_of(d2) + sign_of(d3));
-        const float mn = fminf(fminf(fabsf(d0), fabsf(d1)), fminf(fabsf(d2), fabsf(d3)));
-        if (__builtin_expect(mn <= kCountBand, 0))
-            h = (int)hit_of(d0, j, exact) + (int)hit_of(d1, j + 1, exact) +
-                (int)hit_of(d2, j + 2, exact) + (int)hit_of(d3, j + 3, exact);
-        if (h && nrec < nbr_k) {
-            lst[nrec * STRIDE] = (RecT)(j | (tag << 11) | (3 << 13));
-            ++nrec;
-        }
-        cnt += h;
-        if (cnt >= min_points) return true;
-    }
-    if (j < e) {  // the last 1-3 candidates: the batch reads past e (inside LDS), masked
+// One LDS range of candidates in batches of kScanBatch (the last batch masked).  Hits by the sign
+// of D (count_d), candidates inside the band by the exact fp64 predicate (exact(q) for LDS index
+// q).  REC: each batch with
+// hits is noted as ONE record (first LDS index | range tag << 11 | hit bits << 16) in the
+// thread's column of lst while fewer than nbr_k records exist; a point that ends below
+// minPoints has at most minPoints - 1 hits, so its records are complete.
+// Candidates per batch: 4, the batch's tail clamped and masked once (round 2: against 8 with
+// a per-candidate select, count_wave + count_tiny 0.092 -> 0.087 ms at 10^7, 0.256 -> 0.236
+// on config 3's share; 8 in this form spilled at 80 VGPRs).
+constexpr int kScanBatch = 4;
+template <bool REC, int STRIDE = kBlock, class ExactF>
+__device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
+                                             float2 me, F32Cut cut, int min_points, int& cnt,
+                                             uint32_t* lst, int& nrec, int nbr_k, int tag,
+                                             ExactF exact) {
+    for (int j = b; j < e; j += kScanBatch) {
         const int nin = e - j;
-        float d[4];
+        float2 qq[kScanBatch];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) d[u] = u < nin ? count_d(me, buf[j + u], cut.ne2) : 1.0f;
-        int h = (int)(sign_of(d[0]) + sign_of(d[1]) + sign_of(d[2]) + sign_of(d[3]));
-        const float mn = fminf(fminf(fabsf(d[0]), fabsf(d[1])), fminf(fabsf(d[2]), fabsf(d[3])));
-        if (__builtin_expect(mn <= kCountBand, 0)) {
-            h = 0;
+        for (int u = 0; u < kScanBatch; ++u) qq[u] = buf[min(j + u, e - 1)];  // tail masked below
+        // the signed form (count_d): hits from sign bits, one band test per batch (the F <= lo /
+        // F <= hi compares per candidate measured 0.312 -> 0.307 ms in count32)
+        const uint32_t valid = nin >= kScanBatch ? (1u << kScanBatch) - 1u : (1u << nin) - 1u;
+        uint32_t hm = 0, am = 0;
+        float d[kScanBatch];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) h += (u < nin && hit_of(d[u], j + u, exact)) ? 1 : 0;
+        for (int u = 0; u < kScanBatch; ++u) {
+            d[u] = count_d(me, qq[u], cut.ne2);
+            hm |= sign_of(d[u]) << u;
         }
-        if (h && nrec < nbr_k) {
-            lst[nrec * STRIDE] = (RecT)(j | (tag << 11) | ((nin - 1) << 13));
+        hm &= valid;
+        const float mn = fminf(fminf(fabsf(d[0]), fabsf(d[1])), fminf(fabsf(d[2]), fabsf(d[3])));
+        if (__builtin_expect(mn <= kCountBand, 0)) {  // band members: the exact predicate
+#pragma unroll
+            for (int u = 0; u < kScanBatch; ++u)
+                if (((valid >> u) & 1u) && fabsf(d[u]) <= kCountBand) am |= 1u << u;
+            hm &= ~am;
+        }
+        if (__builtin_expect(am != 0, 0)) {
+            for (uint32_t m = am; m; m &= m - 1) {
+                const int u = __ffs(m) - 1;
+                if (exact(j + u)) hm |= 1u << u;
+            }
+        }
+        if (REC && hm && nrec < nbr_k) {
+            lst[nrec * STRIDE] = (uint32_t)j | ((uint32_t)tag << 11) | (hm << 16);
             ++nrec;
         }
-        cnt += h;
+        cnt += __popc(hm);
+        if (cnt >= min_points) return true;
     }
     return cnt >= min_points;
 }
 
-// Up to 4 cores of a quarter (LDS begin ab, length len, core bits m of its first 32 points) in
-// registers; the unused entries hold a far sentinel (side: +1 / -1, so that two sentinels are
-// never near each other).  ok = false when the quarter has more than 4 cores or more than 32
-// points (the caller then takes quarters_touch32).
-struct Cores4 {
-    float2 p0, p1, p2, p3;
-    bool ok;
-};
-__device__ __forceinline__ Cores4 cores4(const float2* __restrict__ buf, uint32_t r, uint32_t m,
-                                         float side) {
-    const int ab = (int)(r & 2047u), len = (int)((r >> 11) & 2047u);
-    const float2 far = make_float2(side * 1e18f, side * 1e18f);
-    Cores4 c;
-    int j = m ? __ffs(m) - 1 : -1;
-    m &= m - 1;
-    c.p0 = j >= 0 ? buf[ab + j] : far;
-    j = m ? __ffs(m) - 1 : -1;
-    m &= m - 1;
-    c.p1 = j >= 0 ? buf[ab + j] : far;
-    j = m ? __ffs(m) - 1 : -1;
-    m &= m - 1;
-    c.p2 = j >= 0 ? buf[ab + j] : far;
-    j = m ? __ffs(m) - 1 : -1;
-    m &= m - 1;
-    c.p3 = j >= 0 ? buf[ab + j] : far;
-    c.ok = m == 0 && len <= 32;
-    return c;
-}
-
-// Do the cores of two quarters (in registers) hold a sure pair (returns 1), no pair (0), or only
-// ambiguous ones (2: the caller decides exactly)?
-__device__ __forceinline__ void pairs4(float2 a, const Cores4& b, F32Cut cut, int& sure,
-                                       int& maybe) {
-    const float F0 = f32_d2(a, b.p0), F1 = f32_d2(a, b.p1), F2 = f32_d2(a, b.p2),
-                F3 = f32_d2(a, b.p3);
-    const float m = fminf(fminf(F0, F1), fminf(F2, F3));
-    sure |= m <= cut.lo ? 1 : 0;
-    maybe |= m <= cut.hi ? 1 : 0;
-}
-__device__ __forceinline__ int pairs44(const Cores4& a, const Cores4& b, F32Cut cut) {
-    int sure = 0, maybe = 0;
-    pairs4(a.p0, b, cut, sure, maybe);
-    pairs4(a.p1, b, cut, sure, maybe);
-    pairs4(a.p2, b, cut, sure, maybe);
-    pairs4(a.p3, b, cut, sure, maybe);
-    return sure ? 1 : (maybe ? 2 : 0);
-}
-
-struct UnionLds32 {  // aliases the count's neighbour records (the two never overlap in time)
-    int lp[kMaxTileQ];           // LDS union-find over the tile's quarters
-    uint8_t comp[kMaxTileQ];     // each core quarter's component after the adjacent unions
-    uint32_t lrange[kMaxTileQ];  // LDS begin | length << 11 | local quarter (16 y + x) << 22;
-                                 // bit 31: holds cores
-    uint32_t lmask[kMaxTileQ];   // cores among the first 32 points
-    unsigned long long cmin[kMaxTileQ];  // per component: min (visit index << 32 | rep)
-};
-
-// The tile-local quarter union of a staged medium tile (fused into count_tile32_kernel): quarter
-// records, unions of core quarters within eps (adjacent quarters from each core quarter's lane,
-// then -- only if the tile is still split -- the quarters at distance 2 as (quarter, offset)
-// items), each tile component's rep = its core with the smallest visit index.  Pair tests run
-// on the quarters' cores held in registers (cores4 / pairs44); ambiguous or crowded quarters take
-// quarters_touch32.  qmap (16x16 local quarter grid -> quarter) is all 0xFFFF on entry and is
-// left so.
-__device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e, uint32_t key,
-                             const FuseArgs& fa, int gx0, int gy0, const TileStage& st,
-                             const float2* __restrict__ buf, const uint32_t* __restrict__ lcore,
-                             const double2* __restrict__ xy, double eps2, F32Cut cut,
-                             int32_t* __restrict__ parent, UnionLds32& u, uint16_t* qmap,
-                             int& s_first, int& s_tflags) {
+// fused_tile_union over the float2 stage (see fused_tile_union for the structure)
+__device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t key,
+                                   const FuseArgs& fa,
+                                   const GridParams& g, const TileStage& st,
+                                   const float2* __restrict__ buf,
+                                   const uint32_t* __restrict__ lcore,
+                                   const double2* __restrict__ xy, double eps2, F32Cut cut,
+                                   int32_t* __restrict__ parent, UnionLds& u) {
     const int i = threadIdx.x;
     const auto is_core = [&](int j) { return ((lcore[j >> 5] >> (j & 31)) & 1u) != 0; };
     const auto exact = [&](int qa, int qb) {
         const double2 pa = xy[stage_slot(st, qa)], pb = xy[stage_slot(st, qb)];
         return within_eps(pa.x, pa.y, pb.x, pb.y, eps2);
     };
-    // pa: quarter A's cores (cores4)
-    const auto touch = [&](const Cores4& pa, uint32_t ri, uint32_t mi, uint32_t rj,
-                           uint32_t mj) {
-        const Cores4 pb = cores4(buf, rj, mj, -1.0f);
-        int v = 2;
-        if (pa.ok && pb.ok) v = pairs44(pa, pb, cut);
-        if (v != 2) return v == 1;
-        const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
-        const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
-        return quarters_touch32(buf, ab, ae, mi, bb, be, mj, is_core, cut, exact);
-    };
-    int rep = -1, best = 0x7FFFFFFF, lq = 0, gx = 0, gy = 0;
+    __shared__ int s_first;  // smallest local quarter holding a core
+    __shared__ int s_tflags;  // the tile's edge strips holding cores (FuseArgs::tcore)
+    if (i == 0) {
+        s_first = 0x7FFFFFFF;
+        s_tflags = 0;
+    }
+    u.qmap[i] = 0xFFFF;
+    u.cmin[i] = ~0ull;
+    lds_barrier();
+    int rep = -1, best = 0x7FFFFFFF, gx = 0, gy = 0;
     if (i < nq) {
-        const int l = (int)((key >> 2) & 63u), lx = l & 7, ly = l >> 3;
-        const int qx = (int)(key & 1u), qy = (int)((key >> 1) & 1u);
-        const int lqx = 2 * lx + qx, lqy = 2 * ly + qy;
-        lq = lqy * 16 + lqx;
-        gx = gx0 + lqx;
-        gy = gy0 + lqy;
+        uint32_t cx, cy;
+        cell_xy(key >> 2, g.ntx, cx, cy);
+        gx = (int)(2 * cx + (key & 1u));
+        gy = (int)(2 * cy + ((key >> 1) & 1u));
+        const int lq = (gy & 15) * 16 + (gx & 15);
         const int len = e - b;
-        const int k = (ly + 1) * 10 + lx + 1;
+        const int l = (int)((key >> 2) & 63u);
+        const int k = ((l >> 3) + 1) * 10 + (l & 7) + 1;
         const int jb = st.off[k] + (b - st.cb[k]);
         uint32_t mask = 0;
         int first = -1;
@@ -1837,9 +1674,11 @@ __device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e
         if (first >= 0) {
             rep = b + first;
             best = fa.perm[rep];
+        }
+        if (rep >= 0) {
             atomicMin(&s_first, i);
             // east cell column: local quarter x 14, 15; south cell row: local quarter y 14, 15
-            const int tf = (lqx >= 14 ? 1 : 0) | (lqy >= 14 ? 2 : 0);
+            const int tf = ((gx & 15) >= 14 ? 1 : 0) | ((gy & 15) >= 14 ? 2 : 0);
             if (tf) atomicOr(&s_tflags, tf);
         }
         fa.qinfo[q0 + i] = make_int4(b, e, rep, (int)mask);
@@ -1847,75 +1686,44 @@ __device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e
         u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22) | (uint32_t)jb |
                       ((uint32_t)len << 11);
         u.lmask[i] = mask;
-        u.cmin[i] = ~0ull;
-        qmap[lq] = (uint16_t)i;
+        u.qmap[lq] = (uint16_t)i;
     }
     lds_barrier();
-    AB_STAMP(5);
     if (i == 0) fa.tcore[t] = (uint8_t)s_tflags;
-    // adjacent quarters (the 4 backward offsets) from each core quarter's own lane: the four
-    // lookups, the neighbours' records and their cores are loaded together
-    if (i < nq && rep >= 0) {
-        constexpr int kDx[4] = {-1, 0, 1, -1}, kDy[4] = {-1, -1, -1, 0};
-        const uint32_t ri = u.lrange[i], mi = u.lmask[i];
-        const int lqx = lq & 15, lqy = lq >> 4;
-        int jn[4];
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            const int ux = lqx + kDx[o], uy = lqy + kDy[o];
-            jn[o] = (ux >= 0 && ux <= 15 && uy >= 0) ? (int)qmap[uy * 16 + ux] : 0xFFFF;
-        }
-        uint32_t rj[4], mj[4];
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            const int jj = jn[o] == 0xFFFF ? i : jn[o];
-            rj[o] = jn[o] == 0xFFFF ? 0u : u.lrange[jj];
-            mj[o] = u.lmask[jj];
-        }
-        const Cores4 pa = cores4(buf, ri, mi, 1.0f);
-        uint32_t tt = 0;
-#pragma unroll 1
-        for (int o = 0; o < 4; ++o) {  // (one copy of the pair test: instruction cache)
-            const uint32_t r = o == 0 ? rj[0] : o == 1 ? rj[1] : o == 2 ? rj[2] : rj[3];
-            const uint32_t m = o == 0 ? mj[0] : o == 1 ? mj[1] : o == 2 ? mj[2] : mj[3];
-            if ((r >> 31) && touch(pa, ri, mi, r, m)) tt |= 1u << o;
-        }
-#pragma unroll
-        for (int o = 0; o < 4; ++o)
-            if ((tt >> o) & 1u) lunite(u.lp, i, jn[o]);
-    }
-    lds_barrier();
-    AB_STAMP(6);
-    // each core quarter's component after the adjacent pairs, once; if they joined every core
-    // of the tile, no distance-2 pair can add an edge
-    const int f = s_first;
-    int ci = -1;
-    if (i < nq && rep >= 0) {
-        ci = lfind(u.lp, i);
-        u.comp[i] = ci;
-    }
-    const bool split = ci >= 0 && ci != lfind(u.lp, f);
-    if (__syncthreads_or(split)) {
-        // distance-2 pairs between quarters of different components (the snapshot above: a
-        // pair joined meanwhile by another distance-2 union is only tested again)
-        for (int k = i; k < nq * 8; k += kBlock) {
-            const int o = k / nq, qi = k - o * nq;
-            const uint32_t ri = u.lrange[qi];
-            if (!(ri >> 31)) continue;
-            const int lqq = (int)((ri >> 22) & 255u);
-            const int ux = (lqq & 15) + kRingDx[4 + o], uy = (lqq >> 4) + kRingDy[4 + o];
-            if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
-            const int j = qmap[uy * 16 + ux];
-            if (j == 0xFFFF) continue;
-            const uint32_t rj = u.lrange[j];
-            if (!(rj >> 31)) continue;
-            if (u.comp[qi] == u.comp[j]) continue;
-            const uint32_t mi = u.lmask[qi];
-            if (touch(cores4(buf, ri, mi, 1.0f), ri, mi, rj, u.lmask[j])) lunite(u.lp, qi, j);
-        }
+    AB_STAMP(5);
+    {
+        // adjacent quarters (the 4 backward offsets) from each core quarter's own thread
+        if (i < nq && rep >= 0)
+            unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, i, buf, is_core, cut, exact);
         lds_barrier();
+        AB_STAMP(6);
+        // the adjacent pairs joined every core of the tile: no distance-2 pair can add an edge
+        // inside it
+        const int f = s_first;
+        const bool split = i < nq && rep >= 0 && lfind(u.lp, i) != lfind(u.lp, f);
+        if (__syncthreads_or(split)) {
+            for (int k = i; k < nq * 8; k += kBlock) {
+                const int o = k / nq, qi = k - o * nq;
+                const uint32_t ri = u.lrange[qi];
+                if (!(ri >> 31)) continue;
+                const int lq = (int)((ri >> 22) & 255u);
+                const int ux = (lq & 15) + kRingDx[4 + o], uy = (lq >> 4) + kRingDy[4 + o];
+                if (ux < 0 || uy < 0 || ux > 15 || uy > 15) continue;
+                const int j = u.qmap[uy * 16 + ux];
+                if (j == 0xFFFF) continue;
+                const uint32_t rj = u.lrange[j];
+                if (!(rj >> 31)) continue;
+                if (lfind(u.lp, qi) == lfind(u.lp, j)) continue;
+                const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
+                const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
+                if (quarters_touch32(buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, cut,
+                                     exact))
+                    lunite(u.lp, qi, j);
+            }
+            lds_barrier();
+        }
+        AB_STAMP(7);
     }
-    AB_STAMP(7);
     int r = -1;
     if (i < nq && rep >= 0) {
         r = lfind(u.lp, i);
@@ -1928,12 +1736,11 @@ __device__ __forceinline__ void tile_union32(int t, int q0, int nq, int b, int e
         fa.qg[q0 + i] = make_int4(gx, gy, best, 0);
         fa.qcomp[q0 + i] = crep;
         if (rep >= 0) parent[rep] = crep;
-        qmap[lq] = 0xFFFF;  // (the next tile's writes follow the staging barriers)
     }
 }
 
 // Count + fused tile union on clique grids with the fp32 tile records above (the fp64
-// count_tile_kernel runs the other grids; each exits at once on the other's).
+// count_tile_kernel<.., true> runs the other grids; each exits at once on the other's).
 template <int CAP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
@@ -1945,24 +1752,20 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
         if (threadIdx.x == 0) block_cores[blockIdx.x] = 0;
         return;
     }
-    static_assert(CAP <= 1536, "OwnTable::ocell, 11-bit LDS ranges");
     __shared__ TileStage st;
-    __shared__ float2 buf[CAP + 4];  // (+4: a masked batch may read 3 records past the end)
-    __shared__ OwnTable ot;
+    __shared__ float2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
-    __shared__ __attribute__((aligned(16))) uint16_t lsts[kMaxNbr * kBlock];
+    __shared__ int rowoff[9];
+    __shared__ __attribute__((aligned(16))) uint32_t lsts[kMaxNbr * kBlock];
     __shared__ uint32_t lcore[(CAP + 31) / 32 + 1];
-    __shared__ uint16_t qmap[kMaxTileQ];
-    __shared__ int s_first, s_tflags;
-    static_assert(sizeof(UnionLds32) <= sizeof(lsts), "UnionLds32 must fit");
-    uint16_t* lst = lsts + threadIdx.x;
+    static_assert(CAP < 2048, "LDS ranges are packed in 11 bits");
+    static_assert(sizeof(UnionLds) <= sizeof(lsts), "UnionLds must fit");
+    uint32_t* lst = lsts + threadIdx.x;
     const int ntiles = *ntiles_p;
     const F32Cut cut = f32_cut(g, eps2);
     int mine = 0;
-    static_assert(kBlock == kMaxTileQ, "one qmap entry per thread");
-    qmap[threadIdx.x] = 0xFFFF;  // (ordered by the staging barriers)
     // the medium tiles (tile_class_kernel): each fits the staging capacity
-    const BucketWalk<kMedBuckets> order(fa.tl.mb);
+    const BucketWalk<kMedBuckets> order(fa.tl.mb);  // largest stages first (tile_class_kernel)
     const int nt = order.size();
     const auto tile_at = [&](int k) { return k < nt ? order.at(fa.tl.medium, fa.tl.cap, k) : ntiles; };
     StageMeta meta = stage_meta(tile_at(blockIdx.x), ntiles, tstage, tstart, fa.tq);
@@ -1970,89 +1773,100 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
         AB_STAMP(0);
         const int t = tile_at(k);
         if (threadIdx.x < (CAP + 31) / 32 + 1) lcore[threadIdx.x] = 0u;
-        if (threadIdx.x == 0) {
-            s_first = 0x7FFFFFFF;
-            s_tflags = 0;
-        }
-        const uint32_t tk = fa.tkey[t];
-        const TileOrg org = tile_org(g, fa.tpart, t, tk);
-        stage_build_own32<CAP>(meta, xy, st, buf, ot, g.invx, g.invy, org);
+        stage_build32<CAP>(meta, xy, st, buf, g, tile_org(g, fa.tpart, t, fa.tkey[t]));
         AB_STAMP(1);
         AB_NOTE(10, st.total);
         meta = stage_meta(tile_at(k + gridDim.x), ntiles, tstage, tstart, fa.tq);
         const int q0 = st.q0, nq = st.nq;
         int qb = 0, qe = 0;
         uint32_t qk = 0;
-        if ((int)threadIdx.x < nq) {  // this thread's quarter record, in flight during the count
+        if ((int)threadIdx.x < nq) {
             qb = fa.qstart[q0 + threadIdx.x];
             qe = fa.qstart[q0 + threadIdx.x + 1];
             qk = fa.qkey[q0 + threadIdx.x];
         }
-        AB_STAMP(2);
-        const int own = ot.own;
-        AB_NOTE(11, own);
-        for (int i = (int)threadIdx.x; i < own; i += kBlock) {
-            const int l = ot.ocell[i];
-            const int j = i + ot.hb[l >> 3];
-            const int p = st.ts + i;  // own points are the tile's slots in order
-            bool is_core = true;
-            if (min_points > 0) {
-                const float2 me = buf[j];
-                const LdsRanges rg = lds_ranges(st, l);
-                const auto exact = [&](int q) {
-                    const double2 a = xy[p], o = xy[stage_slot(st, q)];
-                    return within_eps(a.x, a.y, o.x, o.y, eps2);
-                };
-                // five LDS ranges, one scan loop (one copy of the code: the kernel's instructions
-                // stay inside the instruction cache): the own cell, the rest of its row left and
-                // right of it, the rows above and below (the own row's range always holds the
-                // own cell)
-                int cnt = 0, nrec = 0;
-                bool done = false;
-#pragma unroll 1
-                for (int kk = 0; kk < 5 && !done; ++kk) {
-                    const int b = kk == 0 ? rg.cs : kk == 1 ? rg.b[0] : kk == 2 ? rg.ce
-                                : kk == 3 ? rg.b[1] : rg.b[2];
-                    const int e = kk == 0 ? rg.ce : kk == 1 ? rg.cs : kk == 2 ? rg.e[0]
-                                : kk == 3 ? rg.e[1] : rg.e[2];
-                    done = scan_lean32(buf, b, e, me, cut, min_points, cnt, lst, nrec, nbr_k,
-                                       kk < 3 ? 0 : kk - 2, exact);
+        {
+            if (threadIdx.x == 0) {
+                int acc = 0;
+                for (int r = 0; r < 8; ++r) {
+                    rowoff[r] = acc;
+                    acc += st.off[(r + 1) * 10 + 9] - st.off[(r + 1) * 10 + 1];
                 }
-                is_core = cnt >= min_points;
-                if (!is_core && nbr_k > 0) {  // (a complete list: cnt < minPoints)
-                    // the non-core's neighbours (self excluded), -1 terminated: the recorded
-                    // batches' hits, re-derived
-                    int32_t* out = nbr + (int64_t)p * nbr_k;
-                    const int lx = l & 7, ly = l >> 3;
-                    int w = 0;
-                    for (int rr = 0; rr < nrec; ++rr) {
-                        const uint32_t v = lst[rr * kBlock];
-                        const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
-                        const int nin = (int)(v >> 13) + 1;
-                        const int k0 = (ly + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + lx;
-                        for (int uu = 0; uu < nin; ++uu) {
-                            const int qq = q + uu;
-                            if (!hit_of(count_d(me, buf[qq], cut.ne2), qq, exact)) continue;
-                            const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
-                                          (qq >= st.off[k0 + 2] ? 1 : 0);
-                            const int sq = st.cb[c] + (qq - st.off[c]);
-                            if (sq != p) out[w++] = sq;
+                rowoff[8] = acc;
+            }
+            __syncthreads();
+            AB_STAMP(2);
+            const int own = rowoff[8];
+            AB_NOTE(11, own);
+            for (int i = (int)threadIdx.x; i < own; i += kBlock) {
+                int r = 0;
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (r + s < 8 && rowoff[r + s] <= i) r += s;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - rowoff[r]);
+                int ex = 0;
+#pragma unroll
+                for (int s = 4; s > 0; s >>= 1)
+                    if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
+                const int p = st.cb[base + ex] + (j - st.off[base + ex]);
+                bool is_core = true;
+                if (min_points > 0) {
+                    const int l = r * 8 + ex;
+                    const float2 me = buf[j];
+                    const LdsRanges rg = lds_ranges(st, l);
+                    const auto exact = [&](int q) {
+                        const double2 a = xy[p], o = xy[stage_slot(st, q)];
+                        return within_eps(a.x, a.y, o.x, o.y, eps2);
+                    };
+                    int cnt = 0, nrec = 0;
+                    const int k_rec = nbr_k;
+                    bool done = scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points, cnt,
+                                                   lst, nrec, k_rec, 0, exact);
+#pragma unroll
+                    for (int k = 0; k < 3 && !done; ++k) {
+                        const int lo = rg.b[k], hi = rg.e[k];
+                        if (lo <= rg.cs && rg.ce <= hi) {
+                            done = scan_count32<true>(buf, lo, rg.cs, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact) ||
+                                   scan_count32<true>(buf, rg.ce, hi, me, cut, min_points, cnt,
+                                                      lst, nrec, k_rec, k, exact);
+                        } else {
+                            done = scan_count32<true>(buf, lo, hi, me, cut, min_points, cnt, lst,
+                                                      nrec, k_rec, k, exact);
                         }
                     }
-                    if (w < nbr_k) out[w] = -1;
+                    is_core = cnt >= min_points;
+                    if (!is_core && k_rec > 0) {  // (a complete list: cnt < minPoints)
+                        // the non-core's neighbours (self excluded), -1 terminated
+                        int32_t* out = nbr + (int64_t)p * nbr_k;
+                        int w = 0;
+                        for (int rr = 0; rr < nrec; ++rr) {
+                            const uint32_t v = lst[rr * kBlock];
+                            const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
+                            const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
+                            for (uint32_t m = v >> 16; m; m &= m - 1) {
+                                const int qq = q + __ffs(m) - 1;
+                                const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
+                                              (qq >= st.off[k0 + 2] ? 1 : 0);
+                                const int sq = st.cb[c] + (qq - st.off[c]);
+                                if (sq != p) out[w++] = sq;
+                            }
+                        }
+                        if (w < nbr_k) out[w] = -1;
+                    }
                 }
+                if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
+                if (is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
+                core[p] = is_core ? 1 : 0;
+                mine += is_core ? 1 : 0;
             }
-            if (fa.zs && fa.zs[p] == 2) is_core = false;  // slab halo: candidate only
-            if (is_core) atomicOr(&lcore[j >> 5], 1u << (j & 31));
-            core[p] = is_core ? 1 : 0;
-            mine += is_core ? 1 : 0;
+            AB_STAMP(3);
+            __syncthreads();
+            AB_STAMP(4);
+            fused_tile_union32(t, q0, nq, qb, qe, qk, fa, g, st, buf, lcore, xy, eps2, cut, parent,
+                               *reinterpret_cast<UnionLds*>(lsts));
         }
-        AB_STAMP(3);
-        lds_barrier();
-        AB_STAMP(4);
-        const uint32_t tyy = tk / g.ntx, txx = tk - tyy * g.ntx;  // the tile in the (virtual) grid
-        tile_union32(t, q0, nq, qb, qe, qk, fa, 16 * (int)txx, 16 * (int)tyy, st, buf, lcore, xy, eps2, cut,
-                     parent, *reinterpret_cast<UnionLds32*>(lsts), qmap, s_first, s_tflags);
         __syncthreads();
         AB_STAMP(9);
     }
@@ -2065,6 +1879,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
         block_cores[blockIdx.x] = tot;
     }
 }
+
 
 // Small clique-grid tiles (tile + halo <= kSmallCap points; most tiles of a clustered set are
 // sparse ones at cluster edges): ONE WAVE per tile, the same stage / count / quarter union as
@@ -2221,15 +2036,20 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                     };
                     uint32_t* lst = wt[w].rec + lane;
                     int cnt = 0, nrec = 0;
-                    bool done = false;
-#pragma unroll 1
-                    for (int kk = 0; kk < 5 && !done; ++kk) {  // (as count_tile32_kernel)
-                        const int b = kk == 0 ? rg.cs : kk == 1 ? rg.b[0] : kk == 2 ? rg.ce
-                                    : kk == 3 ? rg.b[1] : rg.b[2];
-                        const int e = kk == 0 ? rg.ce : kk == 1 ? rg.cs : kk == 2 ? rg.e[0]
-                                    : kk == 3 ? rg.e[1] : rg.e[2];
-                        done = scan_lean32<64>(T.buf, b, e, me, cut, min_points, cnt, lst, nrec,
-                                               nbr_k, kk < 3 ? 0 : kk - 2, exact);
+                    bool done = scan_count32<true, 64>(T.buf, rg.cs, rg.ce, me, cut, min_points,
+                                                       cnt, lst, nrec, nbr_k, 0, exact);
+#pragma unroll
+                    for (int kk = 0; kk < 3 && !done; ++kk) {
+                        const int lo = rg.b[kk], hi = rg.e[kk];
+                        if (lo <= rg.cs && rg.ce <= hi) {
+                            done = scan_count32<true, 64>(T.buf, lo, rg.cs, me, cut, min_points,
+                                                          cnt, lst, nrec, nbr_k, kk, exact) ||
+                                   scan_count32<true, 64>(T.buf, rg.ce, hi, me, cut, min_points,
+                                                          cnt, lst, nrec, nbr_k, kk, exact);
+                        } else {
+                            done = scan_count32<true, 64>(T.buf, lo, hi, me, cut, min_points, cnt,
+                                                          lst, nrec, nbr_k, kk, exact);
+                        }
                     }
                     is_core = cnt >= min_points;
                     if (!is_core && nbr_k > 0) {
@@ -2238,11 +2058,9 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
                         for (int rr = 0; rr < nrec; ++rr) {
                             const uint32_t v = lst[rr * 64];
                             const int q = (int)(v & 2047u), row = (int)((v >> 11) & 3u);
-                            const int nin = (int)((v >> 13) & 3u) + 1;
                             const int k0 = (r + (row == 0 ? 0 : (row == 1 ? -1 : 1)) + 1) * 10 + ex;
-                            for (int uu = 0; uu < nin; ++uu) {
-                                const int qq = q + uu;
-                                if (!hit_of(count_d(me, T.buf[qq], cut.ne2), qq, exact)) continue;
+                            for (uint32_t mm = v >> 16; mm; mm &= mm - 1) {
+                                const int qq = q + __ffs(mm) - 1;
                                 const int c = k0 + (qq >= st.off[k0 + 1] ? 1 : 0) +
                                               (qq >= st.off[k0 + 2] ? 1 : 0);
                                 const int sq = st.cb[c] + (qq - st.off[c]);
@@ -2885,10 +2703,9 @@ __global__ __launch_bounds__(kBlock) void label_sorted_kernel(
     const int64_t* __restrict__ gid, const int64_t* __restrict__ gs_of_root,
     const int32_t* __restrict__ label_of_root, uint32_t* __restrict__ packed,
     const int32_t* __restrict__ place) {
-#ifndef DBSCAN_AB_XCD_LABEL
-#define DBSCAN_AB_XCD_LABEL 0
-#endif
-    const int64_t blk = (DBSCAN_AB_XCD_LABEL && place) ? (int64_t)xcd_block() : (int64_t)blockIdx.x;
+    // bucketed fits: XCD-contiguous slot ranges (gather_block: the packed[place] writes of a band
+    // merge in one L2)
+    const int64_t blk = place ? gather_block() : (int64_t)blockIdx.x;
     const int64_t p = blk * kBlock + threadIdx.x;
     if (p >= n) return;
     const int64_t nf = *nf_p;
@@ -3730,10 +3547,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                         a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
                 DBSCAN_HIP_CHECK(hipMemsetAsync(bc + 2 * tile_grid, 0, tile_grid * sizeof(int32_t), s));
-#ifndef DBSCAN_AB_C32W
-#define DBSCAN_AB_C32W 6
-#endif
-                klaunch(prof, "count32", count_tile32_kernel<kCap32, DBSCAN_AB_C32W>, dim3(tile_grid),
+                klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
                         dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
                         a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
                 klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,

@@ -1,4 +1,3 @@
-VARIANTS="base main m5 u2 xg" ROUNDS=2 timeout -k 10 500 bash tools/ab_bench.sh > gpurun_out/ab_r4d.log 2>&1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib/f -o run -- python3 tools/pmc_calibrate.py run > gpurun_out/calib_f.log 2>&1 && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib/w -o run -- python3 tools/pmc_calibrate.py run > gpurun_out/calib_w.log 2>&1 && python3 tools/pmc_calibrate.py report gpurun_out/calib > gpurun_out/calib_report.txt 2>&1
-DBSCAN_NODE_TRACE=1 timeout -k 10 300 python tools/train_node_probe.py > gpurun_out/train_node_probe.log 2>&1
+VARIANTS="base main sgn xg xgl" ROUNDS=2 timeout -k 10 500 bash tools/ab_bench.sh > gpurun_out/ab_r4f.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_structure.py tests/test_gpu_small.py -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest_r4f.log 2>&1
+for v in sgn xgl; do DBSCAN_LIB_PATH=dbscan-on-spark_amd/lib_ab/$v/libdbscan_hip.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_structure.py -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest_r4f_$v.log 2>&1; done
