@@ -514,10 +514,12 @@ def seam(args, h, threads):
     partition of <= maxPointsPerPartition points + eps halo).
       per_call   one fit of m points per call, m in 250 / 2k / 8k / 64k: dbscan_fit_h (host
                  arrays, PCIe included) and dbscan_fit_device (device-resident, synchronous),
-                 median of repeated calls; the plain columns force the one-workgroup kernel
+                 median of repeated calls, and capi_us: the dbscan_fit_device call alone as a JNI
+                 caller makes it (no torch stream sync); the plain columns are the LDS kernels
                  (small.hip) up to 8192 points, 'tiled' is the same call through the tiled
                  pipeline (dbscan_set_small_max 0); a handle's default routes single fits of
-                 <= DBSCAN_SMALL_DEFAULT_POINTS (3072) points to the one-workgroup kernel
+                 <= DBSCAN_SMALL_DEFAULT_POINTS (8192) points to the LDS kernels, from
+                 DBSCAN_SPREAD_DEFAULT_POINTS (512) the multi-workgroup form
       train      G(10^7) (config 2) cut by the reference's EvenSplitPartitioner with
                  maxPointsPerPartition 8192 and duplicated into eps-grown partitions
                  (DBSCAN.scala:105-137): every partition fitted (a) by one dbscan_fit_h call each
@@ -526,6 +528,8 @@ def seam(args, h, threads):
                  (dbscan_fit_batch_device_async, back to back), against (d) the reference's
                  LocalDBSCANNaive.fit O(m^2) restated in C on the same partitions, `threads`
                  host threads, for a bounded sample of partitions."""
+    import ctypes
+
     import numpy as np
     import torch
 
@@ -543,20 +547,28 @@ def seam(args, h, threads):
         dcl = torch.empty(m, dtype=torch.int32, device="cuda")
         dfl = torch.empty(m, dtype=torch.uint8, device="cuda")
         row = {}
+        lib = dbscan_amd.load()
+        kk = ctypes.c_int32(0)
+        capi_args = (h.ptr, ctypes.c_void_p(tx.data_ptr()), ctypes.c_void_p(ty.data_ptr()), m,
+                     float(eps), int(mp), 0, ctypes.c_void_p(dcl.data_ptr()),
+                     ctypes.c_void_p(dfl.data_ptr()), ctypes.byref(kk))
+        torch.cuda.synchronize()
         for tag, small in (("", 8192), ("tiled_", 0)):
             if small == 0 and m > 8192:
                 continue
             h.set_small_max(small)
             reps = 30 if m <= 8192 else 10
-            for kind in ("host", "device"):
+            for kind in ("host", "device", "capi"):
                 ts = []
                 for i in range(reps + 2):
                     t0 = time.perf_counter()
                     if kind == "host":
                         dbscan_amd.fit_arrays(hx, hy, eps, mp, 0, handle=h, cluster_out=cl,
                                               flag_out=fl)
-                    else:
+                    elif kind == "device":
                         D.fit_tensors(tx, ty, eps, mp, 0, h, dcl, dfl)
+                    else:  # the C-ABI call alone, as a JNI caller makes it (inputs resident)
+                        lib.dbscan_fit_device(*capi_args)
                     if i >= 2:
                         ts.append(time.perf_counter() - t0)
                 row[f"{tag}{kind}_us"] = round(float(np.median(ts)) * 1e6, 1)
@@ -583,6 +595,29 @@ def seam(args, h, threads):
         dbscan_amd.fit_arrays(px[a:b], py[a:b], eps, mp, 0, handle=h, cluster_out=cl[a:b],
                               flag_out=fl[a:b])
     t_calls = time.perf_counter() - t0
+    # (a') the same calls from 4 executor threads with a handle each (Spark local[4]: the box
+    # gives a process 4 hardware queues), partitions dealt round-robin
+    import threading
+
+    hs = [dbscan_amd.Handle(h.device) for _ in range(4)]
+
+    def worker(t):
+        for p in range(t, npart, 4):
+            a, b = offs[p], offs[p + 1]
+            dbscan_amd.fit_arrays(px[a:b], py[a:b], eps, mp, 0, handle=hs[t], cluster_out=cl[a:b],
+                                  flag_out=fl[a:b])
+
+    for hh in hs:  # (each handle's workspace allocated before the clock starts)
+        dbscan_amd.fit_arrays(px[:1000], py[:1000], eps, mp, 0, handle=hh)
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    t_calls4 = time.perf_counter() - t0
+    for hh in hs:
+        hh.close()
     # (b) one batch call, host arrays
     ts = []
     for i in range(4):
@@ -615,6 +650,9 @@ def seam(args, h, threads):
         "partitions": npart, "points_with_halos": total,
         "per_partition_calls": {"seconds": round(t_calls, 4),
                                 "us_per_partition": round(t_calls / npart * 1e6, 2)},
+        "per_partition_calls_4_threads": {"seconds": round(t_calls4, 4),
+                                          "us_per_partition": round(t_calls4 / npart * 1e6, 2),
+                                          "points_per_s": round(total / t_calls4, 1)},
         "batch_host": {"seconds": round(t_batch, 4),
                        "us_per_partition": round(t_batch / npart * 1e6, 3),
                        "points_per_s": round(total / t_batch, 1)},

@@ -185,6 +185,7 @@ struct dbscan_handle {
     size_t bpinned_bytes = 0;
     hipEvent_t bcopied = nullptr;     // the last batch tables' upload (pinned buffer reusable)
     int64_t small_max = DBSCAN_SMALL_DEFAULT_POINTS;  // one-workgroup fits up to this many points
+    int64_t spread_min = DBSCAN_SPREAD_DEFAULT_POINTS;  // LDS fits from here: several workgroups
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
@@ -380,6 +381,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
         a.small_max = h->small_max;
+        a.spread_min = h->spread_min;
         h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
@@ -415,6 +417,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
         a.small_max = h->small_max;
+        a.spread_min = h->spread_min;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
@@ -456,6 +459,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         }
         dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
         a.small_max = h->small_max;
+        a.spread_min = h->spread_min;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         {
@@ -910,6 +914,17 @@ int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points) {
     std::lock_guard<std::mutex> lk(h->mu);
     const int64_t prev = h->small_max;
     h->small_max = std::min<int64_t>(std::max<int64_t>(max_points, 0), dbscan::kSmallMaxPoints);
+    return prev;
+}
+
+int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int64_t prev = h->spread_min;
+    h->spread_min = std::max<int64_t>(min_points, 0);
     return prev;
 }
 

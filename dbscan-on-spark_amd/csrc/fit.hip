@@ -3309,8 +3309,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     double* misc = static_cast<double*>(ws.misc.ensure(64 * sizeof(double)));
     GridParams* gp = reinterpret_cast<GridParams*>(misc + kMiscGrid);
     int32_t* st = reinterpret_cast<int32_t*>(misc + kMiscState);
-    DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
     if (n == 0) {
+        DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
         if (slab) {
             slab->valid = a.zone != nullptr;
             slab->nlroots = -1;
@@ -3320,14 +3320,19 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     const int32_t* nf_p = &st[kStNf];
     // partition-sized full fits (the seam's usual call, DBSCAN.scala:150-155): one launch,
-    // one workgroup, everything in LDS (small.hip)
+    // everything in LDS (small.hip), one workgroup or several; the kernel zeroes the fit state
     if (!a.zone && n <= std::min<int64_t>(a.small_max, kSmallMaxPoints) &&
         small_fit_eligible(n, a.eps, a.mode)) {
         StageTimer t(prof, s, "small_fit");
-        enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
-                           a.mode, a.cluster, a.flag, nullptr, gp, st);
+        if (n >= a.spread_min)  // several workgroups, two grid barriers (spread_fit_kernel)
+            enqueue_spread_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
+                               a.flag, gp, st);
+        else
+            enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
+                               a.mode, a.cluster, a.flag, nullptr, gp, st);
         return;
     }
+    DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
 
     // large direct fits sort through the padded bands (bucket_sort: cache-resident random writes)
     const bool bucketed = !a.batch && mode == kGridEps && n >= kBucketMinPoints &&
@@ -3738,10 +3743,12 @@ void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst) {
 }
 
 FitStats read_fit_stats(hipStream_t s, Workspace& ws) {
-    double buf[kFitStatsDoubles];
-    enqueue_fit_stats_copy(s, ws, buf);
+    if (!ws.stats_host)  // (pinned: a pageable copy costs a staging pass per fit)
+        DBSCAN_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ws.stats_host),
+                                       kFitStatsDoubles * sizeof(double), hipHostMallocDefault));
+    enqueue_fit_stats_copy(s, ws, ws.stats_host);
     if (ws.fit_n != 0) DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-    return parse_fit_stats(ws, buf);
+    return parse_fit_stats(ws, ws.stats_host);
 }
 
 FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
@@ -3753,6 +3760,9 @@ FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
     memcpy(&g, buf + kMiscGrid, sizeof(g));
     int32_t v[kStTileBuckets];  // (the stats copy holds the states before the buckets)
     memcpy(v, buf + kMiscState, sizeof(v));
+    if (v[kStError] == 2)  // (spread_fit_kernel: its workgroups were not all resident)
+        throw HipError(hipErrorLaunchTimeOut, "spread_fit_kernel grid barrier (workgroups not resident)",
+                       __FILE__, __LINE__);
     if (v[kStError]) throw ArgError{"cannot size the eps grid"};
     stats.nf = v[kStNf];
     if (ws.fit_mode == kGridEps && stats.nf == 0) stats.grid_mode = kGridNoPairs;

@@ -173,7 +173,14 @@ struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
-        key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, route, route_tab;
+        key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, route, route_tab,
+        spread;
+    bool spread_ready = false;  // spread.p holds zeroed barrier words (small.hip)
+    double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
+    Workspace() = default;
+    ~Workspace() {
+        if (stats_host) (void)hipHostFree(stats_host);
+    }
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
     int64_t fit_n = 0;               // the last enqueued fit
@@ -189,8 +196,11 @@ struct Workspace {
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &lroots,
                           &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm, &route,
-                          &route_tab})
+                          &route_tab, &spread})
             b->release();
+        spread_ready = false;
+        if (stats_host) (void)hipHostFree(stats_host);
+        stats_host = nullptr;
     }
 };
 
@@ -273,6 +283,8 @@ struct FitArgs {
     // full fits of n <= small_max points (and a mode / eps the one-workgroup kernel serves) run
     // small.hip's single-launch fit; 0 keeps every fit on the tiled pipeline
     int64_t small_max = 0;  // (0: the tiled pipeline; entry points opt in from the handle)
+    // ... of which fits of >= spread_min points spread over several workgroups of one launch
+    int64_t spread_min = INT64_MAX;
     // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
     const BatchFit* batch = nullptr;
 };
@@ -393,6 +405,12 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
                         int64_t single_n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, int32_t* d_nclusters, GridParams* gp,
                         int32_t* st);
+// One fit of n <= kSmallMaxPoints points spread over several workgroups of one launch
+// (small.hip, spread_fit_kernel): the same results as the one-workgroup fit; statistics into
+// st / gp (the handle's fit state), st[kStError] = 2 if a grid barrier gave up.
+void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
+                        const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
+                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st);
 // DBSCAN.scala:116-137 on the host: the points every partition's outer rectangle (main grown
 // by eps, inclusive) holds, in input order (partition.hip)
 int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,

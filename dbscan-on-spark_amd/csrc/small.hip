@@ -229,41 +229,41 @@ __device__ void sm_make_grid(double xmin, double xmax, double ymin, double ymax,
     g->hi = __double2float_ru(e2 + M);
 }
 
-// One partition per workgroup.  offs == nullptr: one partition [0, single_n) (blockIdx 0);
-// else partition list[blockIdx.x] = points [offs[p], offs[p+1]).  nclusters[p] (or st) gets its
-// cluster count.  st/gp (single fits only): the handle's fit statistics.
-__global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
-    const double* __restrict__ x, const double* __restrict__ y, const int64_t* __restrict__ offs,
-    const int32_t* __restrict__ list, int64_t single_n, double eps, double eps2, int min_points,
-    int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
-    int32_t* __restrict__ nclusters, GridParams* __restrict__ gp, int32_t* __restrict__ st) {
-    __shared__ float2 rec[kSmN];           // fp32 records by slot
-    __shared__ uint32_t info[kSmN];        // visit index << 16 | cell (kNoCell: outside the grid)
-    __shared__ int par[kSmN];              // sort cursors, then union-find parents (slots)
-    __shared__ uint16_t cst[kSmCells + 2];  // first slot of every cell; cst[ncells] = nf
-    __shared__ uint8_t core[kSmN];
-    __shared__ uint32_t rbits[kSmN / 32];  // roots by visit index
-    __shared__ int wrank[kSmN / 32];       // roots before each word
-    __shared__ double red[5][kSmW];
-    __shared__ int wsc[kSmW + 1];
-    __shared__ int nonfin;
-    __shared__ SmGrid G;
-    __shared__ uint32_t sbest[kSmT / 3 + 1];  // row-split labels: min root per point
+// A partition staged in one workgroup's LDS (small_fit_kernel, spread_fit_kernel).
+struct SmLds {
+    float2 rec[kSmN];           // fp32 records by slot
+    uint32_t info[kSmN];        // visit index << 16 | quadrant << 13 | cell (kNoCell: no cell)
+    int par[kSmN];              // sort cursors, then union-find parents
+    uint16_t cst[kSmCells + 2];  // first slot of every cell; cst[ncells] = nf
+    uint8_t core[kSmN];         // by slot
+    uint32_t rbits[kSmN / 32];  // roots by visit index
+    int wrank[kSmN / 32];       // roots before each word
+    double red[5][kSmW];
+    int wsc[kSmW + 1];
+    int nonfin;
+    int band[4];  // spread fits: the owned slots [band[0], band[1]), the published pair count
+    SmGrid G;
+    uint32_t sbest[kSmT / 3 + 1];  // row-split phases: per-point counters / min roots
+};
 
+// What the stencil walks read in registers (from L.G, once per kernel)
+struct SmCtx {
+    const double* px;
+    const double* py;
+    double eps2;
+    float lo, hi;
+    int nx, ny;
+    bool exact_only;
+};
+
+// ---- load + bbox + grid + counting sort by cell (points [0, m) of px, py) ----
+// false: the grid could not be sized.  occupied: this thread's share of the occupied cells.
+// The order of the slots inside a cell depends on LDS atomics; nothing computed from the stage
+// depends on it (spread_fit_kernel's workgroups each stage the partition, in their own order).
+__device__ __forceinline__ bool sm_stage(SmLds& L, const double* __restrict__ px,
+                                         const double* __restrict__ py, int m, double eps,
+                                         double eps2, int& occupied) {
     const int tid = threadIdx.x;
-    int64_t off = 0, m64 = single_n;
-    int part = 0;
-    if (offs) {
-        part = list[blockIdx.x];
-        off = offs[part];
-        m64 = offs[part + 1] - off;
-    }
-    const int m = (int)m64;  // the host routes only m <= kSmN here
-    const double* px = x + off;
-    const double* py = y + off;
-    SM_STAMP(0);
-
-    // ---- load + bbox ----
     double vx[kSmPer], vy[kSmPer];
     double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, nfin = 0;
 #pragma unroll
@@ -283,8 +283,8 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
             }
         }
     }
-    if (tid < kSmN / 32) rbits[tid] = 0;
-    if (tid == 0) nonfin = 0;
+    if (tid < kSmN / 32) L.rbits[tid] = 0;
+    if (tid == 0) L.nonfin = 0;
     {
         const int lane = tid & 63, w = tid >> 6;
         mnx = wave_min(mnx);
@@ -294,36 +294,31 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) nfin += __shfl_xor(nfin, o, 64);
         if (lane == 0) {
-            red[0][w] = mnx;
-            red[1][w] = mxx;
-            red[2][w] = mny;
-            red[3][w] = mxy;
-            red[4][w] = nfin;
+            L.red[0][w] = mnx;
+            L.red[1][w] = mxx;
+            L.red[2][w] = mny;
+            L.red[3][w] = mxy;
+            L.red[4][w] = nfin;
         }
         __syncthreads();
         if (tid == 0) {
             for (int k = 1; k < kSmW; ++k) {
-                red[0][0] = fmin(red[0][0], red[0][k]);
-                red[1][0] = fmax(red[1][0], red[1][k]);
-                red[2][0] = fmin(red[2][0], red[2][k]);
-                red[3][0] = fmax(red[3][0], red[3][k]);
-                red[4][0] += red[4][k];
+                L.red[0][0] = fmin(L.red[0][0], L.red[0][k]);
+                L.red[1][0] = fmax(L.red[1][0], L.red[1][k]);
+                L.red[2][0] = fmin(L.red[2][0], L.red[2][k]);
+                L.red[3][0] = fmax(L.red[3][0], L.red[3][k]);
+                L.red[4][0] += L.red[4][k];
             }
-            sm_make_grid(red[0][0], red[1][0], red[2][0], red[3][0], (int)red[4][0], eps, eps2,
-                         &G);
+            sm_make_grid(L.red[0][0], L.red[1][0], L.red[2][0], L.red[3][0], (int)L.red[4][0], eps,
+                         eps2, &L.G);
         }
         __syncthreads();
     }
     SM_STAMP(1);
-    const int nf = G.nf;
-    const int nx = G.nx, ny = G.ny, ncells = G.ncells;
-    if (G.bad) {  // (unreachable for finite bboxes: 4096 doublings span every double extent)
-        if (tid == 0 && st) st[kStError] = 1;
-        return;
-    }
+    if (L.G.bad) return false;  // (unreachable for finite bboxes: 4096 doublings span any extent)
+    const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny, ncells = L.G.ncells;
 
-    // ---- counting sort by cell ----
-    for (int c = tid; c < ncells; c += kSmT) par[c] = 0;
+    for (int c = tid; c < ncells; c += kSmT) L.par[c] = 0;
     __syncthreads();
     int mycell[kSmPer];
 #pragma unroll
@@ -332,38 +327,38 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         mycell[k] = -1;
         if (i < m && isfinite(vx[k]) && isfinite(vy[k])) {
             // quarter-grid coordinates: floor(2t) >> 1 == floor(t) exactly (2t is exact)
-            int qx = (int)floor(2.0 * ((vx[k] * 0.5 - G.xmin2) * G.invx));
-            int qy = (int)floor(2.0 * ((vy[k] * 0.5 - G.ymin2) * G.invy));
+            int qx = (int)floor(2.0 * ((vx[k] * 0.5 - L.G.xmin2) * L.G.invx));
+            int qy = (int)floor(2.0 * ((vy[k] * 0.5 - L.G.ymin2) * L.G.invy));
             qx = min(max(qx, 0), 2 * nx - 1);
             qy = min(max(qy, 0), 2 * ny - 1);
             const int c = (qy >> 1) * nx + (qx >> 1);
             mycell[k] = c | (((qy & 1) << 1 | (qx & 1)) << 13);
-            atomicAdd(&par[c], 1);
+            atomicAdd(&L.par[c], 1);
         }
     }
     __syncthreads();
-    int occupied = 0;
+    occupied = 0;
     {
         int cnt[kSmCellPer], sum = 0;
 #pragma unroll
         for (int k = 0; k < kSmCellPer; ++k) {
             const int c = tid * kSmCellPer + k;
-            cnt[k] = c < ncells ? par[c] : 0;
+            cnt[k] = c < ncells ? L.par[c] : 0;
             sum += cnt[k];
             occupied += cnt[k] > 0 ? 1 : 0;
         }
         int tot = 0;
-        int run = sm_excl_scan(sum, wsc, &tot);
+        int run = sm_excl_scan(sum, L.wsc, &tot);
 #pragma unroll
         for (int k = 0; k < kSmCellPer; ++k) {
             const int c = tid * kSmCellPer + k;
             if (c < ncells) {
-                par[c] = run;
-                cst[c] = (uint16_t)run;
+                L.par[c] = run;
+                L.cst[c] = (uint16_t)run;
             }
             run += cnt[k];
         }
-        if (tid == 0) cst[ncells] = (uint16_t)nf;
+        if (tid == 0) L.cst[ncells] = (uint16_t)nf;
     }
     __syncthreads();
 #pragma unroll
@@ -371,67 +366,272 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         const int i = tid + k * kSmT;
         if (i >= m) continue;
         if (mycell[k] >= 0) {
-            const int s = atomicAdd(&par[mycell[k] & kCellMask], 1);
-            rec[s] = make_float2((float)((vx[k] * 0.5 - G.cx2) * G.invs),
-                                 (float)((vy[k] * 0.5 - G.cy2) * G.invs));
-            info[s] = ((uint32_t)i << 16) | (uint32_t)mycell[k];
+            const int s = atomicAdd(&L.par[mycell[k] & kCellMask], 1);
+            L.rec[s] = make_float2((float)((vx[k] * 0.5 - L.G.cx2) * L.G.invs),
+                                   (float)((vy[k] * 0.5 - L.G.cy2) * L.G.invs));
+            L.info[s] = ((uint32_t)i << 16) | (uint32_t)mycell[k];
         } else {
-            const int s = nf + atomicAdd(&nonfin, 1);
-            info[s] = ((uint32_t)i << 16) | kNoCell;
+            const int s = nf + atomicAdd(&L.nonfin, 1);
+            L.info[s] = ((uint32_t)i << 16) | kNoCell;
         }
     }
     __syncthreads();
+    return true;
+}
 
-    SM_STAMP(2);
-    // ---- stencil walk helpers ----
-    const float lo = G.lo, hi = G.hi;
-    const bool exact_only = G.exact_only != 0;
-    // neighbour test of slots p (record me) and q (record rq)
-    auto pair = [&](int p, float2 me, int q, float2 rq) -> bool {
-        if (!exact_only) {
-            const float F = sm_d2(me, rq);
-            if (F <= lo) return true;
-            if (F > hi) return false;
+__device__ __forceinline__ SmCtx sm_ctx(const SmLds& L, const double* px, const double* py,
+                                        double eps2) {
+    return {px, py, eps2, L.G.lo, L.G.hi, L.G.nx, L.G.ny, L.G.exact_only != 0};
+}
+
+// neighbour test of slots p (record me) and q (record rq)
+__device__ __forceinline__ bool sm_pair(const SmLds& L, const SmCtx& c, int p, float2 me, int q,
+                                        float2 rq) {
+    if (!c.exact_only) {
+        const float F = sm_d2(me, rq);
+        if (F <= c.lo) return true;
+        if (F > c.hi) return false;
+    }
+    const int vp = (int)(L.info[p] >> 16), vq = (int)(L.info[q] >> 16);
+    return sm_within(c.px[vp], c.py[vp], c.px[vq], c.py[vq], c.eps2);
+}
+
+// f(q, rec[q], w) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own row
+// first), w = the 6x6 quarter-window position of q's cell: (row 0..2) * 3 + col 0..2 (rows cy-1,
+// cy, cy+1 -> 0, 1, 2); f returns false to stop.  The candidates' records are loaded kSmBatch at
+// a time (their LDS reads in flight together: the walks are bound by the latency of dependent
+// LDS reads, not by their count).  only = 0..2: that row alone (row-split phases), -1: all three.
+constexpr int kSmBatch = 4;
+// part / nparts: only that share of each row's candidates (spread fits split long walks)
+__device__ __forceinline__ void sm_row_part(int& qs, int& e, int part, int nparts) {
+    if (nparts > 1 && e > qs) {
+        const int len = e - qs;
+        e = qs + len * (part + 1) / nparts;
+        qs = qs + len * part / nparts;
+    }
+}
+template <class F>
+__device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_, int p, int qmin,
+                                               F&& f, int only, int part = 0, int nparts = 1) {
+    const int nx = cx_.nx, ny = cx_.ny;
+    const int c = (int)(L.info[p] & kCellMask);
+    const int cy = c / nx, cx = c - cy * nx;
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        if (only >= 0 && d != only) continue;
+        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+        if (r < 0 || r >= ny) continue;
+        const int rb = r * nx;
+        int e = L.cst[rb + x1 + 1];
+        // boundaries of the row's second and third cell (q's column = x0 + crossings)
+        const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
+        const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
+        const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
+        int qs = max((int)L.cst[rb + x0], qmin);
+        sm_row_part(qs, e, part, nparts);
+        for (int q = qs; q < e; q += kSmBatch) {
+            float2 rq[kSmBatch];
+#pragma unroll
+            for (int u = 0; u < kSmBatch; ++u) rq[u] = L.rec[min(q + u, e - 1)];
+#pragma unroll
+            for (int u = 0; u < kSmBatch; ++u) {
+                const int qq = q + u;
+                if (qq < e && !f(qq, rq[u], wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0)))
+                    return;
+            }
         }
-        const int vp = (int)(info[p] >> 16), vq = (int)(info[q] >> 16);
-        return sm_within(px[vp], py[vp], px[vq], py[vq], eps2);
-    };
-    // f(q, rec[q], w) for every slot q >= qmin of slot p's 3x3 stencil (three row ranges, own
-    // row first), w = the 6x6 quarter-window position of q's cell: (row 0..2) * 3 + col 0..2
-    // (rows cy-1, cy, cy+1 -> 0, 1, 2); f returns false to stop.  The candidates' records are
-    // loaded kSmBatch at a time (their LDS reads in flight together: the walks are bound by
-    // the latency of dependent LDS reads, not by their count).
-    constexpr int kSmBatch = 4;
-    // only = 0..2: that row alone (row-split fits), -1: all three
-    auto for_stencil = [&](int p, int qmin, auto&& f, int only = -1) {
-        const int c = (int)(info[p] & kCellMask);
-        const int cy = c / nx, cx = c - cy * nx;
-        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+    }
+}
+
+// |N(p)| capped at minPoints over stencil row `only` (-1: all rows; LocalDBSCANNaive.scala:52-56)
+__device__ __forceinline__ int sm_count(const SmLds& L, const SmCtx& c, int p, int min_points,
+                                        int only, int part = 0, int nparts = 1) {
+    const float2 me = L.rec[p];
+    int cnt = 0;
+    sm_for_stencil(L, c, p, 0, [&](int q, float2 rq, int) {
+        cnt += sm_pair(L, c, p, me, q, rq) ? 1 : 0;
+        return cnt < min_points;
+    }, only, part, nparts);
+    return cnt;
+}
+
+// Core p's unions over core-core pairs (each unordered pair from its smaller slot: q > p) in
+// stencil row `only` (-1: all rows), union-find over slots in L.par.
+// Clique grids: p unites with the FIRST core q > p of each quarter cell (side ~eps/2, a clique)
+// of its stencil within eps, and no other of that quarter.  Enough: the cores of one quarter
+// are chained (each to the next core of its quarter), and a pair p < q within eps makes p unite
+// with some core of q's quarter.  So a dense cell costs a few unions per point instead of one
+// per neighbour.  reach_k: record -> cell-local coordinate offsets (clique grids).
+__device__ __forceinline__ void sm_union_walk(SmLds& L, const SmCtx& cx_, int p, int only,
+                                              bool quarters, double reach_kx, double reach_ky,
+                                              int part = 0, int nparts = 1) {
+    const int nx = cx_.nx, ny = cx_.ny;
+    const float2 me = L.rec[p];
+    uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
+    // a root of p's set (possibly stale: it stays an ancestor of p, so a q whose parent it is
+    // belongs to p's set already and needs neither a pair test nor a union)
+    int rp = sm_find(L.par, p);
+    // the stencil walk of sm_for_stencil with each batch's records, infos, core flags and
+    // parents loaded together (the walk is bound by dependent LDS reads: one round trip per
+    // batch instead of three per candidate).  A parent read before a union of this batch is
+    // still an ancestor of that candidate, so `parent == rp` still proves p's set.
+    const int c = (int)(L.info[p] & kCellMask);
+    const int cy = c / nx, cx = c - cy * nx;
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+    if (quarters && !cx_.exact_only) {
+        // quarters of the 6x6 window wholly beyond eps of p (their nearest point farther than
+        // the F threshold plus a margin over the fp32 records' error) count as done
+        const float tx = (float)((double)me.x + reach_kx - (double)cx);
+        const float ty = (float)((double)me.y + reach_ky - (double)cy);
+        const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
+        const float rr = (sqrtf(cx_.hi) + mg) * (sqrtf(cx_.hi) + mg);
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (only >= 0 && d != only) continue;
-            const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
-            if (r < 0 || r >= ny) continue;
-            const int rb = r * nx;
-            const int e = cst[rb + x1 + 1];
-            // boundaries of the row's second and third cell (q's column = x0 + crossings)
-            const int b1 = x0 + 1 <= x1 ? (int)cst[rb + x0 + 1] : 0x7FFFFFFF;
-            const int b2 = x0 + 2 <= x1 ? (int)cst[rb + x0 + 2] : 0x7FFFFFFF;
-            const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
-            for (int q = max((int)cst[rb + x0], qmin); q < e; q += kSmBatch) {
-                float2 rq[kSmBatch];
+        for (int a = 0; a < 6; ++a) {
+            const float y0 = 0.5f * (float)a - 1.0f,
+                        dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
 #pragma unroll
-                for (int u = 0; u < kSmBatch; ++u) rq[u] = rec[min(q + u, e - 1)];
+            for (int b = 0; b < 6; ++b) {
+                const float xb = 0.5f * (float)b - 1.0f;
+                const float dx = fmaxf(0.0f, fmaxf(xb - tx, tx - (xb + 0.5f)));
+                if (dx * dx + dy * dy > rr) done |= 1ull << (a * 6 + b);
+            }
+        }
+    }
 #pragma unroll
-                for (int u = 0; u < kSmBatch; ++u) {
-                    const int qq = q + u;
-                    if (qq < e &&
-                        !f(qq, rq[u], wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0)))
-                        return;
+    for (int d = 0; d < 3; ++d) {
+        if (only >= 0 && d != only) continue;
+        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+        if (r < 0 || r >= ny) continue;
+        const int rb = r * nx;
+        int e = L.cst[rb + x1 + 1];
+        const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
+        const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
+        const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
+        int qs = max((int)L.cst[rb + x0], p + 1);
+        sm_row_part(qs, e, part, nparts);
+        for (int q = qs; q < e; q += kSmBatch) {
+            if (quarters) {
+                // every quarter of q's cell done: the rest of the cell needs no visit
+                const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
+                const int sh = 2 * (w / 3) * 6 + 2 * (w % 3);
+                const uint64_t m4 = (3ull << sh) | (3ull << (sh + 6));
+                if ((done & m4) == m4) {
+                    q = min(q < b1 ? b1 : (q < b2 ? b2 : e), e) - kSmBatch;
+                    continue;
+                }
+            }
+            float2 rq[kSmBatch];
+            uint32_t iq[kSmBatch];
+            int pq[kSmBatch];
+            bool cq[kSmBatch];
+#pragma unroll
+            for (int u = 0; u < kSmBatch; ++u) {
+                const int qq = min(q + u, e - 1);
+                rq[u] = L.rec[qq];
+                iq[u] = L.info[qq];
+                cq[u] = L.core[qq] != 0;
+                pq[u] = sm_ld(L.par + qq);
+            }
+#pragma unroll
+            for (int u = 0; u < kSmBatch; ++u) {
+                const int qq = q + u;
+                if (qq >= e || !cq[u]) continue;
+                int bit = 0;
+                if (quarters) {
+                    const int w = wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0);
+                    const int qd = (int)((iq[u] >> 13) & 3u);
+                    bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
+                    if ((done >> bit) & 1ull) continue;
+                }
+                if (pq[u] == rp) {
+                    if (quarters) done |= 1ull << bit;
+                    continue;
+                }
+                if (sm_pair(L, cx_, p, me, qq, rq[u])) {
+                    // unite from the root p's walk holds (finding p's root again measured
+                    // slower: 370 -> 348 us at 8192 points)
+                    rp = sm_unite_from(L.par, L.info, rp, qq);
+                    if (quarters) done |= 1ull << bit;
                 }
             }
         }
-    };
+    }
+}
+
+// The smallest root visit index among non-core p's core neighbours in stencil row `only`
+// (root_of(q): the root visit index of core slot q)
+template <class RootF>
+__device__ __forceinline__ uint32_t sm_best_root(const SmLds& L, const SmCtx& c, int p, int only,
+                                                 RootF root_of) {
+    const float2 me = L.rec[p];
+    uint32_t best = 0xFFFFFFFFu;
+    sm_for_stencil(L, c, p, 0, [&](int q, float2 rq, int) {
+        if (L.core[q]) {
+            const uint32_t s = root_of(q);
+            if (s < best && sm_pair(L, c, p, me, q, rq)) best = s;
+        }
+        return true;
+    }, only);
+    return best;
+}
+
+// 1 + roots with a smaller visit index (the reference's cluster id of the cluster s(K) opens)
+__device__ __forceinline__ int sm_cluster_of(const SmLds& L, uint32_t s) {
+    return L.wrank[s >> 5] + __popc(L.rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
+}
+
+// Slot p's label (LocalDBSCANNaive.scala:89-106; Archery re-claim LocalDBSCANArchery.scala:
+// 103-106): cores their root's cluster (root_v: the root's visit index), non-cores the cluster
+// of best (min s(K) over core neighbours) under the Naive / Archery rule; written in input order.
+__device__ __forceinline__ void sm_write_label(const SmLds& L, int p, uint32_t root_v,
+                                               uint32_t best, int mode, int32_t* cl_out,
+                                               uint8_t* fl_out) {
+    const uint32_t v = L.info[p] >> 16;
+    int cid = 0;
+    uint8_t f = DBSCAN_FLAG_NOISE;
+    if (L.core[p]) {
+        cid = sm_cluster_of(L, root_v);
+        f = DBSCAN_FLAG_CORE;
+    } else if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
+        cid = sm_cluster_of(L, best);
+        f = DBSCAN_FLAG_BORDER;
+    }
+    cl_out[v] = cid;
+    fl_out[v] = f;
+}
+
+// One partition per workgroup.  offs == nullptr: one partition [0, single_n) (blockIdx 0);
+// else partition list[blockIdx.x] = points [offs[p], offs[p+1]).  nclusters[p] (or st) gets its
+// cluster count.  st/gp (single fits only): the handle's fit statistics.
+__global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, const int64_t* __restrict__ offs,
+    const int32_t* __restrict__ list, int64_t single_n, double eps, double eps2, int min_points,
+    int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
+    int32_t* __restrict__ nclusters, GridParams* __restrict__ gp, int32_t* __restrict__ st) {
+    __shared__ SmLds L;
+
+    const int tid = threadIdx.x;
+    int64_t off = 0, m64 = single_n;
+    int part = 0;
+    if (offs) {
+        part = list[blockIdx.x];
+        off = offs[part];
+        m64 = offs[part + 1] - off;
+    }
+    const int m = (int)m64;  // the host routes only m <= kSmN here
+    const double* px = x + off;
+    const double* py = y + off;
+    SM_STAMP(0);
+    if (st && tid < kStCount) st[tid] = 0;  // (the fit state: no memset ahead of the launch)
+    int occupied = 0;
+    if (!sm_stage(L, px, py, m, eps, eps2, occupied)) {
+        if (tid == 0 && st) st[kStError] = 1;
+        return;
+    }
+    SM_STAMP(2);
+    const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny;
+    const SmCtx c = sm_ctx(L, px, py, eps2);
 
     // Row split (partitions of <= kSmT / 3 points, where most threads would idle): each point's
     // three stencil rows are walked by three threads, counts summed and label minima taken in
@@ -441,148 +641,44 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     // ---- count: core <=> |N(p)| >= minPoints (LocalDBSCANNaive.scala:52-56,99-101) ----
     int ncore_local = 0;
     if (split) {
-        if (tid < m) par[tid] = 0;  // (per-point counters until the union needs par)
+        if (tid < m) L.par[tid] = 0;  // (per-point counters until the union needs par)
         __syncthreads();
         if (tid < 3 * m && min_points > 0) {
             const int p = tid / 3, d = tid - 3 * (tid / 3);
-            if (p < nf) {
-                const float2 me = rec[p];
-                int cnt = 0;  // a row alone reaching minPoints decides the point
-                for_stencil(p, 0, [&](int q, float2 rq, int) {
-                    cnt += pair(p, me, q, rq) ? 1 : 0;
-                    return cnt < min_points;
-                }, d);
-                if (cnt) atomicAdd(&par[p], cnt);
+            if (p < nf) {  // a row alone reaching minPoints decides the point
+                const int cnt = sm_count(L, c, p, min_points, d);
+                if (cnt) atomicAdd(&L.par[p], cnt);
             }
         }
         __syncthreads();
         if (tid < m) {
-            const bool c = min_points <= 0 || (tid < nf && par[tid] >= min_points);
-            core[tid] = c ? 1 : 0;
-            par[tid] = tid;
-            ncore_local = c ? 1 : 0;
+            const bool cc = min_points <= 0 || (tid < nf && L.par[tid] >= min_points);
+            L.core[tid] = cc ? 1 : 0;
+            L.par[tid] = tid;
+            ncore_local = cc ? 1 : 0;
         }
     } else {
         for (int p = tid; p < m; p += kSmT) {
-            bool c = min_points <= 0;
-            if (!c && p < nf) {
-                const float2 me = rec[p];
-                int cnt = 0;
-                for_stencil(p, 0, [&](int q, float2 rq, int) {
-                    cnt += pair(p, me, q, rq) ? 1 : 0;
-                    return cnt < min_points;
-                });
-                c = cnt >= min_points;
-            }
-            core[p] = c ? 1 : 0;
-            par[p] = p;
-            ncore_local += c ? 1 : 0;
+            bool cc = min_points <= 0;
+            if (!cc && p < nf) cc = sm_count(L, c, p, min_points, -1) >= min_points;
+            L.core[p] = cc ? 1 : 0;
+            L.par[p] = p;
+            ncore_local += cc ? 1 : 0;
         }
     }
     __syncthreads();
     SM_STAMP(3);
 
-    // ---- union over core-core pairs (each unordered pair from its smaller slot: q > p) ----
-    // Clique grids: every core p unites with the FIRST core q > p of each quarter cell (side
-    // ~eps/2, a clique) of its stencil within eps, and no other of that quarter.  Enough: the
-    // cores of one quarter are chained (each to the next core of its quarter), and a pair p < q
-    // within eps makes p unite with some core of q's quarter.  So a dense cell costs a few
-    // unions per point instead of one per neighbour.
-    const bool quarters = G.clique != 0;
+    // ---- union over core-core pairs ----
+    const bool quarters = L.G.clique != 0;
     // record -> cell-local coordinate: (v*0.5 - xmin2)*invx - cx = rec + (cx2 - xmin2)*invx - cx
     // (clique grids: invx = invy = invs)
-    const double reach_kx = (G.cx2 - G.xmin2) * G.invx, reach_ky = (G.cy2 - G.ymin2) * G.invy;
+    const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
+    const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy;
     const int R = split ? 3 : 1;  // stencil rows per work item
     for (int it = tid; it < nf * R; it += kSmT) {
         const int p = split ? it / 3 : it, only = split ? it - 3 * (it / 3) : -1;
-        if (!core[p]) continue;
-        const float2 me = rec[p];
-        uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
-        // a root of p's set (possibly stale: it stays an ancestor of p, so a q whose parent it
-        // is belongs to p's set already and needs neither a pair test nor a union)
-        int rp = sm_find(par, p);
-        // the stencil walk of for_stencil with each batch's records, infos, core flags and
-        // parents loaded together (the walk is bound by dependent LDS reads: one round trip per
-        // batch instead of three per candidate).  A parent read before a union of this batch is
-        // still an ancestor of that candidate, so `parent == rp` still proves p's set.
-        const int c = (int)(info[p] & kCellMask);
-        const int cy = c / nx, cx = c - cy * nx;
-        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
-        if (quarters && !exact_only) {
-            // quarters of the 6x6 window wholly beyond eps of p (their nearest point farther
-            // than the F threshold plus a margin over the fp32 records' error) count as done
-            const float tx = (float)((double)me.x + reach_kx - (double)cx);
-            const float ty = (float)((double)me.y + reach_ky - (double)cy);
-            const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
-            const float rr = (sqrtf(hi) + mg) * (sqrtf(hi) + mg);
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const float y0 = 0.5f * (float)a - 1.0f, dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
-#pragma unroll
-                for (int b = 0; b < 6; ++b) {
-                    const float xb = 0.5f * (float)b - 1.0f;
-                    const float dx = fmaxf(0.0f, fmaxf(xb - tx, tx - (xb + 0.5f)));
-                    if (dx * dx + dy * dy > rr) done |= 1ull << (a * 6 + b);
-                }
-            }
-        }
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (only >= 0 && d != only) continue;
-            const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
-            if (r < 0 || r >= ny) continue;
-            const int rb = r * nx;
-            const int e = cst[rb + x1 + 1];
-            const int b1 = x0 + 1 <= x1 ? (int)cst[rb + x0 + 1] : 0x7FFFFFFF;
-            const int b2 = x0 + 2 <= x1 ? (int)cst[rb + x0 + 2] : 0x7FFFFFFF;
-            const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
-            for (int q = max((int)cst[rb + x0], p + 1); q < e; q += kSmBatch) {
-                if (quarters) {
-                    // every quarter of q's cell done: the rest of the cell needs no visit
-                    const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
-                    const int sh = 2 * (w / 3) * 6 + 2 * (w % 3);
-                    const uint64_t m4 = (3ull << sh) | (3ull << (sh + 6));
-                    if ((done & m4) == m4) {
-                        q = min(q < b1 ? b1 : (q < b2 ? b2 : e), e) - kSmBatch;
-                        continue;
-                    }
-                }
-                float2 rq[kSmBatch];
-                uint32_t iq[kSmBatch];
-                int pq[kSmBatch];
-                bool cq[kSmBatch];
-#pragma unroll
-                for (int u = 0; u < kSmBatch; ++u) {
-                    const int qq = min(q + u, e - 1);
-                    rq[u] = rec[qq];
-                    iq[u] = info[qq];
-                    cq[u] = core[qq] != 0;
-                    pq[u] = sm_ld(par + qq);
-                }
-#pragma unroll
-                for (int u = 0; u < kSmBatch; ++u) {
-                    const int qq = q + u;
-                    if (qq >= e || !cq[u]) continue;
-                    int bit = 0;
-                    if (quarters) {
-                        const int w = wr + (qq >= b1 ? 1 : 0) + (qq >= b2 ? 1 : 0);
-                        const int qd = (int)((iq[u] >> 13) & 3u);
-                        bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
-                        if ((done >> bit) & 1ull) continue;
-                    }
-                    if (pq[u] == rp) {
-                        if (quarters) done |= 1ull << bit;
-                        continue;
-                    }
-                    if (pair(p, me, qq, rq[u])) {
-                        // unite from the root p's walk holds (finding p's root again
-                        // measured slower: 370 -> 348 us at 8192 points)
-                        rp = sm_unite_from(par, info, rp, qq);
-                        if (quarters) done |= 1ull << bit;
-                    }
-                }
-            }
-        }
+        if (L.core[p]) sm_union_walk(L, c, p, only, quarters, reach_kx, reach_ky);
     }
     __syncthreads();
     SM_STAMP(4);
@@ -595,86 +691,63 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     for (int k = 0; k < kSmPer; ++k) {
         const int p = tid + k * kSmT;
         myroot[k] = -1;
-        if (p < m && core[p]) {
+        if (p < m && L.core[p]) {
             int r = p;
-            for (int u = par[r]; u != r; u = par[r]) r = u;
+            for (int u = L.par[r]; u != r; u = L.par[r]) r = u;
             myroot[k] = r;
             if (r == p) {
-                const uint32_t v = info[p] >> 16;
-                atomicOr(&rbits[v >> 5], 1u << (v & 31u));
+                const uint32_t v = L.info[p] >> 16;
+                atomicOr(&L.rbits[v >> 5], 1u << (v & 31u));
             }
         }
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kSmPer; ++k)
-        if (myroot[k] >= 0) par[tid + k * kSmT] = myroot[k];
+        if (myroot[k] >= 0) L.par[tid + k * kSmT] = myroot[k];
     int nclust = 0;
     {
-        const int v = tid < kSmN / 32 ? __popc(rbits[tid]) : 0;
-        const int r = sm_excl_scan(v, wsc, &nclust);  // (its barriers also order the compression)
-        if (tid < kSmN / 32) wrank[tid] = r;
+        const int v = tid < kSmN / 32 ? __popc(L.rbits[tid]) : 0;
+        const int r = sm_excl_scan(v, L.wsc, &nclust);  // (its barriers also order the compression)
+        if (tid < kSmN / 32) L.wrank[tid] = r;
     }
     __syncthreads();
     SM_STAMP(5);
-    auto cluster_of = [&](uint32_t s) -> int {  // 1 + roots with a smaller visit index
-        return wrank[s >> 5] + __popc(rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
-    };
 
-    // ---- labels (LocalDBSCANNaive.scala:89-106; Archery re-claim :103-106) ----
+    // ---- labels ----
     int32_t* cl_out = cluster + off;
     uint8_t* fl_out = flag + off;
-    // the smallest root visit index among p's core neighbours in stencil row `only`
-    auto best_root = [&](int p, int only) -> uint32_t {
-        const float2 me = rec[p];
-        uint32_t best = 0xFFFFFFFFu;
-        for_stencil(p, 0, [&](int q, float2 rq, int) {
-            if (core[q]) {
-                const uint32_t s = info[par[q]] >> 16;
-                if (s < best && pair(p, me, q, rq)) best = s;
-            }
-            return true;
-        }, only);
-        return best;
-    };
-    auto write_label = [&](int p, uint32_t best) {
-        const uint32_t v = info[p] >> 16;
-        int cid = 0;
-        uint8_t f = DBSCAN_FLAG_NOISE;
-        if (core[p]) {
-            cid = cluster_of(info[par[p]] >> 16);
-            f = DBSCAN_FLAG_CORE;
-        } else if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
-            cid = cluster_of(best);
-            f = DBSCAN_FLAG_BORDER;
-        }
-        cl_out[v] = cid;
-        fl_out[v] = f;
-    };
+    const auto root_of = [&](int q) { return L.info[L.par[q]] >> 16; };
     if (split) {
-        if (tid < m) sbest[tid] = 0xFFFFFFFFu;
+        if (tid < m) L.sbest[tid] = 0xFFFFFFFFu;
         __syncthreads();
         if (tid < 3 * m) {
             const int p = tid / 3;
-            if (!core[p] && p < nf) {
-                const uint32_t b = best_root(p, tid - 3 * p);
-                if (b != 0xFFFFFFFFu) atomicMin(&sbest[p], b);
+            if (!L.core[p] && p < nf) {
+                const uint32_t b = sm_best_root(L, c, p, tid - 3 * p, root_of);
+                if (b != 0xFFFFFFFFu) atomicMin(&L.sbest[p], b);
             }
         }
         __syncthreads();
-        if (tid < m) write_label(tid, sbest[tid]);
+        if (tid < m)
+            sm_write_label(L, tid, L.core[tid] ? root_of(tid) : 0u, L.sbest[tid], mode, cl_out,
+                           fl_out);
     } else {
-        for (int p = tid; p < m; p += kSmT)
-            write_label(p, (!core[p] && p < nf) ? best_root(p, -1) : 0xFFFFFFFFu);
+        for (int p = tid; p < m; p += kSmT) {
+            const bool cc = L.core[p] != 0;
+            sm_write_label(L, p, cc ? root_of(p) : 0u,
+                           (!cc && p < nf) ? sm_best_root(L, c, p, -1, root_of) : 0xFFFFFFFFu,
+                           mode, cl_out, fl_out);
+        }
     }
 
     SM_STAMP(6);
     // ---- counts and statistics ----
     {
         int tot = 0;
-        (void)sm_excl_scan(ncore_local, wsc, &tot);
+        (void)sm_excl_scan(ncore_local, L.wsc, &tot);
         int occ = 0;
-        (void)sm_excl_scan(occupied, wsc, &occ);
+        (void)sm_excl_scan(occupied, L.wsc, &occ);
         if (tid == 0) {
             if (nclusters) nclusters[part] = nclust;
             if (st) {
@@ -686,11 +759,335 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
                 st[kStBits] = 0;
             }
             if (gp) {
-                GridParams g{G.xmin2, G.ymin2, G.invx, G.invy, (uint32_t)nx, (uint32_t)ny, 1u, 1u,
-                             0};
+                GridParams g{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
+                             1u, 1u, 0};
                 *gp = g;
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// The same fit spread over G workgroups of one launch (spread_fit_kernel): a partition of a
+// few thousand points keeps one CU busy for hundreds of microseconds in small_fit_kernel (the
+// count and union walks are chains of dependent LDS reads, eight points per thread), while a
+// launch chain of the tiled pipeline costs ~45 kernel boundaries.  Here every workgroup stages
+// the WHOLE partition in its LDS (the same stage as small_fit_kernel, in its own slot order),
+// owns the slots of a contiguous cell range holding ~1/G of the points, and
+//   count   counts its own points; core flags by input index to global memory
+//   -- grid barrier 1 --
+//   union   reads every core flag; walks its own cores' stencils (the union rule above) into a
+//           union-find over its staged slots; publishes every non-root core of that forest as
+//           (input index, its root's input index)
+//   -- grid barrier 2 --
+//   merge   unites every workgroup's published pairs in a union-find over input indices: the
+//           union of all forests, so each root is the smallest input index of its cluster's
+//           cores, s(K), in every workgroup alike; numbering as small_fit_kernel
+//   label   its own points (and the non-finite points, last workgroup) in input order
+// Every edge of the closed form is found by the workgroup owning the smaller cell (cells are
+// ordered alike in every stage; a cell's quarters, and so its chains, have one owner), so the
+// merged forest has the components small_fit_kernel finds, and the results are the same bit
+// for bit.  Two grid barriers (every workgroup resident: the host caps the grid far below one
+// workgroup per CU); the arrival counter is reset by the last workgroup to leave.
+// ---------------------------------------------------------------------------------------
+#ifndef DBSCAN_AB_SPREAD_MAXWG
+#define DBSCAN_AB_SPREAD_MAXWG 32
+#endif
+constexpr int kSpreadMaxWG = DBSCAN_AB_SPREAD_MAXWG;
+#ifndef DBSCAN_AB_SPREAD_PARTS
+#define DBSCAN_AB_SPREAD_PARTS 1
+#endif
+constexpr int kSpreadParts = DBSCAN_AB_SPREAD_PARTS;  // work items per stencil row (walks)
+static_assert(kSpreadMaxWG <= 64 && 2 * 64 + 1 <= kSmN / 32, "merge tables in SmLds::wrank");
+
+struct SpreadArgs {
+    uint8_t* core;     // [n] core flags by input index (count -> union)
+    uint32_t* pairs;   // [G][n] published (input index << 16 | root input index)
+    int32_t* npairs;   // [G]
+    uint32_t* bar;     // [2] arrivals, departures (zero between launches)
+};
+
+__device__ __forceinline__ uint32_t sp_load(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid-wide barrier: every wave drains its stores, the workgroup meets, one lane releases
+// (agent fence, then its own drain) and adds its arrival, polls the count relaxed with a sleep
+// until `target` arrivals, and acquires (agent fence: this CU's stale lines dropped) before the
+// workgroup meets again and reads what the others published.  The poll gives up after ~2^21
+// rounds (seconds) and flags st[kStError] = 2: the fit then fails loudly instead of hanging.
+__device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t spins = 0; sp_load(bar) < target;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 21)) {
+                __hip_atomic_store(st + kStError, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// Union-find over input indices (merge phase): the larger root hooked under the smaller.
+__device__ __forceinline__ void sm_unite_v(int* par, int a, int b) {
+    while (true) {
+        a = sm_find(par, a);
+        b = sm_find(par, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(par + a, a, b) == a) return;
+    }
+}
+
+__global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, int m, double eps, double eps2,
+    int min_points, int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
+    GridParams* __restrict__ gp, int32_t* st, SpreadArgs sa) {
+    __shared__ SmLds L;
+    const int tid = threadIdx.x;
+    const int g = blockIdx.x, G = gridDim.x;
+    SM_STAMP(0);
+    if (g == 0 && tid < kStCount) st[tid] = 0;  // (the fit state: no memset ahead of the launch)
+    int occupied = 0;
+    // (every workgroup computes the same grid: a grid that cannot be sized returns them all
+    // here, before any barrier)
+    if (!sm_stage(L, x, y, m, eps, eps2, occupied)) {
+        if (tid == 0 && g == 0) st[kStError] = 1;
+        return;
+    }
+    SM_STAMP(2);
+    const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny, ncells = L.G.ncells;
+    const SmCtx c = sm_ctx(L, x, y, eps2);
+    // the owned cells: a contiguous cell range holding ~1/G of the walks' work, estimated per
+    // cell as its points x its stencil's points (cell counts are alike in every stage); the
+    // prefix of the estimate before each cell in par (free until the union)
+    {
+        int w[kSmCellPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kSmCellPer; ++k) {
+            const int cc = tid * kSmCellPer + k;
+            w[k] = 0;
+            if (cc < ncells) {
+                const int npt = (int)L.cst[cc + 1] - (int)L.cst[cc];
+                if (npt > 0) {
+                    const int cy = cc / nx, cx = cc - cy * nx;
+                    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+                    int cand = 0;
+                    for (int r = max(cy - 1, 0); r <= min(cy + 1, ny - 1); ++r)
+                        cand += (int)L.cst[r * nx + x1 + 1] - (int)L.cst[r * nx + x0];
+                    w[k] = npt * cand;
+                }
+            }
+            sum += w[k];
+        }
+        int tot = 0;
+        int run = sm_excl_scan(sum, L.wsc, &tot);
+#pragma unroll
+        for (int k = 0; k < kSmCellPer; ++k) {
+            const int cc = tid * kSmCellPer + k;
+            if (cc < ncells) L.par[cc] = run;
+            run += w[k];
+        }
+        __syncthreads();
+        if (tid < 2) {
+            const int64_t want = (int64_t)(g + tid) * tot / G;
+            int lo = 0, hi = ncells;  // smallest cell k whose prefix is >= want (ncells: tot)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)L.par[mid] >= want) hi = mid; else lo = mid + 1;
+            }
+            L.band[tid] = g + tid == G ? nf : (int)L.cst[lo];
+            if (tid == 0) L.band[2] = 0;
+        }
+        __syncthreads();
+    }
+    const int s0 = L.band[0], s1 = L.band[1], nb = s1 - s0;
+    const bool split = 3 * nb <= kSmT;  // (labels: one thread per stencil row)
+
+    // ---- count (own slots): each stencil row in kSpreadParts shares, one work item each, the
+    // counts summed per point in par (free until the union): a dense cell's walk is no longer
+    // one thread's chain ----
+    constexpr int K3 = 3 * kSpreadParts;
+    for (int i = tid; i < nb; i += kSmT) L.par[i] = 0;
+    __syncthreads();
+    if (min_points > 0) {
+        for (int it = tid; it < nb * K3; it += kSmT) {
+            const int i = it / K3, rem = it - i * K3;
+            const int cnt = sm_count(L, c, s0 + i, min_points, rem / kSpreadParts,
+                                     rem % kSpreadParts, kSpreadParts);
+            if (cnt) atomicAdd(&L.par[i], cnt);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nb; i += kSmT)
+        sa.core[L.info[s0 + i] >> 16] = (min_points <= 0 || L.par[i] >= min_points) ? 1 : 0;
+    SM_STAMP(7);
+    sp_grid_sync(sa.bar, (uint32_t)G, st);
+    SM_STAMP(8);
+
+    // ---- union of the own cores' walks (union-find over this stage's slots) ----
+    for (int p = tid; p < m; p += kSmT) {
+        L.core[p] = p < nf ? sa.core[L.info[p] >> 16] : (min_points <= 0 ? 1 : 0);
+        L.par[p] = p;
+    }
+    __syncthreads();
+    const bool quarters = L.G.clique != 0;
+    const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
+    const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy;
+    for (int it = tid; it < nb * K3; it += kSmT) {
+        const int i = it / K3, rem = it - i * K3;
+        if (L.core[s0 + i])
+            sm_union_walk(L, c, s0 + i, rem / kSpreadParts, quarters, reach_kx, reach_ky,
+                          rem % kSpreadParts, kSpreadParts);
+    }
+    __syncthreads();
+    SM_STAMP(9);
+    // publish the forest: every core slot that is not a root, with its root (read-only walks)
+    uint32_t* mine = sa.pairs + (int64_t)g * m;
+    for (int p = tid; p < nf; p += kSmT) {
+        if (!L.core[p] || L.par[p] == p) continue;
+        int r = p;
+        for (int u = L.par[r]; u != r; u = L.par[r]) r = u;
+        const int k = atomicAdd(&L.band[2], 1);
+        mine[k] = (L.info[p] & 0xFFFF0000u) | (L.info[r] >> 16);
+    }
+    __syncthreads();
+    if (tid == 0) sa.npairs[g] = L.band[2];
+    SM_STAMP(10);
+    sp_grid_sync(sa.bar, 2u * (uint32_t)G, st);
+    SM_STAMP(11);
+
+    // ---- merge: every workgroup's pairs into a union-find over input indices ----
+    for (int v = tid; v < m; v += kSmT) L.par[v] = v;
+    if (tid < G) L.wrank[tid] = (int)sp_load(reinterpret_cast<uint32_t*>(sa.npairs + tid));
+    __syncthreads();
+    if (tid == 0) {  // list starts (wrank[64 + h]) and the total (wrank[128])
+        int acc = 0;
+        for (int h = 0; h < G; ++h) {
+            L.wrank[64 + h] = acc;
+            acc += L.wrank[h];
+        }
+        L.wrank[128] = acc;
+    }
+    __syncthreads();
+    {
+        // eight pairs per thread and round, their loads in flight together
+        constexpr int kMergeBatch = 8;
+        const int total = L.wrank[128];
+        for (int k0 = tid; k0 < total; k0 += kSmT * kMergeBatch) {
+            uint32_t w[kMergeBatch];
+#pragma unroll
+            for (int u = 0; u < kMergeBatch; ++u) {
+                const int k = k0 + u * kSmT;
+                w[u] = 0xFFFFFFFFu;
+                if (k < total) {
+                    int lo = 0;  // the list holding flat index k
+#pragma unroll
+                    for (int sh = 32; sh > 0; sh >>= 1)
+                        if (lo + sh < G && L.wrank[64 + lo + sh] <= k) lo += sh;
+                    w[u] = sa.pairs[(int64_t)lo * m + (k - L.wrank[64 + lo])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kMergeBatch; ++u)
+                if (w[u] != 0xFFFFFFFFu) sm_unite_v(L.par, (int)(w[u] >> 16), (int)(w[u] & 0xFFFFu));
+        }
+    }
+    __syncthreads();
+    SM_STAMP(12);
+    // roots: s(K) flagged by visit index, then every core's parent is its root
+    int myroot[kSmPer];
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k) {
+        const int p = tid + k * kSmT;
+        myroot[k] = -1;
+        if (p < m && L.core[p]) {
+            const int v = (int)(L.info[p] >> 16);
+            int r = v;
+            for (int u = L.par[r]; u != r; u = L.par[r]) r = u;
+            myroot[k] = r;
+            if (r == v) atomicOr(&L.rbits[v >> 5], 1u << (v & 31));
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmPer; ++k)
+        if (myroot[k] >= 0) L.par[L.info[tid + k * kSmT] >> 16] = myroot[k];
+    int nclust = 0;
+    {
+        const int v = tid < kSmN / 32 ? __popc(L.rbits[tid]) : 0;
+        const int r = sm_excl_scan(v, L.wsc, &nclust);
+        if (tid < kSmN / 32) L.wrank[tid] = r;
+    }
+    __syncthreads();
+    SM_STAMP(13);
+
+    // ---- labels of the own slots (+ the non-finite points: the last workgroup) ----
+    const auto root_of = [&](int q) { return (uint32_t)L.par[L.info[q] >> 16]; };
+    if (split) {
+        if (tid < nb) L.sbest[tid] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (tid < 3 * nb) {
+            const int i = tid / 3, p = s0 + i;
+            if (!L.core[p]) {
+                const uint32_t b = sm_best_root(L, c, p, tid - 3 * i, root_of);
+                if (b != 0xFFFFFFFFu) atomicMin(&L.sbest[i], b);
+            }
+        }
+        __syncthreads();
+        if (tid < nb) {
+            const int p = s0 + tid;
+            sm_write_label(L, p, L.core[p] ? root_of(p) : 0u, L.sbest[tid], mode, cluster, flag);
+        }
+    } else {
+        for (int p = s0 + tid; p < s1; p += kSmT) {
+            const bool cc = L.core[p] != 0;
+            sm_write_label(L, p, cc ? root_of(p) : 0u,
+                           cc ? 0xFFFFFFFFu : sm_best_root(L, c, p, -1, root_of), mode, cluster,
+                           flag);
+        }
+    }
+    if (g == G - 1)
+        for (int p = nf + tid; p < m; p += kSmT)
+            sm_write_label(L, p, L.core[p] ? root_of(p) : 0u, 0xFFFFFFFFu, mode, cluster, flag);
+
+    SM_STAMP(14);
+    // ---- statistics (workgroup 0) and the barrier reset (the last workgroup to leave) ----
+    if (g == 0) {
+        int ncore = 0;
+        for (int p = tid; p < m; p += kSmT) ncore += L.core[p];
+        int tot = 0, occ = 0;
+        (void)sm_excl_scan(ncore, L.wsc, &tot);
+        (void)sm_excl_scan(occupied, L.wsc, &occ);
+        if (tid == 0) {
+            st[kStNf] = nf;
+            st[kStCore] = tot;
+            st[kStClusters] = nclust;
+            st[kStCells] = nf > 0 ? occ : 0;
+            st[kStTiles] = 0;
+            st[kStBits] = 0;
+            GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
+                          1u, 1u, 0};
+            *gp = gg;
+        }
+    }
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(sa.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (uint32_t)G - 1) {
+        __hip_atomic_store(sa.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sa.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -719,6 +1116,34 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
     klaunch(prof, "small_fit", small_fit_kernel, dim3(grid), dim3(kSmT), 0, s, x, y, d_offs,
             d_list, single_n, eps, eps * eps, (int)min_points, (int)mode, cluster, flag,
             d_nclusters, gp, st);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+#ifndef DBSCAN_AB_SPREAD_PER
+#define DBSCAN_AB_SPREAD_PER 256
+#endif
+// Workgroups of a spread fit: one per kSpreadPer points (at most kSpreadMaxWG)
+constexpr int kSpreadPer = DBSCAN_AB_SPREAD_PER;
+constexpr size_t kSpreadHead = 512;  // bar[2] at 0, npairs[kSpreadMaxWG] at 64
+
+void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
+                        const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
+                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st) {
+    const size_t bytes = kSpreadHead + kSmN + (size_t)kSpreadMaxWG * kSmN * sizeof(uint32_t);
+    if (ws.spread.bytes < bytes || !ws.spread_ready) {
+        char* p = static_cast<char*>(ws.spread.ensure(bytes));
+        DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, kSpreadHead, s));  // the barrier words, once
+        ws.spread_ready = true;
+    }
+    char* base = static_cast<char*>(ws.spread.p);
+    SpreadArgs sa;
+    sa.bar = reinterpret_cast<uint32_t*>(base);
+    sa.npairs = reinterpret_cast<int32_t*>(base + 64);
+    sa.core = reinterpret_cast<uint8_t*>(base + kSpreadHead);
+    sa.pairs = reinterpret_cast<uint32_t*>(base + kSpreadHead + kSmN);
+    const int G = (int)std::min<int64_t>(kSpreadMaxWG, std::max<int64_t>(1, n / kSpreadPer));
+    klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
+            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, sa);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 

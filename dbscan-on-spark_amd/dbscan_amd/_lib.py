@@ -64,6 +64,7 @@ SIGNATURES = [
     ("dbscan_slab_label_finish_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
     ("dbscan_set_small_max", _i64, [_vp, _i64]),
+    ("dbscan_set_spread_min", _i64, [_vp, _i64]),
     ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_fit_batch_device_async", _i32,
      [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
@@ -160,6 +161,15 @@ class Handle:
         """Fits of <= max_points points run the one-workgroup kernel (small.hip); 0 sends every
         fit through the tiled pipeline.  Returns the previous value."""
         r = load().dbscan_set_small_max(self._h, int(max_points))
+        if r < 0:
+            check(int(r))
+        return int(r)
+
+    def set_spread_min(self, min_points: int) -> int:
+        """LDS fits of >= min_points points run spread over several workgroups (small.hip,
+        spread_fit_kernel); above DBSCAN_SMALL_MAX_POINTS every LDS fit keeps one workgroup.
+        Returns the previous value."""
+        r = load().dbscan_set_spread_min(self._h, int(min_points))
         if r < 0:
             check(int(r))
         return int(r)

@@ -189,16 +189,25 @@ int64_t dbscan_scala_range_count(double start, double end, double step, int32_t 
  * LocalDBSCANNaive(eps, minPoints).fit per spatial partition -- at most maxPointsPerPartition
  * points (EvenSplitPartitioner.scala:44-209) plus the eps halo (DBSCAN.scala:116-137).
  * Full fits of at most dbscan_set_small_max(h, ...) points (default
- * DBSCAN_SMALL_DEFAULT_POINTS, where the one-workgroup kernel stops beating the tiled pipeline
- * on a single call; ceiling DBSCAN_SMALL_MAX_POINTS) with a finite eps*eps in mode NAIVE or
- * ARCHERY run ONE kernel in
- * which one workgroup holds the whole partition in LDS (same results bit for bit as the tiled
- * pipeline; dbscan_fit / dbscan_fit_h / dbscan_fit_device / dbscan_fit_device_async all route
- * there).  dbscan_set_small_max returns the previous value (0 sends every fit through the tiled
- * pipeline). */
+ * DBSCAN_SMALL_DEFAULT_POINTS = the ceiling DBSCAN_SMALL_MAX_POINTS: the LDS fits beat the tiled
+ * pipeline on a single call at every size up to it) with a finite eps*eps in mode NAIVE or
+ * ARCHERY run ONE kernel in which a workgroup holds the whole partition in LDS (same results
+ * bit for bit as the tiled pipeline; dbscan_fit / dbscan_fit_h / dbscan_fit_device /
+ * dbscan_fit_device_async all route there).  dbscan_set_small_max returns the previous value (0
+ * sends every fit through the tiled pipeline). */
 #define DBSCAN_SMALL_MAX_POINTS 8192
-#define DBSCAN_SMALL_DEFAULT_POINTS 3072
+#define DBSCAN_SMALL_DEFAULT_POINTS 8192
 int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
+
+/* Of those LDS fits, the ones of at least dbscan_set_spread_min(h, ...) points (default
+ * DBSCAN_SPREAD_DEFAULT_POINTS) run spread over several workgroups of the one launch: each
+ * workgroup stages the whole partition, counts and walks the unions of ~256 of its points, and two
+ * grid-wide barriers exchange the core flags and the union forests (same results bit for bit).
+ * A value above DBSCAN_SMALL_MAX_POINTS keeps every LDS fit on one workgroup.  Returns the
+ * previous value.  (A spread fit whose workgroups cannot all be resident -- the GPU filled by
+ * other work for seconds -- fails with DBSCAN_EHIP instead of waiting forever.) */
+#define DBSCAN_SPREAD_DEFAULT_POINTS 512
+int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is
  * points [offsets[p], offsets[p+1]) of x, y (host array offsets, n_parts + 1 non-decreasing

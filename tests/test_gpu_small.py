@@ -4,9 +4,10 @@ partition) and batches of them, bit-exact against the CPU oracle.
 DBSCAN.scala:150-155 runs `new LocalDBSCANNaive(eps, minPoints).fit(points)` once per spatial
 partition (EvenSplitPartitioner.scala:44-209 + the eps halo of DBSCAN.scala:116-137), so the
 fits the seam sees hold hundreds to ~10^4 points.  Every case runs through the one-workgroup
-kernel (the default for <= 8192 points) and, where noted, through the tiled pipeline as well
-(dbscan_set_small_max(h, 0)), and both must equal the oracle (LocalDBSCANNaive.scala:37-118 /
-LocalDBSCANArchery.scala:36-112 restated, visit order = array order)."""
+kernel (small_fit_kernel), its multi-workgroup form (spread_fit_kernel: ~256 points per
+workgroup, two grid barriers; dbscan_set_spread_min) and, where noted, through the tiled pipeline
+as well (dbscan_set_small_max(h, 0)), and all must equal the oracle (LocalDBSCANNaive.scala:37-118
+/ LocalDBSCANArchery.scala:36-112 restated, visit order = array order)."""
 import numpy as np
 import pytest
 
@@ -40,15 +41,26 @@ def _eq(got, ref, what=""):
     assert bad.size == 0, f"{what}: {bad.size} mismatches, first {bad[:10]}"
 
 
+ONE_WG = 1 << 30  # dbscan_set_spread_min: every LDS fit on one workgroup
+
+
+def _lds_forms(handle):
+    """(name, spread_min) of the two LDS fit forms: one workgroup, spread from 0 points"""
+    return (("small", ONE_WG), ("spread", 0))
+
+
 def _both_paths(dm, handle, x, y, eps, mp, mode, ref):
-    """The one-workgroup fit and the tiled pipeline, each against ref."""
+    """The one-workgroup fit, the spread fit and the tiled pipeline, each against ref."""
     try:
-        for small in (8192, 0):
-            handle.set_small_max(small)
-            _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref,
-                f"{'small' if small else 'tiled'} path")
+        for name, spread in _lds_forms(handle):
+            handle.set_small_max(8192)
+            handle.set_spread_min(spread)
+            _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, f"{name} path")
+        handle.set_small_max(0)
+        _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, "tiled path")
     finally:
         handle.set_small_max(8192)
+        handle.set_spread_min(512)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -112,11 +124,16 @@ def test_fuzz_sizes(dm, handle, m):
         eps = float(rng.uniform(0.03, 0.4))
         mp = int(rng.integers(1, 15))
         sets.append((x, y, eps, mp))
-    for mode in (0, 1):
-        for x, y, eps, mp in sets:
-            ref = (O.fit_sequential(x, y, eps, mp, mode) if m <= 3000
-                   else O.fit_grid(x, y, eps, mp, mode))
-            _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, f"m={m}")
+    try:
+        for mode in (0, 1):
+            for x, y, eps, mp in sets:
+                ref = (O.fit_sequential(x, y, eps, mp, mode) if m <= 3000
+                       else O.fit_grid(x, y, eps, mp, mode))
+                for name, spread in _lds_forms(handle):
+                    handle.set_spread_min(spread)
+                    _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, f"{name} m={m}")
+    finally:
+        handle.set_spread_min(512)
     # one batch of equal-eps partitions
     x = np.concatenate([s[0] for s in sets])
     y = np.concatenate([s[1] for s in sets])
