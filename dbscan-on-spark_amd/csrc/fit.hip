@@ -1417,11 +1417,13 @@ __device__ __forceinline__ F32Cut f32_cut(const GridParams& g, double eps2) {
 // outside [lo, hi] on the same side, so D < 0 <=> a neighbour, exactly as F <= lo; |D| <= M
 // takes the exact fp64 predicate (a superset of the F band).
 constexpr float kCountBand = 0x1p-14f;
+typedef float pk2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float count_d(float2 me, float2 q, float ne2) {
-    const float dx = q.x - me.x, dy = q.y - me.y;
-    return __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, ne2));
+    // (dx, dy) as one packed subtraction of the record pair (written per coordinate, the
+    // compiler paired the candidates' x and y across records, six moves per batch of four)
+    const pk2f d = pk2f{q.x, q.y} - pk2f{me.x, me.y};
+    return __builtin_fmaf(d.x, d.x, __builtin_fmaf(d.y, d.y, ne2));
 }
-__device__ __forceinline__ uint32_t sign_of(float d) { return __float_as_uint(d) >> 31; }
 
 // LDS index -> global slot of a staged tile (largest extended cell k with off[k] <= q)
 __device__ __forceinline__ int stage_slot(const TileStage& st, int q) {
@@ -1588,17 +1590,21 @@ __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int
         const int nin = e - j;
         float2 qq[kScanBatch];
 #pragma unroll
-        for (int u = 0; u < kScanBatch; ++u) qq[u] = buf[min(j + u, e - 1)];  // tail masked below
+        // (stage buffers end in kScanBatch pad records: a tail batch reads past its range, the
+        // extra candidates masked below; clamped reads measured 0.309 -> 0.299 ms in count32)
+        for (int u = 0; u < kScanBatch; ++u) qq[u] = buf[j + u];
         // the signed form (count_d): hits from sign bits, one band test per batch (the F <= lo /
         // F <= hi compares per candidate measured 0.312 -> 0.307 ms in count32)
         const uint32_t valid = nin >= kScanBatch ? (1u << kScanBatch) - 1u : (1u << nin) - 1u;
         uint32_t hm = 0, am = 0;
         float d[kScanBatch];
 #pragma unroll
-        for (int u = 0; u < kScanBatch; ++u) {
-            d[u] = count_d(me, qq[u], cut.ne2);
-            hm |= sign_of(d[u]) << u;
-        }
+        for (int u = 0; u < kScanBatch; ++u) d[u] = count_d(me, qq[u], cut.ne2);
+        // hit bits by one funnel shift per candidate, last candidate first: (hm << 1) | sign
+        // (with the packed difference above: count32 0.298 -> 0.285 ms)
+#pragma unroll
+        for (int u = kScanBatch - 1; u >= 0; --u)
+            hm = __builtin_amdgcn_alignbit(hm, __float_as_uint(d[u]), 31);
         hm &= valid;
         const float mn = fminf(fminf(fabsf(d[0]), fabsf(d[1])), fminf(fabsf(d[2]), fabsf(d[3])));
         if (__builtin_expect(mn <= kCountBand, 0)) {  // band members: the exact predicate
@@ -1753,7 +1759,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
         return;
     }
     __shared__ TileStage st;
-    __shared__ float2 buf[CAP];
+    __shared__ float2 buf[CAP + kScanBatch];
     __shared__ int wcores[kBlock / 64];
     __shared__ int rowoff[9];
     __shared__ __attribute__((aligned(16))) uint32_t lsts[kMaxNbr * kBlock];
@@ -1799,6 +1805,18 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
             const int own = rowoff[8];
             AB_NOTE(11, own);
             for (int i = (int)threadIdx.x; i < own; i += kBlock) {
+#if DBSCAN_AB_OWNVEC
+                // row and cell by counting the boundaries at or below i / j: the reads of each
+                // count are independent (two rounds of LDS reads instead of six dependent ones)
+                int r = 0;
+#pragma unroll
+                for (int t = 1; t < 8; ++t) r += rowoff[t] <= i ? 1 : 0;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - rowoff[r]);
+                int ex = 0;
+#pragma unroll
+                for (int t = 1; t < 8; ++t) ex += st.off[base + t] <= j ? 1 : 0;
+#else
                 int r = 0;
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
@@ -1809,6 +1827,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
+#endif
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core = true;
                 if (min_points > 0) {
@@ -1904,7 +1923,7 @@ struct WaveSeg {  // one tile of a wave
     TileStage st;
     int rowoff[9];
     uint32_t lcore[SCAP / 32 + 1];
-    float2 buf[SCAP];
+    float2 buf[SCAP + kScanBatch];
 };
 
 template <int SCAP, int NSEG>
@@ -2015,6 +2034,16 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             const int own = T.rowoff[8];
             int tflags = 0;
             for (int i = sl; i < own; i += SEG) {
+#if DBSCAN_AB_OWNVEC
+                int r = 0;
+#pragma unroll
+                for (int t = 1; t < 8; ++t) r += T.rowoff[t] <= i ? 1 : 0;
+                const int base = (r + 1) * 10 + 1;
+                const int j = st.off[base] + (i - T.rowoff[r]);
+                int ex = 0;
+#pragma unroll
+                for (int t = 1; t < 8; ++t) ex += st.off[base + t] <= j ? 1 : 0;
+#else
                 int r = 0;
 #pragma unroll
                 for (int sh = 4; sh > 0; sh >>= 1)
@@ -2025,6 +2054,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
 #pragma unroll
                 for (int sh = 4; sh > 0; sh >>= 1)
                     if (ex + sh < 8 && st.off[base + ex + sh] <= j) ex += sh;
+#endif
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core = true;
                 if (min_points > 0) {
