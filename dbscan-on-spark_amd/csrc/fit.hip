@@ -1580,7 +1580,7 @@ __device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange
 // Candidates per batch: 4, the batch's tail clamped and masked once (round 2: against 8 with
 // a per-candidate select, count_wave + count_tiny 0.092 -> 0.087 ms at 10^7, 0.256 -> 0.236
 // on config 3's share; 8 in this form spilled at 80 VGPRs).
-constexpr int kScanBatch = 4;
+constexpr int kScanBatch = 4;  // (8: equal, 0.283 -> 0.286 ms, with spills at 80 VGPRs)
 template <bool REC, int STRIDE = kBlock, class ExactF>
 __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
                                              float2 me, F32Cut cut, int min_points, int& cnt,
@@ -1606,7 +1606,9 @@ __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int
         for (int u = kScanBatch - 1; u >= 0; --u)
             hm = __builtin_amdgcn_alignbit(hm, __float_as_uint(d[u]), 31);
         hm &= valid;
-        const float mn = fminf(fminf(fabsf(d[0]), fabsf(d[1])), fminf(fabsf(d[2]), fabsf(d[3])));
+        float mn = fabsf(d[0]);
+#pragma unroll
+        for (int u = 1; u < kScanBatch; ++u) mn = fminf(mn, fabsf(d[u]));
         if (__builtin_expect(mn <= kCountBand, 0)) {  // band members: the exact predicate
 #pragma unroll
             for (int u = 0; u < kScanBatch; ++u)
@@ -1805,18 +1807,6 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
             const int own = rowoff[8];
             AB_NOTE(11, own);
             for (int i = (int)threadIdx.x; i < own; i += kBlock) {
-#if DBSCAN_AB_OWNVEC
-                // row and cell by counting the boundaries at or below i / j: the reads of each
-                // count are independent (two rounds of LDS reads instead of six dependent ones)
-                int r = 0;
-#pragma unroll
-                for (int t = 1; t < 8; ++t) r += rowoff[t] <= i ? 1 : 0;
-                const int base = (r + 1) * 10 + 1;
-                const int j = st.off[base] + (i - rowoff[r]);
-                int ex = 0;
-#pragma unroll
-                for (int t = 1; t < 8; ++t) ex += st.off[base + t] <= j ? 1 : 0;
-#else
                 int r = 0;
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
@@ -1827,7 +1817,6 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
 #pragma unroll
                 for (int s = 4; s > 0; s >>= 1)
                     if (ex + s < 8 && st.off[base + ex + s] <= j) ex += s;
-#endif
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core = true;
                 if (min_points > 0) {
@@ -2034,16 +2023,6 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
             const int own = T.rowoff[8];
             int tflags = 0;
             for (int i = sl; i < own; i += SEG) {
-#if DBSCAN_AB_OWNVEC
-                int r = 0;
-#pragma unroll
-                for (int t = 1; t < 8; ++t) r += T.rowoff[t] <= i ? 1 : 0;
-                const int base = (r + 1) * 10 + 1;
-                const int j = st.off[base] + (i - T.rowoff[r]);
-                int ex = 0;
-#pragma unroll
-                for (int t = 1; t < 8; ++t) ex += st.off[base + t] <= j ? 1 : 0;
-#else
                 int r = 0;
 #pragma unroll
                 for (int sh = 4; sh > 0; sh >>= 1)
@@ -2054,7 +2033,6 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
 #pragma unroll
                 for (int sh = 4; sh > 0; sh >>= 1)
                     if (ex + sh < 8 && st.off[base + ex + sh] <= j) ex += sh;
-#endif
                 const int p = st.cb[base + ex] + (j - st.off[base + ex]);
                 bool is_core = true;
                 if (min_points > 0) {

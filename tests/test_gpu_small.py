@@ -245,3 +245,40 @@ def test_blob_partitions_batch(dm, handle):
         _eq((cl[a:b], fl[a:b], int(nk[p])), O.fit_grid(px[a:b], py[a:b], 2.55, 10, 0),
             f"partition {p} (m={b - a})")
     assert len(offs) - 1 > 100
+
+
+def test_spread_fits_from_concurrent_handles(dm):
+    """Four executor threads, a handle each, fitting partitions concurrently through the spread
+    form (each launch holds its workgroups at two grid barriers while the other handles' launches
+    share the GPU): every fit equals its oracle fit, no barrier times out."""
+    import threading
+
+    rng = np.random.default_rng(404)
+    sets = []
+    for m in (600, 1500, 3000, 5000, 8192, 2500, 7000, 4096):
+        x, y = _fuzz_set(rng, m)
+        sets.append((x, y, float(rng.uniform(0.05, 0.3)), int(rng.integers(2, 12))))
+    refs = [O.fit_grid(x, y, e, mp, 0) for x, y, e, mp in sets]
+    handles = [dm.Handle(0) for _ in range(4)]
+    errors = []
+
+    def worker(t):
+        try:
+            for rep in range(3):
+                for k in range(t, len(sets), 4):
+                    x, y, e, mp = sets[k]
+                    _eq(dm.fit_arrays(x, y, e, mp, 0, handle=handles[t]), refs[k],
+                        f"thread {t} set {k} rep {rep}")
+        except Exception as exc:  # (reported below, from the main thread)
+            errors.append(exc)
+
+    try:
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for hh in handles:
+            hh.close()
+    assert not errors, errors[0]
