@@ -189,6 +189,9 @@ struct dbscan_handle {
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
+    void* fpinned = nullptr;          // partition-sized dbscan_fit_h: pinned x|y and cluster|flag
+    size_t fpinned_bytes = 0;
+    dbscan::DevBuf hxy, hclfl;        // ... and their device twins (one copy each way)
     hipEvent_t ready = nullptr;       // marks the root count inside a prepare call
     std::mutex mu;                    // one fit at a time per handle
 };
@@ -206,6 +209,12 @@ void set_err(const std::string& s) { g_err = s; }
 void dbscan::set_last_error(const std::string& s) { set_err(s); }
 
 namespace {
+
+// dbscan_fit_h fits of at most this many points stage through one pinned block (21 B/point)
+#ifndef DBSCAN_AB_PINNED_FIT
+#define DBSCAN_AB_PINNED_FIT 0
+#endif
+constexpr int64_t kPinnedFitMax = DBSCAN_AB_PINNED_FIT;
 
 template <class F>
 int32_t guarded(dbscan_handle* h, F&& f) {
@@ -332,6 +341,7 @@ void dbscan_destroy(dbscan_handle* h) {
     if (h->bpinned) (void)hipHostFree(h->bpinned);
     if (h->bcopied) (void)hipEventDestroy(h->bcopied);
     if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->fpinned) (void)hipHostFree(h->fpinned);
     if (h->ready) (void)hipEventDestroy(h->ready);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -440,6 +450,41 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         if (n == 0) {
             if (n_clusters_out) *n_clusters_out = 0;
             h->stats = dbscan::FitStats();
+            return DBSCAN_OK;
+        }
+        if (n <= kPinnedFitMax) {
+            // partition-sized fits (the seam's call): x|y through one pinned block and ONE DMA,
+            // cluster|flag back the same way, one synchronization for the whole call
+            const size_t in_b = 16 * (size_t)n, out_b = 5 * (size_t)n;
+            if (h->fpinned_bytes < in_b + out_b) {
+                if (h->fpinned) (void)hipHostFree(h->fpinned);
+                h->fpinned = nullptr;
+                h->fpinned_bytes = 0;
+                const size_t cap = 21 * (size_t)std::max<int64_t>(kPinnedFitMax, n);
+                DBSCAN_HIP_CHECK(hipHostMalloc(&h->fpinned, cap, hipHostMallocDefault));
+                h->fpinned_bytes = cap;
+            }
+            char* pin = static_cast<char*>(h->fpinned);
+            memcpy(pin, x, 8 * (size_t)n);
+            memcpy(pin + 8 * (size_t)n, y, 8 * (size_t)n);
+            double* dxy = static_cast<double*>(h->hxy.ensure(in_b));
+            char* dout = static_cast<char*>(h->hclfl.ensure(out_b));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(dxy, pin, in_b, hipMemcpyHostToDevice, h->stream));
+            dbscan::FitArgs a{dxy, dxy + n, nullptr, n, eps, min_points, mode,
+                              reinterpret_cast<int32_t*>(dout),
+                              reinterpret_cast<uint8_t*>(dout + 4 * (size_t)n), nullptr, nullptr};
+            a.small_max = h->small_max;
+            a.spread_min = h->spread_min;
+            h->prepared = false;
+            dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
+            DBSCAN_HIP_CHECK(
+                hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
+            h->stats = dbscan::read_fit_stats(h->stream, h->ws);  // (synchronizes)
+            h->slab.nf = h->stats.nf;
+            memcpy(cluster_out, pin + in_b, 4 * (size_t)n);
+            memcpy(flag_out, pin + in_b + 4 * (size_t)n, (size_t)n);
+            h->prof.flush();
+            if (n_clusters_out) *n_clusters_out = (int32_t)h->stats.nclusters;
             return DBSCAN_OK;
         }
         double* dx = static_cast<double*>(h->hx.ensure(n * sizeof(double)));

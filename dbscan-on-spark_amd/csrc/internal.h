@@ -177,6 +177,8 @@ struct Workspace {
         spread;
     bool spread_ready = false;  // spread.p holds zeroed barrier words (small.hip)
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
+    double* stats_dev = nullptr;   // ... its device address (LDS fits write it directly)
+    bool fit_mirrored = false;     // the last fit wrote its stats into stats_host itself
     Workspace() = default;
     ~Workspace() {
         if (stats_host) (void)hipHostFree(stats_host);
@@ -201,6 +203,7 @@ struct Workspace {
         spread_ready = false;
         if (stats_host) (void)hipHostFree(stats_host);
         stats_host = nullptr;
+        stats_dev = nullptr;
     }
 };
 
@@ -404,13 +407,14 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
                         const int64_t* d_offs, const int32_t* d_list, int32_t nlist,
                         int64_t single_n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, int32_t* d_nclusters, GridParams* gp,
-                        int32_t* st);
+                        int32_t* st, double* mirror = nullptr);
 // One fit of n <= kSmallMaxPoints points spread over several workgroups of one launch
 // (small.hip, spread_fit_kernel): the same results as the one-workgroup fit; statistics into
 // st / gp (the handle's fit state), st[kStError] = 2 if a grid barrier gave up.
 void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
                         const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
-                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st);
+                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
+                        double* mirror = nullptr);
 // DBSCAN.scala:116-137 on the host: the points every partition's outer rectangle (main grown
 // by eps, inclusive) holds, in input order (partition.hip)
 int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,

@@ -402,17 +402,9 @@ __device__ __forceinline__ bool sm_pair(const SmLds& L, const SmCtx& c, int p, f
 // a time (their LDS reads in flight together: the walks are bound by the latency of dependent
 // LDS reads, not by their count).  only = 0..2: that row alone (row-split phases), -1: all three.
 constexpr int kSmBatch = 4;
-// part / nparts: only that share of each row's candidates (spread fits split long walks)
-__device__ __forceinline__ void sm_row_part(int& qs, int& e, int part, int nparts) {
-    if (nparts > 1 && e > qs) {
-        const int len = e - qs;
-        e = qs + len * (part + 1) / nparts;
-        qs = qs + len * part / nparts;
-    }
-}
 template <class F>
 __device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_, int p, int qmin,
-                                               F&& f, int only, int part = 0, int nparts = 1) {
+                                               F&& f, int only) {
     const int nx = cx_.nx, ny = cx_.ny;
     const int c = (int)(L.info[p] & kCellMask);
     const int cy = c / nx, cx = c - cy * nx;
@@ -423,14 +415,12 @@ __device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_,
         const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
         if (r < 0 || r >= ny) continue;
         const int rb = r * nx;
-        int e = L.cst[rb + x1 + 1];
+        const int e = L.cst[rb + x1 + 1];
         // boundaries of the row's second and third cell (q's column = x0 + crossings)
         const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
         const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
         const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
-        int qs = max((int)L.cst[rb + x0], qmin);
-        sm_row_part(qs, e, part, nparts);
-        for (int q = qs; q < e; q += kSmBatch) {
+        for (int q = max((int)L.cst[rb + x0], qmin); q < e; q += kSmBatch) {
             float2 rq[kSmBatch];
 #pragma unroll
             for (int u = 0; u < kSmBatch; ++u) rq[u] = L.rec[min(q + u, e - 1)];
@@ -446,13 +436,13 @@ __device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_,
 
 // |N(p)| capped at minPoints over stencil row `only` (-1: all rows; LocalDBSCANNaive.scala:52-56)
 __device__ __forceinline__ int sm_count(const SmLds& L, const SmCtx& c, int p, int min_points,
-                                        int only, int part = 0, int nparts = 1) {
+                                        int only) {
     const float2 me = L.rec[p];
     int cnt = 0;
     sm_for_stencil(L, c, p, 0, [&](int q, float2 rq, int) {
         cnt += sm_pair(L, c, p, me, q, rq) ? 1 : 0;
         return cnt < min_points;
-    }, only, part, nparts);
+    }, only);
     return cnt;
 }
 
@@ -464,8 +454,7 @@ __device__ __forceinline__ int sm_count(const SmLds& L, const SmCtx& c, int p, i
 // with some core of q's quarter.  So a dense cell costs a few unions per point instead of one
 // per neighbour.  reach_k: record -> cell-local coordinate offsets (clique grids).
 __device__ __forceinline__ void sm_union_walk(SmLds& L, const SmCtx& cx_, int p, int only,
-                                              bool quarters, double reach_kx, double reach_ky,
-                                              int part = 0, int nparts = 1) {
+                                              bool quarters, double reach_kx, double reach_ky) {
     const int nx = cx_.nx, ny = cx_.ny;
     const float2 me = L.rec[p];
     uint64_t done = 0;  // quarters of the 6x6 window around p's cell already joined
@@ -504,13 +493,11 @@ __device__ __forceinline__ void sm_union_walk(SmLds& L, const SmCtx& cx_, int p,
         const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
         if (r < 0 || r >= ny) continue;
         const int rb = r * nx;
-        int e = L.cst[rb + x1 + 1];
+        const int e = L.cst[rb + x1 + 1];
         const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
         const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
         const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
-        int qs = max((int)L.cst[rb + x0], p + 1);
-        sm_row_part(qs, e, part, nparts);
-        for (int q = qs; q < e; q += kSmBatch) {
+        for (int q = max((int)L.cst[rb + x0], p + 1); q < e; q += kSmBatch) {
             if (quarters) {
                 // every quarter of q's cell done: the rest of the cell needs no visit
                 const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
@@ -601,6 +588,19 @@ __device__ __forceinline__ void sm_write_label(const SmLds& L, int p, uint32_t r
     fl_out[v] = f;
 }
 
+// The fit statistics of an LDS fit: the handle's device state (st, gp) and, when given, the
+// same words in the handle's pinned host block (mirror: read back without a copy).
+__device__ __forceinline__ void sm_zero_stats(int32_t* st, double* mirror, int tid) {
+    if (tid < kStCount) {
+        if (st) st[tid] = 0;
+        if (mirror) reinterpret_cast<int32_t*>(mirror + kMiscState)[tid] = 0;
+    }
+}
+__device__ __forceinline__ void sm_set_stat(int32_t* st, double* mirror, int k, int32_t v) {
+    if (st) st[k] = v;
+    if (mirror) reinterpret_cast<int32_t*>(mirror + kMiscState)[k] = v;
+}
+
 // One partition per workgroup.  offs == nullptr: one partition [0, single_n) (blockIdx 0);
 // else partition list[blockIdx.x] = points [offs[p], offs[p+1]).  nclusters[p] (or st) gets its
 // cluster count.  st/gp (single fits only): the handle's fit statistics.
@@ -608,7 +608,8 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     const double* __restrict__ x, const double* __restrict__ y, const int64_t* __restrict__ offs,
     const int32_t* __restrict__ list, int64_t single_n, double eps, double eps2, int min_points,
     int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
-    int32_t* __restrict__ nclusters, GridParams* __restrict__ gp, int32_t* __restrict__ st) {
+    int32_t* __restrict__ nclusters, GridParams* __restrict__ gp, int32_t* __restrict__ st,
+    double* __restrict__ mirror) {
     __shared__ SmLds L;
 
     const int tid = threadIdx.x;
@@ -623,10 +624,10 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     const double* px = x + off;
     const double* py = y + off;
     SM_STAMP(0);
-    if (st && tid < kStCount) st[tid] = 0;  // (the fit state: no memset ahead of the launch)
+    sm_zero_stats(st, mirror, tid);  // (the fit state: no memset ahead of the launch)
     int occupied = 0;
     if (!sm_stage(L, px, py, m, eps, eps2, occupied)) {
-        if (tid == 0 && st) st[kStError] = 1;
+        if (tid == 0) sm_set_stat(st, mirror, kStError, 1);
         return;
     }
     SM_STAMP(2);
@@ -750,19 +751,14 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
         (void)sm_excl_scan(occupied, L.wsc, &occ);
         if (tid == 0) {
             if (nclusters) nclusters[part] = nclust;
-            if (st) {
-                st[kStNf] = nf;
-                st[kStCore] = tot;
-                st[kStClusters] = nclust;
-                st[kStCells] = nf > 0 ? occ : 0;
-                st[kStTiles] = 0;
-                st[kStBits] = 0;
-            }
-            if (gp) {
-                GridParams g{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
-                             1u, 1u, 0};
-                *gp = g;
-            }
+            sm_set_stat(st, mirror, kStNf, nf);
+            sm_set_stat(st, mirror, kStCore, tot);
+            sm_set_stat(st, mirror, kStClusters, nclust);
+            sm_set_stat(st, mirror, kStCells, nf > 0 ? occ : 0);
+            GridParams g{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
+                         1u, 1u, 0};
+            if (gp) *gp = g;
+            if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = g;
         }
     }
 }
@@ -790,14 +786,8 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
 // for bit.  Two grid barriers (every workgroup resident: the host caps the grid far below one
 // workgroup per CU); the arrival counter is reset by the last workgroup to leave.
 // ---------------------------------------------------------------------------------------
-#ifndef DBSCAN_AB_SPREAD_MAXWG
-#define DBSCAN_AB_SPREAD_MAXWG 32
-#endif
-constexpr int kSpreadMaxWG = DBSCAN_AB_SPREAD_MAXWG;
-#ifndef DBSCAN_AB_SPREAD_PARTS
-#define DBSCAN_AB_SPREAD_PARTS 1
-#endif
-constexpr int kSpreadParts = DBSCAN_AB_SPREAD_PARTS;  // work items per stencil row (walks)
+constexpr int kSpreadMaxWG = 32;  // (64 measured no faster: the workgroups' chains do not shorten)
+
 static_assert(kSpreadMaxWG <= 64 && 2 * 64 + 1 <= kSmN / 32, "merge tables in SmLds::wrank");
 
 struct SpreadArgs {
@@ -816,7 +806,7 @@ __device__ __forceinline__ uint32_t sp_load(uint32_t* p) {
 // until `target` arrivals, and acquires (agent fence: this CU's stale lines dropped) before the
 // workgroup meets again and reads what the others published.  The poll gives up after ~2^21
 // rounds (seconds) and flags st[kStError] = 2: the fit then fails loudly instead of hanging.
-__device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st) {
+__device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st, double* mirror) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -827,6 +817,9 @@ __device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1u << 21)) {
                 __hip_atomic_store(st + kStError, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (mirror)
+                    __hip_atomic_store(reinterpret_cast<int32_t*>(mirror + kMiscState) + kStError,
+                                       2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
         }
@@ -851,20 +844,137 @@ __device__ __forceinline__ void sm_unite_v(int* par, int a, int b) {
     }
 }
 
+// The wave-cooperative walks of the spread form: p is the same in every lane of the wave.
+// |N(p)| capped at minPoints: 64 candidates of a stencil row per step, hits by ballot.
+__device__ __forceinline__ int sp_count_wave(const SmLds& L, const SmCtx& c, int p,
+                                             int min_points) {
+    const int lane = (int)(threadIdx.x & 63);
+    const float2 me = L.rec[p];
+    const int cc = (int)(L.info[p] & kCellMask);
+    const int cy = cc / c.nx, cx = cc - cy * c.nx;
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, c.nx - 1);
+    int cnt = 0;
+    for (int d = 0; d < 3 && cnt < min_points; ++d) {
+        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+        if (r < 0 || r >= c.ny) continue;
+        const int e = L.cst[r * c.nx + x1 + 1];
+        for (int q0 = L.cst[r * c.nx + x0]; q0 < e && cnt < min_points; q0 += 64) {
+            const int q = q0 + lane;
+            const bool hit = q < e && sm_pair(L, c, p, me, q, L.rec[q]);
+            cnt += __popcll(__ballot(hit));
+        }
+    }
+    return cnt;
+}
+
+// Core p's unions (the rule of sm_union_walk): 64 candidates q > p of a stencil row per step;
+// among the step's hits (cores within eps, not already under p's root), the first of each
+// quarter not yet joined unites with p -- one lane unites, in lane order, so the first core of
+// a quarter is the one joined, as in the serial walk.
+__device__ __forceinline__ void sp_union_wave(SmLds& L, const SmCtx& cx_, int p, bool quarters,
+                                              double reach_kx, double reach_ky) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int nx = cx_.nx, ny = cx_.ny;
+    const float2 me = L.rec[p];
+    uint64_t done = 0;
+    int rp = 0;
+    if (lane == 0) rp = sm_find(L.par, p);  // (one lane: the find compresses the path)
+    rp = __shfl(rp, 0);
+    const int c = (int)(L.info[p] & kCellMask);
+    const int cy = c / nx, cx = c - cy * nx;
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+    if (quarters && !cx_.exact_only) {  // quarters wholly beyond eps (sm_union_walk)
+        const float tx = (float)((double)me.x + reach_kx - (double)cx);
+        const float ty = (float)((double)me.y + reach_ky - (double)cy);
+        const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
+        const float rr = (sqrtf(cx_.hi) + mg) * (sqrtf(cx_.hi) + mg);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const float y0 = 0.5f * (float)a - 1.0f,
+                        dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
+#pragma unroll
+            for (int b = 0; b < 6; ++b) {
+                const float xb = 0.5f * (float)b - 1.0f;
+                const float dx = fmaxf(0.0f, fmaxf(xb - tx, tx - (xb + 0.5f)));
+                if (dx * dx + dy * dy > rr) done |= 1ull << (a * 6 + b);
+            }
+        }
+    }
+    for (int d = 0; d < 3; ++d) {
+        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+        if (r < 0 || r >= ny) continue;
+        const int rb = r * nx;
+        const int e = L.cst[rb + x1 + 1];
+        const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
+        const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
+        const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
+        for (int q0 = max((int)L.cst[rb + x0], p + 1); q0 < e; q0 += 64) {
+            const int q = q0 + lane;
+            int bit = 0;
+            bool cand = q < e && L.core[q] != 0;
+            if (cand && quarters) {
+                const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
+                const int qd = (int)((L.info[q] >> 13) & 3u);
+                bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
+                cand = ((done >> bit) & 1ull) == 0;
+            }
+            if (cand) cand = sm_ld(L.par + q) != rp && sm_pair(L, cx_, p, me, q, L.rec[q]);
+            uint64_t hits = __ballot(cand);
+            while (hits) {
+                const int l = __ffsll((long long)hits) - 1;
+                int nr = 0;
+                if (lane == 0) nr = sm_unite_from(L.par, L.info, rp, q0 + l);
+                rp = __shfl(nr, 0);
+                if (quarters) {
+                    const int bl = __shfl(bit, l);
+                    done |= 1ull << bl;
+                    hits &= ~__ballot(cand && bit == bl);
+                } else {
+                    hits &= hits - 1;
+                }
+            }
+        }
+    }
+}
+
+// The smallest root visit index among non-core p's core neighbours (sm_best_root), 64
+// candidates per step, the minimum taken across the wave.
+__device__ __forceinline__ uint32_t sp_best_root_wave(const SmLds& L, const SmCtx& c, int p) {
+    const int lane = (int)(threadIdx.x & 63);
+    const float2 me = L.rec[p];
+    const int cc = (int)(L.info[p] & kCellMask);
+    const int cy = cc / c.nx, cx = cc - cy * c.nx;
+    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, c.nx - 1);
+    uint32_t best = 0xFFFFFFFFu;
+    for (int d = 0; d < 3; ++d) {
+        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+        if (r < 0 || r >= c.ny) continue;
+        const int e = L.cst[r * c.nx + x1 + 1];
+        for (int q = L.cst[r * c.nx + x0] + lane; q < e; q += 64) {
+            if (!L.core[q]) continue;
+            const uint32_t s = (uint32_t)L.par[L.info[q] >> 16];
+            if (s < best && sm_pair(L, c, p, me, q, L.rec[q])) best = s;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    return best;
+}
+
 __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     const double* __restrict__ x, const double* __restrict__ y, int m, double eps, double eps2,
     int min_points, int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
-    GridParams* __restrict__ gp, int32_t* st, SpreadArgs sa) {
+    GridParams* __restrict__ gp, int32_t* st, double* mirror, SpreadArgs sa) {
     __shared__ SmLds L;
     const int tid = threadIdx.x;
     const int g = blockIdx.x, G = gridDim.x;
     SM_STAMP(0);
-    if (g == 0 && tid < kStCount) st[tid] = 0;  // (the fit state: no memset ahead of the launch)
+    if (g == 0) sm_zero_stats(st, mirror, tid);  // (the fit state: no memset ahead of launch)
     int occupied = 0;
     // (every workgroup computes the same grid: a grid that cannot be sized returns them all
     // here, before any barrier)
     if (!sm_stage(L, x, y, m, eps, eps2, occupied)) {
-        if (tid == 0 && g == 0) st[kStError] = 1;
+        if (tid == 0 && g == 0) sm_set_stat(st, mirror, kStError, 1);
         return;
     }
     SM_STAMP(2);
@@ -916,25 +1026,34 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     const int s0 = L.band[0], s1 = L.band[1], nb = s1 - s0;
     const bool split = 3 * nb <= kSmT;  // (labels: one thread per stencil row)
 
-    // ---- count (own slots): each stencil row in kSpreadParts shares, one work item each, the
-    // counts summed per point in par (free until the union): a dense cell's walk is no longer
-    // one thread's chain ----
-    constexpr int K3 = 3 * kSpreadParts;
+    // ---- count (own slots) ----
+#if DBSCAN_AB_SPREAD_WAVE
+    // one wave per own point, its 64 lanes over 64 candidates of a stencil row at a time, the
+    // hits counted by a ballot (no lane runs a walk of its own)
+    {
+        const int wv = tid >> 6;
+        for (int p = s0 + wv; p < s1; p += kSmW) {
+            const bool cc = min_points <= 0 || sp_count_wave(L, c, p, min_points) >= min_points;
+            if ((tid & 63) == 0) sa.core[L.info[p] >> 16] = cc ? 1 : 0;
+        }
+    }
+#else
+    // each stencil row one work item, the counts summed per point in par (free until the union)
     for (int i = tid; i < nb; i += kSmT) L.par[i] = 0;
     __syncthreads();
     if (min_points > 0) {
-        for (int it = tid; it < nb * K3; it += kSmT) {
-            const int i = it / K3, rem = it - i * K3;
-            const int cnt = sm_count(L, c, s0 + i, min_points, rem / kSpreadParts,
-                                     rem % kSpreadParts, kSpreadParts);
+        for (int it = tid; it < nb * 3; it += kSmT) {
+            const int i = it / 3;
+            const int cnt = sm_count(L, c, s0 + i, min_points, it - 3 * i);
             if (cnt) atomicAdd(&L.par[i], cnt);
         }
     }
     __syncthreads();
     for (int i = tid; i < nb; i += kSmT)
         sa.core[L.info[s0 + i] >> 16] = (min_points <= 0 || L.par[i] >= min_points) ? 1 : 0;
+#endif
     SM_STAMP(7);
-    sp_grid_sync(sa.bar, (uint32_t)G, st);
+    sp_grid_sync(sa.bar, (uint32_t)G, st, mirror);
     SM_STAMP(8);
 
     // ---- union of the own cores' walks (union-find over this stage's slots) ----
@@ -946,12 +1065,16 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     const bool quarters = L.G.clique != 0;
     const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
     const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy;
-    for (int it = tid; it < nb * K3; it += kSmT) {
-        const int i = it / K3, rem = it - i * K3;
+#if DBSCAN_AB_SPREAD_WAVE
+    for (int p = s0 + (tid >> 6); p < s1; p += kSmW)
+        if (L.core[p]) sp_union_wave(L, c, p, quarters, reach_kx, reach_ky);
+#else
+    for (int it = tid; it < nb * 3; it += kSmT) {
+        const int i = it / 3;
         if (L.core[s0 + i])
-            sm_union_walk(L, c, s0 + i, rem / kSpreadParts, quarters, reach_kx, reach_ky,
-                          rem % kSpreadParts, kSpreadParts);
+            sm_union_walk(L, c, s0 + i, it - 3 * i, quarters, reach_kx, reach_ky);
     }
+#endif
     __syncthreads();
     SM_STAMP(9);
     // publish the forest: every core slot that is not a root, with its root (read-only walks)
@@ -966,7 +1089,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     __syncthreads();
     if (tid == 0) sa.npairs[g] = L.band[2];
     SM_STAMP(10);
-    sp_grid_sync(sa.bar, 2u * (uint32_t)G, st);
+    sp_grid_sync(sa.bar, 2u * (uint32_t)G, st, mirror);
     SM_STAMP(11);
 
     // ---- merge: every workgroup's pairs into a union-find over input indices ----
@@ -1036,6 +1159,15 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 
     // ---- labels of the own slots (+ the non-finite points: the last workgroup) ----
     const auto root_of = [&](int q) { return (uint32_t)L.par[L.info[q] >> 16]; };
+#if DBSCAN_AB_SPREAD_WAVE
+    for (int p = s0 + tid; p < s1; p += kSmT)  // cores: one thread each
+        if (L.core[p]) sm_write_label(L, p, root_of(p), 0xFFFFFFFFu, mode, cluster, flag);
+    for (int p = s0 + (tid >> 6); p < s1; p += kSmW) {  // non-cores: a wave each
+        if (L.core[p]) continue;
+        const uint32_t b = sp_best_root_wave(L, c, p);
+        if ((tid & 63) == 0) sm_write_label(L, p, 0u, b, mode, cluster, flag);
+    }
+#else
     if (split) {
         if (tid < nb) L.sbest[tid] = 0xFFFFFFFFu;
         __syncthreads();
@@ -1059,6 +1191,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
                            flag);
         }
     }
+#endif
     if (g == G - 1)
         for (int p = nf + tid; p < m; p += kSmT)
             sm_write_label(L, p, L.core[p] ? root_of(p) : 0u, 0xFFFFFFFFu, mode, cluster, flag);
@@ -1072,15 +1205,14 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
         (void)sm_excl_scan(ncore, L.wsc, &tot);
         (void)sm_excl_scan(occupied, L.wsc, &occ);
         if (tid == 0) {
-            st[kStNf] = nf;
-            st[kStCore] = tot;
-            st[kStClusters] = nclust;
-            st[kStCells] = nf > 0 ? occ : 0;
-            st[kStTiles] = 0;
-            st[kStBits] = 0;
+            sm_set_stat(st, mirror, kStNf, nf);
+            sm_set_stat(st, mirror, kStCore, tot);
+            sm_set_stat(st, mirror, kStClusters, nclust);
+            sm_set_stat(st, mirror, kStCells, nf > 0 ? occ : 0);
             GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
                           1u, 1u, 0};
             *gp = gg;
+            if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
         }
     }
     if (tid == 0 &&
@@ -1110,12 +1242,12 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
                         const int64_t* d_offs, const int32_t* d_list, int32_t nlist,
                         int64_t single_n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, int32_t* d_nclusters, GridParams* gp,
-                        int32_t* st) {
+                        int32_t* st, double* mirror) {
     const unsigned grid = d_offs ? (unsigned)nlist : 1u;
     if (grid == 0) return;
     klaunch(prof, "small_fit", small_fit_kernel, dim3(grid), dim3(kSmT), 0, s, x, y, d_offs,
             d_list, single_n, eps, eps * eps, (int)min_points, (int)mode, cluster, flag,
-            d_nclusters, gp, st);
+            d_nclusters, gp, st, mirror);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
@@ -1128,7 +1260,8 @@ constexpr size_t kSpreadHead = 512;  // bar[2] at 0, npairs[kSpreadMaxWG] at 64
 
 void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
                         const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
-                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st) {
+                        int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
+                        double* mirror) {
     const size_t bytes = kSpreadHead + kSmN + (size_t)kSpreadMaxWG * kSmN * sizeof(uint32_t);
     if (ws.spread.bytes < bytes || !ws.spread_ready) {
         char* p = static_cast<char*>(ws.spread.ensure(bytes));
@@ -1143,7 +1276,7 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     sa.pairs = reinterpret_cast<uint32_t*>(base + kSpreadHead + kSmN);
     const int G = (int)std::min<int64_t>(kSpreadMaxWG, std::max<int64_t>(1, n / kSpreadPer));
     klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
-            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, sa);
+            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, sa);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
