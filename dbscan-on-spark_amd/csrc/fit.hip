@@ -1185,9 +1185,6 @@ struct UnionLds {  // aliases the count's neighbour-list staging (the two never 
     unsigned long long cmin[kMaxTileQ];  // per component: min (visit index << 32 | rep)
 };
 static_assert(sizeof(UnionLds) <= kMaxNbr * kBlock * sizeof(uint16_t), "UnionLds must fit");
-// count_tile32: deferred quarter pairs behind the union records in the record staging
-constexpr int kPairListCap =
-    (int)((kMaxNbr * kBlock * sizeof(uint32_t) - sizeof(UnionLds)) / sizeof(uint32_t));
 
 // Quarter-grid offsets to test from each quarter: one of each opposite pair (dy < 0, or dy == 0
 // and dx < 0), so every unordered quarter pair within the 5x5 stencil is one item -- the 4
@@ -1531,34 +1528,6 @@ __device__ __forceinline__ bool quarters_touch32(const float2* __restrict__ buf,
     return false;
 }
 
-#if DBSCAN_AB_COOP_TOUCH
-// quarters_touch32 by a whole wave (wave-uniform arguments): lanes 0-31 and 32-63 each hold A's
-// point (lane & 31) against one half of B's points, one B point per round (<= 16 rounds), a hit
-// in any lane ends the test.  Quarters over 32 points: the serial test, run alike by every lane.
-template <class CoreF, class ExactF>
-__device__ __forceinline__ bool quarters_touch32_wave(const float2* __restrict__ buf, int ab,
-                                                      int ae, uint32_t am, int bb, int be,
-                                                      uint32_t bm, CoreF is_core, F32Cut cut,
-                                                      ExactF exact) {
-    if (ae - ab <= 32 && be - bb <= 32) {
-        const int lane = __lane_id(), a = lane & 31, half = lane >> 5;
-        const bool va = a < ae - ab && ((am >> a) & 1u);
-        const float2 pa = buf[ab + (va ? a : 0)];
-        const int nb = be - bb, nr = (nb + 1) >> 1;
-        for (int r = 0; r < nr; ++r) {
-            const int b = half * nr + r;
-            bool hit = false;
-            if (va && b < nb && ((bm >> b) & 1u)) {
-                const float F = f32_d2(pa, buf[bb + b]);
-                hit = F <= cut.lo || (F <= cut.hi && exact(ab + a, bb + b));
-            }
-            if (__any(hit)) return true;
-        }
-        return false;
-    }
-    return quarters_touch32(buf, ab, ae, am, bb, be, bm, is_core, cut, exact);
-}
-#endif
 
 // The 4 adjacent (backward) quarter pairs of core quarter qi, from qi's own lane: the four
 // lookups, and the tests of each pair's first cores, are issued together; a pair whose first
@@ -1568,9 +1537,7 @@ template <class CoreF, class ExactF>
 __device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange,
                                                  const uint32_t* lmask, const uint16_t* qmap,
                                                  int qi, const float2* __restrict__ buf,
-                                                 CoreF is_core, F32Cut cut, ExactF exact,
-                                                 uint32_t* plist = nullptr, int* pcount = nullptr,
-                                                 int pcap = 0) {
+                                                 CoreF is_core, F32Cut cut, ExactF exact) {
     constexpr int kDx[4] = {-1, 0, 1, -1}, kDy[4] = {-1, -1, -1, 0};
     const uint32_t ri = lrange[qi], am = lmask[qi];
     const int lq = (int)((ri >> 22) & 255u);
@@ -1598,13 +1565,6 @@ __device__ __forceinline__ void unite_adjacent32(int* lp, const uint32_t* lrange
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
         if ((rj[o] >> 31) && !t[o]) {
-            if (plist) {  // deferred to a wave-cooperative test (fused_tile_union32)
-                const int k = atomicAdd(pcount, 1);
-                if (k < pcap) {
-                    plist[k] = (uint32_t)qi | ((uint32_t)jn[o] << 16);
-                    continue;
-                }
-            }
             const int bb = (int)(rj[o] & 2047u), be = bb + (int)((rj[o] >> 11) & 2047u);
             t[o] = quarters_touch32(buf, ab, ae, am, bb, be, mj[o], is_core, cut, exact);
         }
@@ -1688,35 +1648,9 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
     };
     __shared__ int s_first;  // smallest local quarter holding a core
     __shared__ int s_tflags;  // the tile's edge strips holding cores (FuseArgs::tcore)
-#if DBSCAN_AB_COOP_TOUCH
-    // quarter pairs whose first cores do not decide, tested by whole waves: a list behind the
-    // union records in the same LDS
-    __shared__ int s_npairs;
-    uint32_t* plist = reinterpret_cast<uint32_t*>(&u + 1);
-    const int pcap = kPairListCap;
-    const int lane = i & 63, wv = i >> 6;
-    const auto run_list = [&]() {
-        const int np = min(s_npairs, pcap);
-        for (int k = wv; k < np; k += kBlock / 64) {
-            const uint32_t pr = plist[k];
-            const int qa = (int)(pr & 0xFFFFu), qc = (int)(pr >> 16);
-            if (lfind(u.lp, qa) == lfind(u.lp, qc)) continue;
-            const uint32_t ra = u.lrange[qa], rc = u.lrange[qc];
-            const int ab = (int)(ra & 2047u), ae = ab + (int)((ra >> 11) & 2047u);
-            const int cb = (int)(rc & 2047u), ce = cb + (int)((rc >> 11) & 2047u);
-            if (quarters_touch32_wave(buf, ab, ae, u.lmask[qa], cb, ce, u.lmask[qc], is_core, cut,
-                                      exact) &&
-                lane == 0)
-                lunite(u.lp, qa, qc);
-        }
-    };
-#endif
     if (i == 0) {
         s_first = 0x7FFFFFFF;
         s_tflags = 0;
-#if DBSCAN_AB_COOP_TOUCH
-        s_npairs = 0;
-#endif
     }
     u.qmap[i] = 0xFFFF;
     u.cmin[i] = ~0ull;
@@ -1768,19 +1702,9 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
     AB_STAMP(5);
     {
         // adjacent quarters (the 4 backward offsets) from each core quarter's own thread
-#if DBSCAN_AB_COOP_TOUCH
-        if (i < nq && rep >= 0)
-            unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, i, buf, is_core, cut, exact, plist,
-                             &s_npairs, pcap);
-        lds_barrier();
-        run_list();
-        lds_barrier();
-        if (i == 0) s_npairs = 0;  // (ordered before the sweep's pushes by the barrier below)
-#else
         if (i < nq && rep >= 0)
             unite_adjacent32(u.lp, u.lrange, u.lmask, u.qmap, i, buf, is_core, cut, exact);
         lds_barrier();
-#endif
         AB_STAMP(6);
         // the adjacent pairs joined every core of the tile: no distance-2 pair can add an edge
         // inside it
@@ -1799,13 +1723,6 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
                 const uint32_t rj = u.lrange[j];
                 if (!(rj >> 31)) continue;
                 if (lfind(u.lp, qi) == lfind(u.lp, j)) continue;
-#if DBSCAN_AB_COOP_TOUCH
-                const int kk = atomicAdd(&s_npairs, 1);
-                if (kk < pcap) {
-                    plist[kk] = (uint32_t)qi | ((uint32_t)j << 16);
-                    continue;
-                }
-#endif
                 const int ab = (int)(ri & 2047u), ae = ab + (int)((ri >> 11) & 2047u);
                 const int bb = (int)(rj & 2047u), be = bb + (int)((rj >> 11) & 2047u);
                 if (quarters_touch32(buf, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, cut,
@@ -1813,10 +1730,6 @@ __device__ void fused_tile_union32(int t, int q0, int nq, int b, int e, uint32_t
                     lunite(u.lp, qi, j);
             }
             lds_barrier();
-#if DBSCAN_AB_COOP_TOUCH
-            run_list();
-            lds_barrier();
-#endif
         }
         AB_STAMP(7);
     }
@@ -3393,11 +3306,6 @@ static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* s
 // from the device bbox (no host readback), the radix sort skips the key digits the grid does
 // not use, and the clique (quarter-cell) and per-point union paths are both enqueued, each
 // exiting at once when the grid selects the other.
-// LDS fits write their statistics straight into the handle's pinned stats block
-#ifndef DBSCAN_AB_MIRROR
-#define DBSCAN_AB_MIRROR 0
-#endif
-constexpr bool kStatsMirror = DBSCAN_AB_MIRROR != 0;
 // The handle's pinned stats block and its device address (allocated on first use).
 static double* stats_mirror(Workspace& ws) {
     if (!ws.stats_host) {
@@ -3438,14 +3346,14 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (!a.zone && n <= std::min<int64_t>(a.small_max, kSmallMaxPoints) &&
         small_fit_eligible(n, a.eps, a.mode)) {
         StageTimer t(prof, s, "small_fit");
-        double* mirror = kStatsMirror ? stats_mirror(ws) : nullptr;  // (read back, no copy)
+        double* mirror = stats_mirror(ws);  // (LDS fits write their stats there: no copy back)
         if (n >= a.spread_min)  // several workgroups, two grid barriers (spread_fit_kernel)
             enqueue_spread_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
                                a.flag, gp, st, mirror);
         else
             enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
                                a.mode, a.cluster, a.flag, nullptr, gp, st, mirror);
-        ws.fit_mirrored = mirror != nullptr;
+        ws.fit_mirrored = true;
         return;
     }
     DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));

@@ -867,76 +867,6 @@ __device__ __forceinline__ int sp_count_wave(const SmLds& L, const SmCtx& c, int
     return cnt;
 }
 
-// Core p's unions (the rule of sm_union_walk): 64 candidates q > p of a stencil row per step;
-// among the step's hits (cores within eps, not already under p's root), the first of each
-// quarter not yet joined unites with p -- one lane unites, in lane order, so the first core of
-// a quarter is the one joined, as in the serial walk.
-__device__ __forceinline__ void sp_union_wave(SmLds& L, const SmCtx& cx_, int p, bool quarters,
-                                              double reach_kx, double reach_ky) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int nx = cx_.nx, ny = cx_.ny;
-    const float2 me = L.rec[p];
-    uint64_t done = 0;
-    int rp = 0;
-    if (lane == 0) rp = sm_find(L.par, p);  // (one lane: the find compresses the path)
-    rp = __shfl(rp, 0);
-    const int c = (int)(L.info[p] & kCellMask);
-    const int cy = c / nx, cx = c - cy * nx;
-    const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
-    if (quarters && !cx_.exact_only) {  // quarters wholly beyond eps (sm_union_walk)
-        const float tx = (float)((double)me.x + reach_kx - (double)cx);
-        const float ty = (float)((double)me.y + reach_ky - (double)cy);
-        const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
-        const float rr = (sqrtf(cx_.hi) + mg) * (sqrtf(cx_.hi) + mg);
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const float y0 = 0.5f * (float)a - 1.0f,
-                        dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
-#pragma unroll
-            for (int b = 0; b < 6; ++b) {
-                const float xb = 0.5f * (float)b - 1.0f;
-                const float dx = fmaxf(0.0f, fmaxf(xb - tx, tx - (xb + 0.5f)));
-                if (dx * dx + dy * dy > rr) done |= 1ull << (a * 6 + b);
-            }
-        }
-    }
-    for (int d = 0; d < 3; ++d) {
-        const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
-        if (r < 0 || r >= ny) continue;
-        const int rb = r * nx;
-        const int e = L.cst[rb + x1 + 1];
-        const int b1 = x0 + 1 <= x1 ? (int)L.cst[rb + x0 + 1] : 0x7FFFFFFF;
-        const int b2 = x0 + 2 <= x1 ? (int)L.cst[rb + x0 + 2] : 0x7FFFFFFF;
-        const int wr = (r - cy + 1) * 3 + (x0 - cx + 1);
-        for (int q0 = max((int)L.cst[rb + x0], p + 1); q0 < e; q0 += 64) {
-            const int q = q0 + lane;
-            int bit = 0;
-            bool cand = q < e && L.core[q] != 0;
-            if (cand && quarters) {
-                const int w = wr + (q >= b1 ? 1 : 0) + (q >= b2 ? 1 : 0);
-                const int qd = (int)((L.info[q] >> 13) & 3u);
-                bit = (2 * (w / 3) + (qd >> 1)) * 6 + 2 * (w % 3) + (qd & 1);
-                cand = ((done >> bit) & 1ull) == 0;
-            }
-            if (cand) cand = sm_ld(L.par + q) != rp && sm_pair(L, cx_, p, me, q, L.rec[q]);
-            uint64_t hits = __ballot(cand);
-            while (hits) {
-                const int l = __ffsll((long long)hits) - 1;
-                int nr = 0;
-                if (lane == 0) nr = sm_unite_from(L.par, L.info, rp, q0 + l);
-                rp = __shfl(nr, 0);
-                if (quarters) {
-                    const int bl = __shfl(bit, l);
-                    done |= 1ull << bl;
-                    hits &= ~__ballot(cand && bit == bl);
-                } else {
-                    hits &= hits - 1;
-                }
-            }
-        }
-    }
-}
-
 // The smallest root visit index among non-core p's core neighbours (sm_best_root), 64
 // candidates per step, the minimum taken across the wave.
 __device__ __forceinline__ uint32_t sp_best_root_wave(const SmLds& L, const SmCtx& c, int p) {
@@ -1024,34 +954,14 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
         __syncthreads();
     }
     const int s0 = L.band[0], s1 = L.band[1], nb = s1 - s0;
-    const bool split = 3 * nb <= kSmT;  // (labels: one thread per stencil row)
 
-    // ---- count (own slots) ----
-#if DBSCAN_AB_SPREAD_WAVE
-    // one wave per own point, its 64 lanes over 64 candidates of a stencil row at a time, the
-    // hits counted by a ballot (no lane runs a walk of its own)
-    {
-        const int wv = tid >> 6;
-        for (int p = s0 + wv; p < s1; p += kSmW) {
-            const bool cc = min_points <= 0 || sp_count_wave(L, c, p, min_points) >= min_points;
-            if ((tid & 63) == 0) sa.core[L.info[p] >> 16] = cc ? 1 : 0;
-        }
+    // ---- count (own slots): one wave per own point, its 64 lanes over 64 candidates of a
+    // stencil row at a time, hits counted by a ballot (one thread per row measured slower from
+    // 2000 points: 19.8 -> 18.1 us at 2000, 26.9 -> 24.6 at 8192) ----
+    for (int p = s0 + (tid >> 6); p < s1; p += kSmW) {
+        const bool cc = min_points <= 0 || sp_count_wave(L, c, p, min_points) >= min_points;
+        if ((tid & 63) == 0) sa.core[L.info[p] >> 16] = cc ? 1 : 0;
     }
-#else
-    // each stencil row one work item, the counts summed per point in par (free until the union)
-    for (int i = tid; i < nb; i += kSmT) L.par[i] = 0;
-    __syncthreads();
-    if (min_points > 0) {
-        for (int it = tid; it < nb * 3; it += kSmT) {
-            const int i = it / 3;
-            const int cnt = sm_count(L, c, s0 + i, min_points, it - 3 * i);
-            if (cnt) atomicAdd(&L.par[i], cnt);
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < nb; i += kSmT)
-        sa.core[L.info[s0 + i] >> 16] = (min_points <= 0 || L.par[i] >= min_points) ? 1 : 0;
-#endif
     SM_STAMP(7);
     sp_grid_sync(sa.bar, (uint32_t)G, st, mirror);
     SM_STAMP(8);
@@ -1065,16 +975,13 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     const bool quarters = L.G.clique != 0;
     const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
     const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy;
-#if DBSCAN_AB_SPREAD_WAVE
-    for (int p = s0 + (tid >> 6); p < s1; p += kSmW)
-        if (L.core[p]) sp_union_wave(L, c, p, quarters, reach_kx, reach_ky);
-#else
+    // (one thread per stencil row: the wave-cooperative form, a serial unite per joined quarter,
+    // measured 48 -> 92 us at 8192 points)
     for (int it = tid; it < nb * 3; it += kSmT) {
         const int i = it / 3;
         if (L.core[s0 + i])
             sm_union_walk(L, c, s0 + i, it - 3 * i, quarters, reach_kx, reach_ky);
     }
-#endif
     __syncthreads();
     SM_STAMP(9);
     // publish the forest: every core slot that is not a root, with its root (read-only walks)
@@ -1159,7 +1066,6 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 
     // ---- labels of the own slots (+ the non-finite points: the last workgroup) ----
     const auto root_of = [&](int q) { return (uint32_t)L.par[L.info[q] >> 16]; };
-#if DBSCAN_AB_SPREAD_WAVE
     for (int p = s0 + tid; p < s1; p += kSmT)  // cores: one thread each
         if (L.core[p]) sm_write_label(L, p, root_of(p), 0xFFFFFFFFu, mode, cluster, flag);
     for (int p = s0 + (tid >> 6); p < s1; p += kSmW) {  // non-cores: a wave each
@@ -1167,31 +1073,6 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
         const uint32_t b = sp_best_root_wave(L, c, p);
         if ((tid & 63) == 0) sm_write_label(L, p, 0u, b, mode, cluster, flag);
     }
-#else
-    if (split) {
-        if (tid < nb) L.sbest[tid] = 0xFFFFFFFFu;
-        __syncthreads();
-        if (tid < 3 * nb) {
-            const int i = tid / 3, p = s0 + i;
-            if (!L.core[p]) {
-                const uint32_t b = sm_best_root(L, c, p, tid - 3 * i, root_of);
-                if (b != 0xFFFFFFFFu) atomicMin(&L.sbest[i], b);
-            }
-        }
-        __syncthreads();
-        if (tid < nb) {
-            const int p = s0 + tid;
-            sm_write_label(L, p, L.core[p] ? root_of(p) : 0u, L.sbest[tid], mode, cluster, flag);
-        }
-    } else {
-        for (int p = s0 + tid; p < s1; p += kSmT) {
-            const bool cc = L.core[p] != 0;
-            sm_write_label(L, p, cc ? root_of(p) : 0u,
-                           cc ? 0xFFFFFFFFu : sm_best_root(L, c, p, -1, root_of), mode, cluster,
-                           flag);
-        }
-    }
-#endif
     if (g == G - 1)
         for (int p = nf + tid; p < m; p += kSmT)
             sm_write_label(L, p, L.core[p] ? root_of(p) : 0u, 0xFFFFFFFFu, mode, cluster, flag);
