@@ -5,15 +5,16 @@
 //                          -> n_shards x-slabs at count quantiles snapped to the 2*eps grid,
 //                             each with its 2-zone halo (node.py: make_cuts, zones)
 //   DBSCAN.scala:150-155   LocalDBSCANNaive.fit per partition
-//                          -> dbscan_slab_fit_device per shard, shard s on device
-//                             s % device_count, one host thread and one handle (HIP stream) per
-//                             device; shards sharing a device run one after another on its
-//                             handle and are re-fitted before their label (one workspace per
-//                             device, so 8 shards of 10^9 points fit one GPU's HBM)
+//                          -> the lean slab fit per shard, shard s on device s % device_count,
+//                             one host thread and one handle (HIP stream) per device; shards
+//                             sharing a device run one after another on its handle and are
+//                             re-fitted before their label (one workspace per device, so 8
+//                             shards of 10^9 points fit one GPU's HBM)
 //   DBSCAN.scala:158-222   band points, findAdjacencies, DBSCANGraph, global ids
-//                          -> records (gid of a shared core, gid of its local root) merged by a
-//                             host union-find (the records are a thin band: O(1e5) at 1e8 pts),
-//                             global s(K) per local root, cluster id = rank of s(K)
+//                          -> records (gid of a shared core, gid of its local root) merged by
+//                             merge.hip's lock-free union-find on every device (the records are
+//                             a thin band: O(1e5) at 1e8 pts), global s(K) per local root,
+//                             cluster id = rank of s(K)
 //   DBSCAN.scala:232-270   relabel                  -> dbscan_slab_label_device per shard
 // The result equals ONE fit of all points, bit for bit.
 #include "../../include/dbscan_hip.h"

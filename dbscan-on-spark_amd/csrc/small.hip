@@ -1,12 +1,14 @@
-// small.hip -- the local fit of one partition held entirely in ONE workgroup's LDS, for the
+// small.hip -- the local fit of one partition held entirely in LDS, in one launch, for the
 // partition sizes DBSCAN.train hands the seam, and its batched form.
 //
 // DBSCAN.scala:150-155 calls `new LocalDBSCANNaive(eps, minPoints).fit(points)` once per spatial
 // partition: at most maxPointsPerPartition points (EvenSplitPartitioner.scala:44-209) plus the
 // eps halo (DBSCAN.scala:116-137) -- hundreds to ~10^4 points.  The tiled pipeline of fit.hip is
-// ~45 launches whose fixed cost dominates at that size; here one workgroup of 1024 threads does
-// the whole fit of a partition of <= kSmallMaxPoints points in one launch, and a batch of an
-// executor's partitions is one launch with one workgroup per partition (dbscan_fit_batch).
+// ~45 launches whose fixed cost dominates at that size; here a partition of <= kSmallMaxPoints
+// points is fitted in one launch: by one workgroup of 1024 threads (small_fit_kernel; a batch of
+// an executor's partitions is one launch with one workgroup per partition, dbscan_fit_batch), or
+// by ~n/256 workgroups that each stage the whole partition and meet at two grid barriers
+// (spread_fit_kernel, below).
 //
 // Same closed form as fit.hip (LocalDBSCANNaive.scala:37-118,
 // LocalDBSCANArchery.scala:103-106), same fp64 predicate (DBSCANPoint.scala:26-30), same results
