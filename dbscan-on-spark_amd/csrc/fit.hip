@@ -533,6 +533,78 @@ __global__ __launch_bounds__(kBlock) void tslot_kernel(
     }
 }
 
+// tslot_kernel with kTslotU tiles per wave and trip, their dependent loads (tile -> its first
+// slot -> that slot's cell -> the cells' keys and starts) issued together: at config 5's share
+// (1.46 M tiles) the one-tile form walks ~45 tiles per wave, a chain of four loads each (fit
+// 24.6 -> 24.45 ms there; at 10^7 points the one-tile form is 5 us faster: kTslotMultiPoints).
+constexpr int kTslotU = 4;
+constexpr int64_t kTslotMultiPoints = int64_t(1) << 25;
+__global__ __launch_bounds__(kBlock) void tslot_multi_kernel(
+    const int32_t* __restrict__ tstart, const uint32_t* __restrict__ tkey,
+    const int32_t* __restrict__ ntiles_p, const int32_t* __restrict__ cell,
+    const uint32_t* __restrict__ ckey, const int32_t* __restrict__ cstart,
+    const int32_t* __restrict__ ncells_p, const int32_t* __restrict__ qidx,
+    int32_t* __restrict__ tslot, int32_t* __restrict__ tq) {
+    const int lane = threadIdx.x & 63;
+    const int ntiles = *ntiles_p, ncells = *ncells_p;
+    const int stride = gridDim.x * (kBlock / 64);
+    for (int t0 = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); t0 < ntiles;
+         t0 += kTslotU * stride) {  // wave-uniform; no block barriers below
+        int t[kTslotU], ts0[kTslotU], end[kTslotU], c0[kTslotU];
+        uint32_t tk[kTslotU], ck[kTslotU];
+#pragma unroll
+        for (int u = 0; u < kTslotU; ++u) {
+            t[u] = t0 + u * stride;
+            const bool live = t[u] < ntiles;
+            tk[u] = live ? tkey[t[u]] : 0u;
+            ts0[u] = live ? tstart[t[u]] : 0;
+            end[u] = live ? tstart[t[u] + 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kTslotU; ++u) c0[u] = t[u] < ntiles ? cell[ts0[u]] : 0;
+#pragma unroll
+        for (int u = 0; u < kTslotU; ++u) {
+            const int c = c0[u] + lane;
+            ck[u] = (t[u] < ntiles && c < ncells) ? ckey[c] : ~0u;
+        }
+        int st[kTslotU];
+#pragma unroll
+        for (int u = 0; u < kTslotU; ++u) {
+            uint64_t occ = (ck[u] >> 6) == tk[u] ? 1ull << (ck[u] & 63u) : 0ull;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) occ |= __shfl_xor(occ, o, 64);
+            const uint64_t rest = occ >> lane;
+            st[u] = end[u];
+            if (t[u] < ntiles && rest) {
+                const int nl = lane + __builtin_ctzll(rest);  // first occupied local >= lane
+                const int rank = __popcll(occ & ((nl == 0) ? 0ull : (~0ull >> (64 - nl))));
+                st[u] = cstart[c0[u] + rank];
+            }
+        }
+        int qs[kTslotU], qe[kTslotU];
+        if (qidx) {
+#pragma unroll
+            for (int u = 0; u < kTslotU; ++u) {
+                const bool live = t[u] < ntiles;
+                qe[u] = live ? qidx[end[u] - 1] + 1 : 0;
+                qs[u] = (live && st[u] < end[u]) ? qidx[st[u]] : qe[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kTslotU; ++u) {
+            if (t[u] >= ntiles) continue;
+            int32_t* ts = tslot + (int64_t)t[u] * kTslot;
+            ts[lane] = st[u];
+            if (lane == 0) ts[64] = end[u];
+            if (qidx) {
+                int32_t* tqq = tq + (int64_t)t[u] * kTslot;
+                tqq[lane] = qs[u];
+                if (lane == 0) tqq[64] = qe[u];
+            }
+        }
+    }
+}
+
 // Per cell: the stencil's slot pieces (rows cy, cy-1, cy+1; a row of 3 cells splits in two
 // where it crosses a tile edge) and the cell's own range.  Used by the global-memory paths.
 __global__ __launch_bounds__(kBlock) void segs_kernel(const uint32_t* __restrict__ ckey,
@@ -3514,10 +3586,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            klaunch(prof, "tslot", tslot_kernel,
-                    dim3((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid)),
-                    dim3(kBlock), 0, s, tstart, tkey, &st[kStTiles], cell, ckey, cstart,
-                    &st[kStCells], qidx, tslot, tq);
+            const dim3 tgrid((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid));
+            if (n >= kTslotMultiPoints)
+                klaunch(prof, "tslot", tslot_multi_kernel, tgrid, dim3(kBlock), 0, s, tstart, tkey,
+                        &st[kStTiles], cell, ckey, cstart, &st[kStCells], qidx, tslot, tq);
+            else
+                klaunch(prof, "tslot", tslot_kernel, tgrid, dim3(kBlock), 0, s, tstart, tkey,
+                        &st[kStTiles], cell, ckey, cstart, &st[kStCells], qidx, tslot, tq);
             DBSCAN_HIP_CHECK(hipGetLastError());
             klaunch(prof, "tstage", thalo_kernel,
                     dim3((unsigned)std::min<int64_t>(

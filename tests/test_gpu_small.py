@@ -282,3 +282,19 @@ def test_spread_fits_from_concurrent_handles(dm):
         for hh in handles:
             hh.close()
     assert not errors, errors[0]
+
+
+@pytest.mark.parametrize("m", [9000, 65536, 65537])
+def test_host_array_fit_around_the_pinned_staging_limit(dm, handle, m):
+    """dbscan_fit_h stages partitions of <= 65536 points through one pinned block and one DMA
+    each way; above that it copies the caller's arrays directly: both sides of the limit, each
+    against the oracle, and the caller's output arrays written in full."""
+    rng = np.random.default_rng(65000 + m)
+    x, y = _fuzz_set(rng, m)
+    x *= 20.0
+    y *= 20.0
+    cl = np.full(m, -5, np.int32)
+    fl = np.full(m, 7, np.uint8)
+    got = dm.fit_arrays(x, y, 0.25, 6, 0, handle=handle, cluster_out=cl, flag_out=fl)
+    _eq(got, O.fit_grid(x, y, 0.25, 6, 0), f"m={m}")
+    assert (cl >= 0).all() and (fl <= 2).all()
