@@ -3586,12 +3586,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            const dim3 tgrid((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid));
+            const dim3 tsgrid((unsigned)std::min<int64_t>((ntile_bound + 3) / 4, kTileGrid));
             if (n >= kTslotMultiPoints)
-                klaunch(prof, "tslot", tslot_multi_kernel, tgrid, dim3(kBlock), 0, s, tstart, tkey,
+                klaunch(prof, "tslot", tslot_multi_kernel, tsgrid, dim3(kBlock), 0, s, tstart, tkey,
                         &st[kStTiles], cell, ckey, cstart, &st[kStCells], qidx, tslot, tq);
             else
-                klaunch(prof, "tslot", tslot_kernel, tgrid, dim3(kBlock), 0, s, tstart, tkey,
+                klaunch(prof, "tslot", tslot_kernel, tsgrid, dim3(kBlock), 0, s, tstart, tkey,
                         &st[kStTiles], cell, ckey, cstart, &st[kStCells], qidx, tslot, tq);
             DBSCAN_HIP_CHECK(hipGetLastError());
             klaunch(prof, "tstage", thalo_kernel,
