@@ -243,7 +243,8 @@ struct SmLds {
     double red[5][kSmW];
     int wsc[kSmW + 1];
     int nonfin;
-    int band[4];  // spread fits: the owned slots [band[0], band[1]), the published pair count
+    int band[8];  // spread fits: the union's slots [band[0], band[1]), the published pair count
+                  // band[2], the count's and labels' slots [band[4], band[5])
     SmGrid G;
     uint32_t sbest[kSmT / 3 + 1];  // row-split phases: per-point counters / min roots
 };
@@ -952,15 +953,26 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
             }
             L.band[tid] = g + tid == G ? nf : (int)L.cst[lo];
             if (tid == 0) L.band[2] = 0;
+        } else if (tid < 4) {
+            // the count and the labels: ~nf/G points each (cell starts are alike in every stage;
+            // the walks' work estimate would give the sparse bands far more points to count)
+            const int want = (int)((int64_t)(g + tid - 2) * nf / G);
+            int lo = 0, hi = ncells;  // smallest cell k with cst[k] >= want (cst[ncells] = nf)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int)L.cst[mid] >= want) hi = mid; else lo = mid + 1;
+            }
+            L.band[tid + 2] = g + tid - 2 == G ? nf : (int)L.cst[lo];
         }
         __syncthreads();
     }
     const int s0 = L.band[0], s1 = L.band[1], nb = s1 - s0;
+    const int c0 = L.band[4], c1 = L.band[5];
 
     // ---- count (own slots): one wave per own point, its 64 lanes over 64 candidates of a
     // stencil row at a time, hits counted by a ballot (one thread per row measured slower from
     // 2000 points: 19.8 -> 18.1 us at 2000, 26.9 -> 24.6 at 8192) ----
-    for (int p = s0 + (tid >> 6); p < s1; p += kSmW) {
+    for (int p = c0 + (tid >> 6); p < c1; p += kSmW) {
         const bool cc = min_points <= 0 || sp_count_wave(L, c, p, min_points) >= min_points;
         if ((tid & 63) == 0) sa.core[L.info[p] >> 16] = cc ? 1 : 0;
     }
@@ -1068,9 +1080,9 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 
     // ---- labels of the own slots (+ the non-finite points: the last workgroup) ----
     const auto root_of = [&](int q) { return (uint32_t)L.par[L.info[q] >> 16]; };
-    for (int p = s0 + tid; p < s1; p += kSmT)  // cores: one thread each
+    for (int p = c0 + tid; p < c1; p += kSmT)  // cores: one thread each
         if (L.core[p]) sm_write_label(L, p, root_of(p), 0xFFFFFFFFu, mode, cluster, flag);
-    for (int p = s0 + (tid >> 6); p < s1; p += kSmW) {  // non-cores: a wave each
+    for (int p = c0 + (tid >> 6); p < c1; p += kSmW) {  // non-cores: a wave each
         if (L.core[p]) continue;
         const uint32_t b = sp_best_root_wave(L, c, p);
         if ((tid & 63) == 0) sm_write_label(L, p, 0u, b, mode, cluster, flag);
