@@ -1146,11 +1146,9 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
-#ifndef DBSCAN_AB_SPREAD_PER
-#define DBSCAN_AB_SPREAD_PER 256
-#endif
-// Workgroups of a spread fit: one per kSpreadPer points (at most kSpreadMaxWG)
-constexpr int kSpreadPer = DBSCAN_AB_SPREAD_PER;
+// Workgroups of a spread fit: one per kSpreadPer points (at most kSpreadMaxWG; 128 and 512
+// measured equal at 8192 points, 512 slower below it)
+constexpr int kSpreadPer = 256;
 constexpr size_t kSpreadHead = 512;  // bar[2] at 0, npairs[kSpreadMaxWG] at 64
 
 void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
