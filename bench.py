@@ -1,6 +1,8 @@
 """Benchmark: points clustered/s on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+        (N > 1 without a launcher: bench.py starts the N ranks below as a child process and
+        relays rank 0's line; fewer than N visible GPUs: exit 2, nothing measured)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -126,6 +128,8 @@ def parse(argv=None):
     ap.add_argument("--no-seam", action="store_true",
                     help="skip the seam leg (partition-sized fits and batches, N = 1)")
     ap.add_argument("--seam-only", action="store_true", help="only the seam leg (no timed fit)")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="test hook: the ranks join the process group and report their devices")
     return ap.parse_args(argv)
 
 
@@ -276,19 +280,98 @@ def cpu_baseline(x, y, eps, min_points, threads, sample_s=None, h=None):
     }
 
 
+def visible_devices() -> int:
+    """GPUs this process can see.  torch.cuda.device_count() does not initialise HIP on this
+    image, so a launcher may still start children after it."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) started without a launcher (no WORLD_SIZE in the environment): start
+    the N ranks as ONE child process -- python -m torch.distributed.run --nproc-per-node N on
+    127.0.0.1 running this script with the same arguments -- relay its output (rank 0 prints
+    the JSON line) and return its exit code.  Fewer than N visible GPUs: a clear error, exit 2,
+    nothing measured.  Called before anything touches the GPU (no exec: the child is a
+    separate process).  Returns None when this process should run the bench itself."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    ndev = visible_devices()
+    if ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this process sees "
+              f"{ndev}; refusing to measure fewer GPUs than asked", file=sys.stderr, flush=True)
+        return 2
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    print(f"bench.py: no launcher in the environment; starting {args.gpus} ranks: "
+          + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def rank_devices(dist, backend):
+    """(world size, the device each rank runs on) as the process group sees them: every rank's
+    (rank, local device index, PCI bus id) all-gathered."""
+    import torch
+
+    if torch.cuda.is_available() and backend == "nccl":
+        d = torch.cuda.current_device()
+        bus = getattr(torch.cuda.get_device_properties(d), "pci_bus_id", -1)
+    else:
+        d, bus = -1, -1
+    mine = [dist.get_rank(), d, int(bus)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, mine)
+    return dist.get_world_size(), [{"rank": r, "device": dv, "pci_bus_id": b}
+                                   for r, dv, b in sorted(out)]
+
+
+def launch_probe(args):
+    """--launch-probe (test hook for the launcher): each rank joins the process group and
+    reports where it runs; rank 0 prints one JSON line.  No fit, no GPU work with gloo."""
+    import torch.distributed as dist
+
+    dist.init_process_group(args.backend)
+    world, devs = rank_devices(dist, args.backend)
+    if dist.get_rank() == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "devices": devs}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_probe:
+        launch_probe(args)
+        return
     import numpy as np
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
+    if world != args.gpus and (world > 1 or "WORLD_SIZE" in os.environ):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     node_path = world > 1 or args.node or args.force_collectives
     workload_defaults(args, world)
-    dev = local_rank % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and local_rank >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK={local_rank} but only {ndev} visible GPUs "
+                         "(one rank per GPU; ranks never share a device)")
+    dev = local_rank % max(1, ndev)
     torch.cuda.set_device(dev)
     import dbscan_amd
     from dbscan_amd import device as D
@@ -311,6 +394,15 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(args.backend)
+        pg_world, pg_devices = rank_devices(dist, args.backend)
+        if pg_world != world:
+            raise SystemExit(f"WORLD_SIZE={world} but the process group has {pg_world} ranks")
+        if args.backend == "nccl" and len({d["pci_bus_id"] for d in pg_devices}) != pg_world:
+            raise SystemExit(f"ranks share GPUs: {pg_devices}")
+    else:
+        pg_devices = [{"rank": 0, "device": dev,
+                       "pci_bus_id": getattr(torch.cuda.get_device_properties(dev),
+                                             "pci_bus_id", -1)}]
 
     n_total = args.points_per_gpu * world
     if not node_path:
@@ -499,6 +591,8 @@ def main():
                                 f"; per-job setup outside the timed steps (synthetic data, "
                                 f"slab cuts, zones, halo routing): {setup_ms} ms"),
                 "node_setup_ms": setup_ms,
+                "world_size": world,
+                "devices": pg_devices,
                 "node_step_note": (None if not node_path else
                                    "a timed step re-fits every slab and exchanges the b-side "
                                    "records; the cuts, zones and the a-side records are fixed "

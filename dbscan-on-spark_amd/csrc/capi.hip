@@ -187,6 +187,7 @@ struct dbscan_handle {
     int64_t small_max = DBSCAN_SMALL_DEFAULT_POINTS;  // one-workgroup fits up to this many points
     int64_t spread_min = DBSCAN_SPREAD_DEFAULT_POINTS;  // LDS fits from here: several workgroups
     bool pending = false;             // an asynchronous fit whose stats are not read yet
+    int32_t* pending_nk = nullptr;    // ... and the device word its cluster count went to
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
     void* fpinned = nullptr;          // partition-sized dbscan_fit_h: pinned x|y and cluster|flag
@@ -354,7 +355,12 @@ namespace {
 void settle(dbscan_handle* h) {
     if (!h->pending) return;
     h->pending = false;
-    h->stats = dbscan::read_fit_stats(h->stream, h->ws);
+    h->stats = dbscan::read_fit_stats(h->stream, h->ws, &h->prof);
+    if (h->ws.spread_recovered && h->pending_nk) {  // (the re-run fit's count, like the first)
+        dbscan::write_nclusters(h->stream, h->ws, h->pending_nk);
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+    }
+    h->pending_nk = nullptr;
     h->prof.flush();
 }
 }  // namespace
@@ -394,6 +400,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
         h->pending = true;
+        h->pending_nk = d_n_clusters;
         return DBSCAN_OK;
     });
 }
@@ -477,7 +484,12 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
             dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
             DBSCAN_HIP_CHECK(
                 hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
-            h->stats = dbscan::read_fit_stats(h->stream, h->ws);  // (synchronizes)
+            h->stats = dbscan::read_fit_stats(h->stream, h->ws, &h->prof);  // (synchronizes)
+            if (h->ws.spread_recovered) {  // the fit was re-run: its labels copied back again
+                DBSCAN_HIP_CHECK(
+                    hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
+                DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+            }
             h->slab.nf = h->stats.nf;
             memcpy(cluster_out, pin + in_b, 4 * (size_t)n);
             memcpy(flag_out, pin + in_b + 4 * (size_t)n, (size_t)n);
@@ -543,6 +555,13 @@ int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double ep
                                               cluster_out, flag_out, n_clusters_out, &err);
         if (rc != DBSCAN_OK) set_err(err);
         return rc;
+    });
+}
+
+int32_t dbscan_selftest_worker_errors(int32_t* rcs, int32_t n) {
+    return guarded(nullptr, [&]() -> int32_t {
+        if (n < 0 || (n > 0 && !rcs)) throw dbscan::ArgError{"selftest: bad arguments"};
+        return dbscan::worker_selftest(rcs, n);
     });
 }
 
@@ -969,6 +988,26 @@ int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points) {
     const int64_t prev = h->spread_min;
     h->spread_min = std::max<int64_t>(min_points, 0);
     return prev;
+}
+
+int64_t dbscan_set_spread_spin_limit(dbscan_handle* h, int64_t polls) {
+    if (!h || polls < 0 || polls > (int64_t)UINT32_MAX) {
+        set_err(h ? "polls out of range" : "NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int64_t prev = h->ws.spread_spin_limit;
+    h->ws.spread_spin_limit = (uint32_t)polls;
+    return prev;
+}
+
+int64_t dbscan_spread_fallbacks(dbscan_handle* h) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    return h->ws.spread_fallbacks;
 }
 
 }  // extern "C"

@@ -3394,6 +3394,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                  SlabState* slab) {
     if (slab) slab->valid = false;
     ws.fit_mirrored = false;
+    ws.spread_recall.valid = false;
     const int64_t n = a.n;
     const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
     const int mode =
@@ -3841,10 +3842,12 @@ void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst) {
         hipMemcpyAsync(dst, ws.misc.p, kFitStatsDoubles * sizeof(double), hipMemcpyDeviceToHost, s));
 }
 
-FitStats read_fit_stats(hipStream_t s, Workspace& ws) {
+FitStats read_fit_stats(hipStream_t s, Workspace& ws, Profiler* prof) {
     stats_mirror(ws);  // (pinned: a pageable copy costs a staging pass per fit)
     enqueue_fit_stats_copy(s, ws, ws.stats_host);
     if (ws.fit_n != 0) DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    // a spread fit whose workgroups were not all resident: re-run by one workgroup
+    ws.spread_recovered = recover_spread_fit(s, prof, ws);
     return parse_fit_stats(ws, ws.stats_host);
 }
 
@@ -3882,7 +3885,7 @@ FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
 int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, FitStats* st,
                 SlabState* slab) {
     enqueue_fit(s, ws, prof, a, slab);
-    const FitStats stats = read_fit_stats(s, ws);
+    const FitStats stats = read_fit_stats(s, ws, prof);
     if (slab) slab->nf = stats.nf;
     if (st) *st = stats;
     return a.zone ? 0 : stats.nclusters;

@@ -169,6 +169,8 @@ struct BucketSort {
     }
 };
 
+struct GridParams;
+
 struct Workspace {
     DevBuf key, key2, perm, perm2, hist, scan_tmp, xy, cell, ckey, cstart, seg, core, parent, lab,
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
@@ -179,6 +181,24 @@ struct Workspace {
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
     double* stats_dev = nullptr;   // ... its device address (LDS fits write it directly)
     bool fit_mirrored = false;     // the last fit wrote its stats into stats_host itself
+    // The last spread fit's arguments (small.hip): when a grid barrier of it gave up
+    // (st[kStError] == 2: its workgroups were not all resident), read_fit_stats re-runs the
+    // fit through the one-workgroup kernel (no barrier; the same results bit for bit).
+    struct SpreadRecall {
+        bool valid = false;
+        const double *x = nullptr, *y = nullptr;
+        int64_t n = 0;
+        double eps = 0.0;
+        int32_t min_points = 0, mode = 0;
+        int32_t* cluster = nullptr;
+        uint8_t* flag = nullptr;
+        GridParams* gp = nullptr;
+        int32_t* st = nullptr;
+        double* mirror = nullptr;
+    } spread_recall;
+    uint32_t spread_spin_limit = 1u << 21;  // barrier polls before giving up (0: at once; tests)
+    int64_t spread_fallbacks = 0;           // spread fits re-run by the one-workgroup kernel
+    bool spread_recovered = false;          // the last read_fit_stats re-ran the fit
     Workspace() = default;
     ~Workspace() {
         if (stats_host) (void)hipHostFree(stats_host);
@@ -314,7 +334,7 @@ int64_t run_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a, 
 // returns its stats, write_nclusters enqueues a copy of its cluster count to device memory.
 void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                  SlabState* slab);
-FitStats read_fit_stats(hipStream_t s, Workspace& ws);
+FitStats read_fit_stats(hipStream_t s, Workspace& ws, Profiler* prof = nullptr);
 // read_fit_stats in two halves: an asynchronous copy of the stats block to dst (pinned host
 // memory, kFitStatsDoubles doubles), and its parse once the copy has completed.
 constexpr int kFitStatsDoubles = 32;
@@ -379,6 +399,7 @@ int64_t scala_range_count(double start, double end, double step, bool inclusive)
 int32_t train_node(const double* x, const double* y, int64_t n, double eps, int32_t min_points,
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
                    int64_t* n_clusters_out, std::string* err);
+int32_t worker_selftest(int32_t* rcs, int32_t n);
 // Node-path routing (node.hip, dbscan_route_slabs_device): see include/dbscan_hip.h.
 int64_t route_slabs(hipStream_t s, DevBuf& scratch, DevBuf& tabbuf, const double* x,
                     const double* y, int64_t m, int64_t start, const double* cuts, int32_t n_cuts,
@@ -415,6 +436,9 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
                         const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
                         double* mirror = nullptr);
+// After the stream has drained: the last fit was a spread fit whose grid barrier gave up ->
+// re-run it through the one-workgroup kernel (synchronously), count it, return true.
+bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws);
 // DBSCAN.scala:116-137 on the host: the points every partition's outer rectangle (main grown
 // by eps, inclusive) holds, in input order (partition.hip)
 int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,

@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <memory>
 #include <thread>
@@ -431,7 +432,86 @@ inline void ccheck(int32_t rc) {
     if (rc != DBSCAN_OK) throw rc;
 }
 
+// One device worker's outcome.  Every exception a worker body can throw (HipFail, an rc from
+// the C-ABI, dbscan::HipError from DBSCAN_HIP_CHECK / DevBuf, dbscan::ArgError, std::bad_alloc
+// from the host vectors, anything else) is mapped here: an exception escaping a std::thread
+// would std::terminate the whole process -- the executor JVM included.
+struct WorkerStatus {
+    int32_t rc = DBSCAN_OK;
+    std::string err;
+};
+
+inline void worker_status_from_current(WorkerStatus& ws) {
+    try {
+        throw;
+    } catch (const HipFail& e) {
+        ws.rc = (e.e == hipErrorOutOfMemory || e.e == hipErrorMemoryAllocation) ? DBSCAN_EOOM
+                                                                                : DBSCAN_EHIP;
+        ws.err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+    } catch (int32_t rc) {
+        ws.rc = rc;
+        ws.err = dbscan_last_error();
+    } catch (const HipError& e) {
+        ws.rc = (e.err == hipErrorOutOfMemory || e.err == hipErrorMemoryAllocation) ? DBSCAN_EOOM
+                                                                                    : DBSCAN_EHIP;
+        ws.err = e.what;
+    } catch (const ArgError& e) {
+        ws.rc = DBSCAN_EARG;
+        ws.err = e.what;
+    } catch (const std::bad_alloc&) {
+        ws.rc = DBSCAN_EOOM;
+        ws.err = "host allocation failed";
+    } catch (const std::exception& e) {
+        ws.rc = DBSCAN_EHIP;
+        ws.err = e.what();
+    } catch (...) {
+        ws.rc = DBSCAN_EHIP;
+        ws.err = "unknown error in a device worker";
+    }
+    if (ws.rc == DBSCAN_OK) ws.rc = DBSCAN_EHIP;  // (a thrown DBSCAN_OK is still a failure)
+}
+
+// f(w) for w < nworkers on one host thread each; false when any worker failed (its status set)
+template <class F>
+bool run_workers(int nworkers, std::vector<WorkerStatus>& st, F&& f) {
+    std::vector<std::thread> th;
+    for (int w = 0; w < nworkers; ++w)
+        th.emplace_back([&, w]() {
+            try {
+                f(w);
+            } catch (...) {
+                worker_status_from_current(st[(size_t)w]);
+            }
+        });
+    for (auto& t : th) t.join();
+    for (auto& s : st)
+        if (s.rc != DBSCAN_OK) return false;
+    return true;
+}
+
 }  // namespace
+
+// The worker error mapping on the host alone (no device): worker w throws kind w (0 none,
+// 1 HipFail OOM, 2 HipFail other, 3 rc EARG, 4 HipError, 5 ArgError, 6 bad_alloc,
+// 7 std::runtime_error, 8 an int64); its rc goes to rcs[w].  The C-ABI selftest behind it.
+int32_t worker_selftest(int32_t* rcs, int32_t n) {
+    std::vector<WorkerStatus> st((size_t)std::max(0, n));
+    run_workers(n, st, [](int w) {
+        switch (w % 9) {
+            case 1: throw HipFail{hipErrorOutOfMemory, "selftest"};
+            case 2: throw HipFail{hipErrorInvalidValue, "selftest"};
+            case 3: throw (int32_t)DBSCAN_EARG;
+            case 4: throw HipError(hipErrorInvalidValue, "selftest", __FILE__, __LINE__);
+            case 5: throw ArgError{"selftest"};
+            case 6: throw std::bad_alloc();
+            case 7: throw std::runtime_error("selftest");
+            case 8: throw (int64_t)7;
+            default: return;
+        }
+    });
+    for (int w = 0; w < n; ++w) rcs[w] = st[(size_t)w].rc;
+    return DBSCAN_OK;
+}
 
 // Routing of one chunk (see route_write_kernel): counts_out[d] = rows for rank d; rows written
 // when rows != nullptr and capacity (rows) suffices.  Returns the total row count.
@@ -546,30 +626,15 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         int64_t *ra = nullptr, *rb = nullptr, *roots = nullptr;
         int32_t* out_cl = nullptr;
         uint8_t* out_fl = nullptr;
-        int32_t rc = DBSCAN_OK;
-        std::string err;
     };
     std::vector<Dev> dv(nworkers);
-    // runs f(w) on one host thread per device; a failure is recorded per device
+    std::vector<WorkerStatus> wst(nworkers);
+    // runs f(w) on one host thread per device; a failure of any kind is recorded per device
     auto each_device = [&](auto&& f) {
-        std::vector<std::thread> th;
-        for (int w = 0; w < nworkers; ++w)
-            th.emplace_back([&, w]() {
-                try {
-                    hcheck(hipSetDevice(w), "hipSetDevice");
-                    f(w);
-                } catch (const HipFail& e) {
-                    dv[w].rc = e.e == hipErrorOutOfMemory ? DBSCAN_EOOM : DBSCAN_EHIP;
-                    dv[w].err = std::string(e.what) + ": " + hipGetErrorString(e.e);
-                } catch (int32_t rc) {
-                    dv[w].rc = rc;
-                    dv[w].err = dbscan_last_error();
-                }
-            });
-        for (auto& t : th) t.join();
-        for (auto& d : dv)
-            if (d.rc != DBSCAN_OK) return false;
-        return true;
+        return run_workers(nworkers, wst, [&](int w) {
+            hcheck(hipSetDevice(w), "hipSetDevice");
+            f(w);
+        });
     };
     auto lean_fit = [&](int r, int w) {
         DevShard& s = sh[r];
@@ -809,7 +874,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         return true;
     }();
     if (!ok) {
-        for (auto& d : dv)
+        for (auto& d : wst)
             if (d.rc != DBSCAN_OK) {
                 rc = d.rc;
                 *err = d.err;

@@ -809,16 +809,18 @@ __device__ __forceinline__ uint32_t sp_load(uint32_t* p) {
 // until `target` arrivals, and acquires (agent fence: this CU's stale lines dropped) before the
 // workgroup meets again and reads what the others published.  The poll gives up after ~2^21
 // rounds (seconds) and flags st[kStError] = 2: the fit then fails loudly instead of hanging.
-__device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st, double* mirror) {
+__device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st, double* mirror,
+                             uint32_t spin_limit) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t spins = 0; sp_load(bar) < target;) {
+        // (spin_limit 0: give up at once, the test of the fallback; the host re-runs the fit)
+        for (uint32_t spins = 0; spin_limit == 0 || sp_load(bar) < target;) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 21)) {
+            if (++spins > spin_limit) {
                 __hip_atomic_store(st + kStError, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (mirror)
                     __hip_atomic_store(reinterpret_cast<int32_t*>(mirror + kMiscState) + kStError,
@@ -897,12 +899,16 @@ __device__ __forceinline__ uint32_t sp_best_root_wave(const SmLds& L, const SmCt
 __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     const double* __restrict__ x, const double* __restrict__ y, int m, double eps, double eps2,
     int min_points, int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
-    GridParams* __restrict__ gp, int32_t* st, double* mirror, SpreadArgs sa) {
+    GridParams* __restrict__ gp, int32_t* st, double* mirror, SpreadArgs sa,
+    uint32_t spin_limit) {
     __shared__ SmLds L;
     const int tid = threadIdx.x;
     const int g = blockIdx.x, G = gridDim.x;
     SM_STAMP(0);
-    if (g == 0) sm_zero_stats(st, mirror, tid);  // (the fit state: no memset ahead of launch)
+    // (the fit state: no memset ahead of launch) -- except kStError, which the host clears
+    // before the launch: a late workgroup 0 must not erase a barrier failure another workgroup
+    // has already flagged
+    if (g == 0 && tid != kStError) sm_zero_stats(st, mirror, tid);
     int occupied = 0;
     // (every workgroup computes the same grid: a grid that cannot be sized returns them all
     // here, before any barrier)
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
         if ((tid & 63) == 0) sa.core[L.info[p] >> 16] = cc ? 1 : 0;
     }
     SM_STAMP(7);
-    sp_grid_sync(sa.bar, (uint32_t)G, st, mirror);
+    sp_grid_sync(sa.bar, (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(8);
 
     // ---- union of the own cores' walks (union-find over this stage's slots) ----
@@ -1010,7 +1016,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     __syncthreads();
     if (tid == 0) sa.npairs[g] = L.band[2];
     SM_STAMP(10);
-    sp_grid_sync(sa.bar, 2u * (uint32_t)G, st, mirror);
+    sp_grid_sync(sa.bar, 2u * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(11);
 
     // ---- merge: every workgroup's pairs into a union-find over input indices ----
@@ -1168,9 +1174,30 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     sa.core = reinterpret_cast<uint8_t*>(base + kSpreadHead);
     sa.pairs = reinterpret_cast<uint32_t*>(base + kSpreadHead + kSmN);
     const int G = (int)std::min<int64_t>(kSpreadMaxWG, std::max<int64_t>(1, n / kSpreadPer));
+    // kStError cleared ahead of the launch (the kernel never clears it): in the device state
+    // and, without waiting on the device, in the pinned mirror the host reads
+    DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
+    if (mirror && ws.stats_host)
+        reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
+    ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
+                                               gp, st, mirror};
     klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
-            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, sa);
+            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, sa,
+            ws.spread_spin_limit);
     DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
+bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws) {
+    Workspace::SpreadRecall& r = ws.spread_recall;
+    if (!ws.fit_mirrored || !r.valid || !ws.stats_host) return false;
+    int32_t* v = reinterpret_cast<int32_t*>(ws.stats_host + kMiscState);
+    if (v[kStError] != 2) return false;
+    // the one-workgroup kernel: no grid barrier, every label and statistic rewritten
+    enqueue_small_fits(s, prof, r.x, r.y, nullptr, nullptr, 1, r.n, r.eps, r.min_points, r.mode,
+                       r.cluster, r.flag, nullptr, r.gp, r.st, r.mirror);
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    ++ws.spread_fallbacks;
+    return true;
 }
 
 }  // namespace dbscan

@@ -50,6 +50,7 @@ SIGNATURES = [
     ("dbscan_format_double", _i32, [_d, ctypes.c_char_p]),
     ("dbscan_scala_range_count", _i64, [_d, _d, _d, _i32]),
     ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
+    ("dbscan_selftest_worker_errors", _i32, [_vp, _i32]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     ("dbscan_slab_fit_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
@@ -65,6 +66,8 @@ SIGNATURES = [
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
     ("dbscan_set_small_max", _i64, [_vp, _i64]),
     ("dbscan_set_spread_min", _i64, [_vp, _i64]),
+    ("dbscan_set_spread_spin_limit", _i64, [_vp, _i64]),
+    ("dbscan_spread_fallbacks", _i64, [_vp]),
     ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_fit_batch_device_async", _i32,
      [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
@@ -170,6 +173,21 @@ class Handle:
         spread_fit_kernel); above DBSCAN_SMALL_MAX_POINTS every LDS fit keeps one workgroup.
         Returns the previous value."""
         r = load().dbscan_set_spread_min(self._h, int(min_points))
+        if r < 0:
+            check(int(r))
+        return int(r)
+
+    def set_spread_spin_limit(self, polls: int) -> int:
+        """Test hook: the spread fit's barrier poll bound (0: every barrier gives up at once and
+        the fit is re-run by the one-workgroup kernel).  Returns the previous bound."""
+        r = load().dbscan_set_spread_spin_limit(self._h, int(polls))
+        if r < 0:
+            check(int(r))
+        return int(r)
+
+    def spread_fallbacks(self) -> int:
+        """Spread fits of this handle re-run by the one-workgroup kernel so far."""
+        r = load().dbscan_spread_fallbacks(self._h)
         if r < 0:
             check(int(r))
         return int(r)

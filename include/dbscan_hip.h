@@ -204,10 +204,19 @@ int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
  * workgroup stages the whole partition, counts and walks the unions of ~256 of its points, and two
  * grid-wide barriers exchange the core flags and the union forests (same results bit for bit).
  * A value above DBSCAN_SMALL_MAX_POINTS keeps every LDS fit on one workgroup.  Returns the
- * previous value.  (A spread fit whose workgroups cannot all be resident -- the GPU filled by
- * other work for seconds -- fails with DBSCAN_EHIP instead of waiting forever.) */
+ * previous value.  A spread fit whose workgroups cannot all be resident (the GPU filled by other
+ * work, e.g. many executors' spread fits at once) gives up its grid barrier after a bounded poll
+ * instead of waiting forever, and the fit is then re-run by the one-workgroup kernel in the same
+ * call (for dbscan_fit_device_async: in dbscan_sync), with the same results; the fit never
+ * fails for it.  Such re-runs are counted (dbscan_spread_fallbacks). */
 #define DBSCAN_SPREAD_DEFAULT_POINTS 512
 int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
+/* Test hook: the spread fit's barrier poll bound (default 2^21 polls, ~seconds); 0 makes every
+ * barrier give up at once, so every spread fit takes the one-workgroup re-run.  Returns the
+ * previous bound (negative: an error code). */
+int64_t dbscan_set_spread_spin_limit(dbscan_handle* h, int64_t polls);
+/* Spread fits of this handle re-run by the one-workgroup kernel so far (negative: an error). */
+int64_t dbscan_spread_fallbacks(dbscan_handle* h);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is
  * points [offsets[p], offsets[p+1]) of x, y (host array offsets, n_parts + 1 non-decreasing
@@ -248,6 +257,13 @@ int64_t dbscan_duplicate(const double* x, const double* y, int64_t n, const doub
 int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double eps,
                           int32_t min_points, int32_t mode, int32_t n_shards,
                           int32_t* cluster_out, uint8_t* flag_out, int64_t* n_clusters_out);
+
+/* Self-test of dbscan_train_node's per-device worker error handling, on the host alone (no
+ * device is touched): worker w of n throws failure kind w % 9 (none; a HIP OOM; another HIP
+ * failure; a C-ABI status; a HIP check; an argument error; std::bad_alloc; std::exception;
+ * an unknown type) and rcs[w] receives the status it maps to (DBSCAN_OK, EOOM, EHIP, EARG,
+ * EHIP, EARG, EOOM, EHIP, EHIP) -- never a process abort. */
+int32_t dbscan_selftest_worker_errors(int32_t* rcs, int32_t n);
 
 /* ---------------------------------------------------------------------------------------
  * Slab fits for the multi-GPU node path (dbscan_amd/node.py).  The caller

@@ -40,3 +40,49 @@ def test_config3_shaped_job_shards_into_slabs(tmp_path):
     np.testing.assert_array_equal(fl, rf)
     np.testing.assert_array_equal(cl, rc)
     assert ks == {rk}
+
+
+def test_gpus_n_without_launcher_starts_n_ranks(monkeypatch, capfd):
+    """`python bench.py --gpus N` with no WORLD_SIZE (the driver's BENCH form) must not time one
+    GPU: it starts N ranks through torch.distributed.run as a child.  The probe ranks (gloo, no
+    GPU) report the process group they joined; device count mocked to N."""
+    import json
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "visible_devices", lambda: 3)
+    argv = ["--gpus", "3", "--backend", "gloo", "--launch-probe"]
+    rc = bench.launch_ranks(bench.parse(argv), argv)
+    assert rc == 0
+    lines = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 3 and [r["rank"] for r in d["devices"]] == [0, 1, 2]
+
+
+def test_gpus_n_refused_without_n_devices(monkeypatch, capfd):
+    """Fewer visible GPUs than --gpus: exit 2 before anything runs, never an n_gpus=1 line."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "visible_devices", lambda: 1)
+    rc = bench.launch_ranks(bench.parse(["--gpus", "8"]), ["--gpus", "8"])
+    assert rc == 2
+    out = capfd.readouterr()
+    assert "n_gpus" not in out.out and "refusing" in out.err
+
+
+def test_gpus_n_cli_exits_nonzero_without_gpus():
+    """The CLI form end to end in this GPU-less container: non-zero, no JSON line."""
+    import os
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "{" not in r.stdout
+
+
+def test_launcher_not_used_under_torchrun(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.launch_ranks(bench.parse(["--gpus", "2"]), ["--gpus", "2"]) is None
+    monkeypatch.delenv("WORLD_SIZE")
+    assert bench.launch_ranks(bench.parse([]), []) is None

@@ -129,3 +129,18 @@ def test_fit_batch_rejects_bad_outputs_and_offsets():
     for o in ([-1, 4, 10], [0, 6, 4, 10], [0, 11]):
         with pytest.raises(ValueError):
             dbscan_amd.fit_batch(x, x, np.array(o), 0.3, 3)
+
+
+def test_train_node_worker_errors_never_abort():
+    """dbscan_train_node runs one host thread per device; every failure a worker can raise (HIP
+    errors, C-ABI codes, HipError / ArgError from the shared helpers, host std::bad_alloc,
+    other exceptions) becomes that device's status code instead of std::terminate (ADVICE
+    round 4).  Host-only self-test of the same runner, no device touched."""
+    L = _lib.load()
+    n = 18
+    rcs = (ctypes.c_int32 * n)(*([99] * n))
+    assert L.dbscan_selftest_worker_errors(rcs, n) == 0
+    ok, earg, ehip, eoom = _lib.DBSCAN_OK, _lib.DBSCAN_EARG, _lib.DBSCAN_EHIP, _lib.DBSCAN_EOOM
+    want = [ok, eoom, ehip, earg, ehip, earg, eoom, ehip, ehip]
+    assert list(rcs) == want * 2
+    assert L.dbscan_selftest_worker_errors(None, 2) == earg

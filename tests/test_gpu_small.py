@@ -298,3 +298,48 @@ def test_host_array_fit_around_the_pinned_staging_limit(dm, handle, m):
     got = dm.fit_arrays(x, y, 0.25, 6, 0, handle=handle, cluster_out=cl, flag_out=fl)
     _eq(got, O.fit_grid(x, y, 0.25, 6, 0), f"m={m}")
     assert (cl >= 0).all() and (fl <= 2).all()
+
+
+def test_spread_fit_barrier_give_up_falls_back(dm):
+    """A spread fit whose grid barrier gives up (its workgroups not all resident: forced here by
+    the test-only poll bound 0, so every barrier gives up at once) is re-run by the
+    one-workgroup kernel in the same call and still equals the oracle -- through dbscan_fit_h
+    (host arrays: the labels copied back again), dbscan_fit_device and dbscan_fit_device_async
+    + dbscan_sync (the device cluster count rewritten); every re-run is counted.  The
+    reference's fit never fails on valid input (DBSCAN.scala:153-154)."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(911)
+    h = dm.Handle(0)
+    try:
+        h.set_spread_min(0)
+        assert h.set_spread_spin_limit(0) == 1 << 21
+        before = h.spread_fallbacks()
+        expect = before
+        for m in (600, 3000, 8192):
+            x, y = _fuzz_set(rng, m)
+            ref = O.fit_grid(x, y, 0.2, 5, 0)
+            _eq(dm.fit_arrays(x, y, 0.2, 5, 0, handle=h), ref, f"fit_h m={m}")
+            expect += 1
+            assert h.spread_fallbacks() == expect
+            tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+            cl, fl, k = D.fit_tensors(tx, ty, 0.2, 5, 0, h)
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), k), ref, f"device m={m}")
+            expect += 1
+            cl = torch.full((m,), -9, dtype=torch.int32, device="cuda")
+            fl = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+            nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+            D.fit_tensors_async(tx, ty, 0.2, 5, 0, h, cl, fl, nk)
+            h.sync()
+            expect += 1
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), int(nk.item())), ref, f"async m={m}")
+            assert h.spread_fallbacks() == expect
+        # the default bound again: no re-runs
+        h.set_spread_spin_limit(1 << 21)
+        x, y = _fuzz_set(rng, 5000)
+        _eq(dm.fit_arrays(x, y, 0.2, 5, 0, handle=h), O.fit_grid(x, y, 0.2, 5, 0), "default")
+        assert h.spread_fallbacks() == expect
+    finally:
+        h.close()
