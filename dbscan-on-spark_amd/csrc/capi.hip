@@ -588,6 +588,88 @@ int64_t dbscan_route_slabs_device(dbscan_handle* h, const double* d_x, const dou
     return rc == DBSCAN_OK ? total : rc;
 }
 
+int64_t dbscan_slab_select_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                                  int64_t n, const double* cuts, int32_t n_cuts, int32_t rank,
+                                  double eps, double* d_sx, double* d_sy, uint8_t* d_szone,
+                                  int64_t* d_sgid, int64_t* d_sshared, int64_t capacity,
+                                  int64_t* n_shared_out) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    int64_t m = 0;
+    const int32_t rc = guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (n < 0 || n_cuts < 0 || n_cuts >= 64 || !n_shared_out || (n_cuts > 0 && !cuts) ||
+            (n > 0 && (!d_x || !d_y)) || capacity < 0 ||
+            (d_sx && (!d_sy || !d_szone || !d_sgid || !d_sshared)))
+            throw dbscan::ArgError{"bad slab selection arguments"};
+        if (!std::isfinite(eps * eps)) throw dbscan::ArgError{"eps*eps must be finite to shard"};
+        settle(h);
+        m = dbscan::select_slab(h->stream, h->ws.route, h->ws.scan, d_x, d_y, n, cuts, n_cuts,
+                                rank, eps, d_sx, d_sy, d_szone, d_sgid, d_sshared, capacity,
+                                n_shared_out);
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? m : rc;
+}
+
+int64_t dbscan_owned_rows_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                                 const int32_t* d_cluster, const uint8_t* d_flag, int64_t m,
+                                 int64_t* d_rows, int64_t capacity) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    int64_t k = 0;
+    const int32_t rc = guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (m < 0 || capacity < 0 || (m > 0 && (!d_zone || !d_gid || !d_cluster || !d_flag)))
+            throw dbscan::ArgError{"bad owned-rows arguments"};
+        settle(h);
+        k = dbscan::owned_rows(h->stream, h->ws.route, h->ws.scan, d_zone, d_gid, d_cluster,
+                               d_flag, m, d_rows, capacity);
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? k : rc;
+}
+
+int64_t dbscan_rows_unpack_device(dbscan_handle* h, const int64_t* d_rows, int64_t k,
+                                  double* d_sx, double* d_sy, uint8_t* d_szone, int64_t* d_sgid,
+                                  int64_t* d_sshared) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    int64_t ns = 0;
+    const int32_t rc = guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (k < 0 || (k > 0 && (!d_rows || !d_sx || !d_sy || !d_szone || !d_sgid || !d_sshared)))
+            throw dbscan::ArgError{"bad unpack arguments"};
+        settle(h);
+        ns = dbscan::unpack_rows(h->stream, h->ws.route, h->ws.scan, d_rows, k, d_sx, d_sy,
+                                 d_szone, d_sgid, d_sshared);
+        return DBSCAN_OK;
+    });
+    return rc == DBSCAN_OK ? ns : rc;
+}
+
+int32_t dbscan_label_scatter_device(dbscan_handle* h, const int64_t* d_rows, int64_t k,
+                                    int64_t start, int64_t m, int32_t* d_cluster,
+                                    uint8_t* d_flag) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    return guarded(h, [&]() -> int32_t {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (k < 0 || m < 0 || (k > 0 && (!d_rows || !d_cluster || !d_flag)))
+            throw dbscan::ArgError{"bad label scatter arguments"};
+        dbscan::label_scatter(h->stream, d_rows, k, start, m, d_cluster, d_flag);
+        return DBSCAN_OK;
+    });
+}
+
 }  // extern "C"
 
 namespace {

@@ -400,6 +400,19 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
                    int64_t* n_clusters_out, std::string* err);
 int32_t worker_selftest(int32_t* rcs, int32_t n);
+// Node-path slab selection, label rows and scatter (node.hip): see include/dbscan_hip.h.
+int64_t select_slab(hipStream_t s, DevBuf& scratch, ScanState& scan, const double* x,
+                    const double* y, int64_t n, const double* cuts, int32_t n_cuts, int32_t rank,
+                    double eps, double* sx, double* sy, uint8_t* sz, int64_t* sgid,
+                    int64_t* sshared, int64_t capacity, int64_t* ns_out);
+int64_t owned_rows(hipStream_t s, DevBuf& scratch, ScanState& scan, const uint8_t* zone,
+                   const int64_t* gid, const int32_t* cl, const uint8_t* fl, int64_t m,
+                   int64_t* rows, int64_t capacity);
+void label_scatter(hipStream_t s, const int64_t* rows, int64_t k, int64_t start, int64_t m,
+                   int32_t* cl, uint8_t* fl);
+int64_t unpack_rows(hipStream_t s, DevBuf& scratch, ScanState& scan, const int64_t* rows,
+                    int64_t k, double* sx, double* sy, uint8_t* sz, int64_t* sgid,
+                    int64_t* sshared);
 // Node-path routing (node.hip, dbscan_route_slabs_device): see include/dbscan_hip.h.
 int64_t route_slabs(hipStream_t s, DevBuf& scratch, DevBuf& tabbuf, const double* x,
                     const double* y, int64_t m, int64_t start, const double* cuts, int32_t n_cuts,

@@ -318,6 +318,132 @@ __global__ __launch_bounds__(kBlock) void plan_scatter_kernel(
 
 unsigned nblocks(int64_t m) { return (unsigned)std::max<int64_t>(1, (m + kBlock - 1) / kBlock); }
 
+// chunk_labels' rows (node.py): the zone-0 points of a slab, in slab order (ascending gid), as
+// (gid, cluster << 8 | flag) int64 pairs -- the same ordered compaction as the plan kernels.
+__global__ __launch_bounds__(kBlock) void owned_count_kernel(const uint8_t* __restrict__ zone,
+                                                             int64_t m,
+                                                             int32_t* __restrict__ cnt) {
+    __shared__ int ws[kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    int c = 0;
+    for (int k = 0; k < kPlanTile / kBlock; ++k) {
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        if (i >= m) break;
+        c += zone[i] == 0 ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (__lane_id() == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void owned_write_kernel(
+    const uint8_t* __restrict__ zone, const int64_t* __restrict__ gid,
+    const int32_t* __restrict__ cl, const uint8_t* __restrict__ fl, int64_t m,
+    const int32_t* __restrict__ off, int64_t* __restrict__ rows) {
+    __shared__ int wc[2][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int o = off[blockIdx.x];
+    for (int k = 0; k < kPlanTile / kBlock; ++k) {
+        if (base + k * kBlock >= m) break;  // (block-uniform)
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        const bool in = i < m && zone[i] == 0;
+        const uint64_t b = __ballot(in);
+        if (lane == 0) wc[k & 1][w] = __popcll(b);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+            before += v < w ? wc[k & 1][v] : 0;
+            total += wc[k & 1][v];
+        }
+        if (in) {
+            const int64_t q = (int64_t)o + before + __popcll(b & lt);
+            rows[2 * q] = gid[i];
+            rows[2 * q + 1] = ((int64_t)cl[i] << 8) | (int64_t)fl[i];
+        }
+        o += total;
+    }
+}
+
+// from_chunk's received rows (x bits, y bits, gid * 8 + zone * 2 + shared) into the slab's
+// columns, and the slab indices of its shared points (an ordered compaction: count, scan, write).
+__global__ __launch_bounds__(kBlock) void unpack_count_kernel(const int64_t* __restrict__ rows,
+                                                              int64_t k,
+                                                              int32_t* __restrict__ cnt) {
+    __shared__ int ws[kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    int c = 0;
+    for (int j = 0; j < kPlanTile / kBlock; ++j) {
+        const int64_t i = base + j * kBlock + threadIdx.x;
+        if (i >= k) break;
+        c += (int)(rows[3 * i + 2] & 1);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (__lane_id() == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void unpack_write_kernel(
+    const int64_t* __restrict__ rows, int64_t k, const int32_t* __restrict__ off,
+    double* __restrict__ sx, double* __restrict__ sy, uint8_t* __restrict__ sz,
+    int64_t* __restrict__ sgid, int64_t* __restrict__ sshared) {
+    __shared__ int wc[2][kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kPlanTile;
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int o = off[blockIdx.x];
+    for (int j = 0; j < kPlanTile / kBlock; ++j) {
+        if (base + j * kBlock >= k) break;  // (block-uniform)
+        const int64_t i = base + j * kBlock + threadIdx.x;
+        bool sh = false;
+        if (i < k) {
+            const int64_t a = rows[3 * i], b = rows[3 * i + 1], code = rows[3 * i + 2];
+            sx[i] = __longlong_as_double(a);
+            sy[i] = __longlong_as_double(b);
+            sz[i] = (uint8_t)((code >> 1) & 3);
+            sgid[i] = code >> 3;
+            sh = (code & 1) != 0;
+        }
+        const uint64_t bb = __ballot(sh);
+        if (lane == 0) wc[j & 1][w] = __popcll(bb);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int v = 0; v < kBlock / 64; ++v) {
+            before += v < w ? wc[j & 1][v] : 0;
+            total += wc[j & 1][v];
+        }
+        if (sh) sshared[o + before + __popcll(bb & lt)] = i;
+        o += total;
+    }
+}
+
+// chunk_labels' scatter: rows (gid, cluster << 8 | flag) received by the chunk's owner.
+__global__ __launch_bounds__(kBlock) void label_scatter_kernel(const int64_t* __restrict__ rows,
+                                                               int64_t k, int64_t start, int64_t m,
+                                                               int32_t* __restrict__ cl,
+                                                               uint8_t* __restrict__ fl) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= k) return;
+    const int64_t g = rows[2 * j] - start;
+    const int64_t v = rows[2 * j + 1];
+    if (g < 0 || g >= m) return;  // (never: every row was routed to its chunk's owner)
+    cl[g] = (int32_t)(v >> 8);
+    fl[g] = (uint8_t)(v & 255);
+}
+
 // ---- the node path's host-to-slab routing (node.py NodeJob.from_chunk) ------------------
 // Every point of a rank's input chunk goes to each slab whose zones 0/1/2 hold it, as a 24-B row
 // (x bits, y bits, gid * 8 + zone * 2 + shared), rows grouped by destination rank, ascending gid
@@ -511,6 +637,92 @@ int32_t worker_selftest(int32_t* rcs, int32_t n) {
     });
     for (int w = 0; w < n; ++w) rcs[w] = st[(size_t)w].rc;
     return DBSCAN_OK;
+}
+
+// NodeJob.from_global's slab selection on the device (the plan kernels of dbscan_train_node):
+// slab `rank`'s points (zones 0/1/2) in input order and the slab indices of its shared points.
+// Returns the slab's point count (ns_out: its shared points); writes when sx != nullptr and
+// capacity >= that count.  Synchronizes the stream.
+int64_t select_slab(hipStream_t s, DevBuf& scratch, ScanState& scan, const double* x,
+                    const double* y, int64_t n, const double* cuts, int32_t n_cuts, int32_t rank,
+                    double eps, double* sx, double* sy, uint8_t* sz, int64_t* sgid,
+                    int64_t* sshared, int64_t capacity, int64_t* ns_out) {
+    const int world = n_cuts + 1;
+    if (rank < 0 || rank >= world) throw ArgError{"slab select: rank out of range"};
+    if (n >= (int64_t)INT32_MAX) throw ArgError{"slab select: more than 2^31 - 1 points"};
+    *ns_out = 0;
+    if (n == 0) return 0;
+    const std::vector<double> cv(cuts, cuts + n_cuts);
+    const std::vector<ZoneCut> zc = zone_cuts(world, cv, reach(eps));
+    const int64_t nb = (n + kPlanTile - 1) / kPlanTile;
+    int32_t* cnt = static_cast<int32_t*>(scratch.ensure((4 * nb + 4) * sizeof(int32_t)));
+    int32_t *cs = cnt, *ch = cnt + nb, *os = cnt + 2 * nb, *oh = cnt + 3 * nb, *tot = cnt + 4 * nb;
+    hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, x, n, rank,
+                       world, zc[rank], cs, ch);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    exclusive_scan(s, 0, cs, os, nb, tot, scan);
+    exclusive_scan(s, 0, ch, oh, nb, tot + 1, scan);
+    int32_t t2[2];
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(t2, tot, sizeof(t2), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    *ns_out = t2[1];
+    if (!sx || capacity < t2[0]) return t2[0];
+    hipLaunchKernelGGL(plan_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, x, y, n, rank,
+                       world, zc[rank], os, oh, sx, sy, sz, sgid, sshared);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    return t2[0];
+}
+
+// chunk_labels' rows: the zone-0 points of a slab as (gid, cluster << 8 | flag), slab order.
+// Returns the row count; writes when rows != nullptr and capacity suffices.
+int64_t owned_rows(hipStream_t s, DevBuf& scratch, ScanState& scan, const uint8_t* zone,
+                   const int64_t* gid, const int32_t* cl, const uint8_t* fl, int64_t m,
+                   int64_t* rows, int64_t capacity) {
+    if (m == 0) return 0;
+    if (m >= (int64_t)INT32_MAX) throw ArgError{"owned rows: more than 2^31 - 1 points"};
+    const int64_t nb = (m + kPlanTile - 1) / kPlanTile;
+    int32_t* cnt = static_cast<int32_t*>(scratch.ensure((2 * nb + 2) * sizeof(int32_t)));
+    int32_t *cs = cnt, *os = cnt + nb, *tot = cnt + 2 * nb;
+    hipLaunchKernelGGL(owned_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, zone, m, cs);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    exclusive_scan(s, 0, cs, os, nb, tot, scan);
+    int32_t t = 0;
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(&t, tot, sizeof(t), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    if (!rows || capacity < t) return t;
+    hipLaunchKernelGGL(owned_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, zone, gid, cl,
+                       fl, m, os, rows);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    return t;
+}
+
+int64_t unpack_rows(hipStream_t s, DevBuf& scratch, ScanState& scan, const int64_t* rows,
+                    int64_t k, double* sx, double* sy, uint8_t* sz, int64_t* sgid,
+                    int64_t* sshared) {
+    if (k == 0) return 0;
+    if (k >= (int64_t)INT32_MAX) throw ArgError{"unpack rows: more than 2^31 - 1 rows"};
+    const int64_t nb = (k + kPlanTile - 1) / kPlanTile;
+    int32_t* cnt = static_cast<int32_t*>(scratch.ensure((2 * nb + 2) * sizeof(int32_t)));
+    int32_t *cs = cnt, *os = cnt + nb, *tot = cnt + 2 * nb;
+    hipLaunchKernelGGL(unpack_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, rows, k, cs);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    exclusive_scan(s, 0, cs, os, nb, tot, scan);
+    hipLaunchKernelGGL(unpack_write_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, rows, k, os,
+                       sx, sy, sz, sgid, sshared);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+    int32_t t = 0;
+    DBSCAN_HIP_CHECK(hipMemcpyAsync(&t, tot, sizeof(t), hipMemcpyDeviceToHost, s));
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    return t;
+}
+
+void label_scatter(hipStream_t s, const int64_t* rows, int64_t k, int64_t start, int64_t m,
+                   int32_t* cl, uint8_t* fl) {
+    if (k <= 0) return;
+    hipLaunchKernelGGL(label_scatter_kernel, dim3(nblocks(k)), dim3(kBlock), 0, s, rows, k, start,
+                       m, cl, fl);
+    DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
 // Routing of one chunk (see route_write_kernel): counts_out[d] = rows for rank d; rows written

@@ -74,6 +74,11 @@ SIGNATURES = [
     ("dbscan_duplicate", _i64, [_vp, _vp, _i64, _vp, _i64, _d, _vp, _vp, _i64]),
     ("dbscan_route_slabs_device", _i64, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _d, _vp, _i64,
                                          _vp]),
+    ("dbscan_slab_select_device", _i64, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _d, _vp, _vp,
+                                         _vp, _vp, _vp, _i64, _vp]),
+    ("dbscan_owned_rows_device", _i64, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64]),
+    ("dbscan_rows_unpack_device", _i64, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    ("dbscan_label_scatter_device", _i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
 ]
 SMALL_MAX_POINTS = 8192  # DBSCAN_SMALL_MAX_POINTS
 

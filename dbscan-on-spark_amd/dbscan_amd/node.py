@@ -286,6 +286,79 @@ class HipSlabOps:
         self._from_handle()
         return rows[:total], [int(v) for v in counts]
 
+    def select(self, x, y, cuts, rank, eps):
+        """from_global's slab (dbscan_slab_select_device): (x, y, zone, gid, shared slab
+        indices) of slab `rank`, in input order."""
+        import numpy as np
+
+        L = _lib.load()
+        n = x.numel()
+        c = np.ascontiguousarray(cuts, dtype=np.float64)
+        ns = ctypes.c_int64(0)
+        vp = ctypes.c_void_p
+        self._to_handle()
+        args = (self.h.ptr, _p(x), _p(y), n, c.ctypes.data_as(vp), len(cuts), int(rank),
+                float(eps))
+        m = L.dbscan_slab_select_device(*args, None, None, None, None, None, 0, ctypes.byref(ns))
+        if m < 0:
+            _lib.check(int(m))
+        dev = x.device
+        sx = torch.empty(max(1, m), dtype=torch.float64, device=dev)
+        sy = torch.empty_like(sx)
+        sz = torch.empty(max(1, m), dtype=torch.uint8, device=dev)
+        sg = torch.empty(max(1, m), dtype=torch.int64, device=dev)
+        sh = torch.empty(max(1, ns.value), dtype=torch.int64, device=dev)
+        got = L.dbscan_slab_select_device(*args, _p(sx), _p(sy), _p(sz), _p(sg), _p(sh), m,
+                                          ctypes.byref(ns))
+        if got < 0:
+            _lib.check(int(got))
+        self._from_handle()
+        return sx[:m], sy[:m], sz[:m], sg[:m], sh[:ns.value]
+
+    def unpack(self, rows):
+        """from_chunk's received rows -> (x, y, zone, gid, shared slab indices)
+        (dbscan_rows_unpack_device)."""
+        k = rows.shape[0]
+        dev = rows.device
+        rows = rows.contiguous()
+        sx = torch.empty(max(1, k), dtype=torch.float64, device=dev)
+        sy = torch.empty_like(sx)
+        sz = torch.empty(max(1, k), dtype=torch.uint8, device=dev)
+        sg = torch.empty(max(1, k), dtype=torch.int64, device=dev)
+        sh = torch.empty(max(1, k), dtype=torch.int64, device=dev)
+        self._to_handle()
+        ns = _lib.load().dbscan_rows_unpack_device(self.h.ptr, _p(rows), k, _p(sx), _p(sy),
+                                                   _p(sz), _p(sg), _p(sh))
+        if ns < 0:
+            _lib.check(int(ns))
+        self._from_handle()
+        return sx[:k], sy[:k], sz[:k], sg[:k], sh[:ns]
+
+    def owned_rows(self, zone, gid, cluster, flag):
+        """chunk_labels' rows (dbscan_owned_rows_device): (gid, cluster << 8 | flag) of the
+        zone-0 points, slab order (ascending gid)."""
+        m = zone.numel()
+        rows = torch.empty((max(1, m), 2), dtype=torch.int64, device=zone.device)
+        self._to_handle()
+        k = _lib.load().dbscan_owned_rows_device(self.h.ptr, _p(zone), _p(gid), _p(cluster),
+                                                 _p(flag), m, _p(rows), m)
+        if k < 0:
+            _lib.check(int(k))
+        self._from_handle()
+        return rows[:k]
+
+    def label_scatter(self, rows, start, m):
+        """The chunk owner's labels from the received rows (dbscan_label_scatter_device)."""
+        dev = rows.device
+        cl = torch.empty(m, dtype=torch.int32, device=dev)
+        fl = torch.empty(m, dtype=torch.uint8, device=dev)
+        rows = rows.contiguous()
+        self._to_handle()
+        _lib.check(_lib.load().dbscan_label_scatter_device(self.h.ptr, _p(rows), rows.shape[0],
+                                                           int(start), int(m), _p(cl), _p(fl)))
+        self._from_handle()
+        return cl, fl
+
     def fit_whole(self, x, y, eps, min_points, mode):
         """One rank, nothing to merge: the slab is the whole data set, so the node step is the
         direct fit (dbscan_fit_device_async) -- labels in slab order, the cluster count."""
@@ -361,7 +434,8 @@ class NodeJob:
     """One rank's share of a whole-node fit.  run() is one step (timed by bench.py)."""
 
     def __init__(self, x, y, zone, gid, shared, eps, min_points, mode, comm: Comm, ops,
-                 n_total: int, sh_idx=None):
+                 n_total: int, sh_idx=None, tick=None):
+        tick = tick or (lambda name: None)
         self.x, self.y, self.zone, self.gid, self.shared = x, y, zone, gid, shared
         self.eps, self.min_points, self.mode = float(eps), int(min_points), int(mode)
         self.comm, self.ops = comm, ops
@@ -373,19 +447,33 @@ class NodeJob:
         dev = x.device
         self.sh_idx = torch.nonzero(shared).flatten() if sh_idx is None else sh_idx
         a = gid[self.sh_idx]
+        tick("job: shared points")
         self.rec_sizes = comm.sizes(a.numel())
         self.all_a = comm.allgather_fixed(a, self.rec_sizes)
+        tick("job: a-side records all-gathered")
         self.parent = torch.full((max(1, int(n_total)),), -1, dtype=torch.int32, device=dev)
         self.gs_of_root = torch.zeros(max(1, x.numel()), dtype=torch.int64, device=dev)
+        tick("job: merge arrays")
 
     @classmethod
     def from_global(cls, x_all, y_all, eps, min_points, mode, comm: Comm, ops,
-                    cuts: Optional[List[float]] = None) -> "NodeJob":
+                    cuts: Optional[List[float]] = None, tick=None) -> "NodeJob":
         """Select this rank's slab (zones 0/1/2, global visit order kept) from the global
-        arrays.  Setup, not part of a step."""
+        arrays.  Setup, not part of a step.  tick(name): called after each phase (traces)."""
+        tick = tick or (lambda name: None)
         if cuts is None:
             cuts = make_cuts(x_all, comm.world, eps)
+        tick("cuts")
         assert len(cuts) == comm.world - 1 or (not cuts), "one slab per rank"
+        if (x_all.is_cuda and hasattr(ops, "select") and math.isfinite(eps * eps)
+                and (cuts or comm.world == 1)):
+            # the plan kernels (ordered compaction on the GPU): no torch pass per zone
+            sx, sy, sz, sg, sh_idx = ops.select(x_all, y_all, cuts, comm.rank, eps)
+            tick("zones + slab selection")
+            job = cls(sx, sy, sz, sg, None, eps, min_points, mode, comm, ops, x_all.numel(),
+                      sh_idx=sh_idx, tick=tick)
+            job.cuts = cuts
+            return job
         if not cuts and comm.world > 1:  # unshardable eps: everything on rank 0
             own = torch.full(x_all.shape, OUT, dtype=torch.uint8, device=x_all.device)
             if comm.rank == 0:
@@ -393,10 +481,12 @@ class NodeJob:
             z, sh = own, torch.zeros_like(own, dtype=torch.bool)
         else:
             z, sh = zones(x_all, comm.rank, cuts, eps)
+        tick("zones")
         idx = torch.nonzero(z != OUT).flatten()  # ascending: global visit order preserved
-        job = cls(x_all[idx].contiguous(), y_all[idx].contiguous(), z[idx].contiguous(),
-                  idx.to(torch.int64).contiguous(), sh[idx].contiguous(), eps, min_points, mode,
-                  comm, ops, x_all.numel())
+        sx, sy, sz = x_all[idx].contiguous(), y_all[idx].contiguous(), z[idx].contiguous()
+        sg, ss = idx.to(torch.int64).contiguous(), sh[idx].contiguous()
+        tick("slab selection")
+        job = cls(sx, sy, sz, sg, ss, eps, min_points, mode, comm, ops, x_all.numel(), tick=tick)
         job.cuts = cuts
         return job
 
@@ -407,13 +497,14 @@ class NodeJob:
 
     @classmethod
     def from_chunk(cls, x, y, start: int, n_total: int, eps, min_points, mode, comm: Comm, ops,
-                   sample: int = 1 << 20) -> "NodeJob":
+                   sample: int = 1 << 20, tick=None) -> "NodeJob":
         """Host-to-slab path: each rank holds only the contiguous chunk [start, start + len(x))
         of the global input (global visit order), e.g. just copied from host memory.  The cuts
         come from an all-gathered sample of every chunk; every point goes to the ranks whose
         zones 0/1/2 hold it in ONE all_to_all of 24-B records (x, y bits, gid/zone/shared),
         so a rank receives its slab in ascending gid (segments in source-rank order, each
         ascending): the same slab from_global selects, without any rank holding all points."""
+        tick = tick or (lambda name: None)
         world = comm.world
         m = x.numel()
         dev = x.device
@@ -424,22 +515,39 @@ class NodeJob:
                       ops, n_total, sh_idx=torch.zeros(0, dtype=torch.int64, device=dev))
             job.cuts = []
             return job
-        xf = x[torch.isfinite(x)]
-        per = max(1, sample // world)
-        smp = xf[::max(1, xf.numel() // per)][:per].contiguous()
-        allx = comm.allgather_varlen(smp)
-        cuts = make_cuts(allx, world, eps, sample=max(1, allx.numel()))
-        if x.is_cuda and cuts and hasattr(ops, "route"):
+        if world > 1:
+            # every rank's strided sample of its chunk (finite values), all-gathered: the same
+            # cuts on every rank
+            per = max(1, sample // world)
+            smp = x[::max(1, m // per)][:per]
+            smp = smp[torch.isfinite(smp)].contiguous()
+            allx = comm.allgather_varlen(smp)
+            cuts = make_cuts(allx, world, eps, sample=max(1, allx.numel()))
+        else:  # (one slab: no cuts whatever the sample)
+            cuts = []
+        tick("chunk: sample + cuts")
+        if x.is_cuda and hasattr(ops, "route") and (cuts or (world == 1 and math.isfinite(eps * eps))):
             # one kernel pass per direction: every destination's rows, grouped and ordered
             rows, counts = ops.route(x, y, start, cuts, eps)
         else:
             rows, counts = cls._route_torch(x, y, start, cuts, eps, world)
+        tick("chunk: route rows")
         recv = comm.alltoall_rows(rows, counts)
+        tick("chunk: all_to_all rows")
+        if recv.is_cuda and hasattr(ops, "unpack"):
+            sx, sy, sz, sg, sh_idx = ops.unpack(recv)
+            del recv
+            tick("chunk: columns")
+            job = cls(sx, sy, sz, sg, None, eps, min_points, mode, comm, ops, n_total,
+                      sh_idx=sh_idx, tick=tick)
+            job.cuts = cuts
+            return job
         code = recv[:, 2].contiguous()
-        job = cls(recv[:, 0].contiguous().view(torch.float64),
-                  recv[:, 1].contiguous().view(torch.float64),
-                  ((code >> 1) & 3).to(torch.uint8), code >> 3, (code & 1) != 0, eps,
-                  min_points, mode, comm, ops, n_total)
+        sx = recv[:, 0].contiguous().view(torch.float64)
+        sy = recv[:, 1].contiguous().view(torch.float64)
+        tick("chunk: columns")
+        job = cls(sx, sy, ((code >> 1) & 3).to(torch.uint8), code >> 3, (code & 1) != 0, eps,
+                  min_points, mode, comm, ops, n_total, tick=tick)
         job.cuts = cuts
         return job
 
@@ -464,37 +572,59 @@ class NodeJob:
             counts.append(int(idx.numel()))
         return torch.cat(recs), counts
 
-    def chunk_labels(self, start: int, m: int, bounds: List[int]):
+    def chunk_labels(self, start: int, m: int, bounds: List[int], tick=None):
         """The labels of the chunk [start, start + m) this rank holds, in input order: every
         rank sends its owned (gid, cluster, flag) to the chunk owner (one all_to_all), which
         scatters them into place.  Returns (cluster int32[m], flag uint8[m]) on the device."""
+        tick = tick or (lambda name: None)
         if self.comm._local():  # one rank: the slab is the chunk, in order, every point owned
             return self.cluster, self.flag
+        if self.zone.is_cuda and hasattr(self.ops, "owned_rows"):
+            # one ordered compaction (the slab is in ascending gid, so are the rows): the
+            # destination of every row is its chunk, the counts a search of the bounds
+            rec = self.ops.owned_rows(self.zone, self.gid, self.cluster, self.flag)
+            b = torch.tensor(bounds[1:-1], dtype=torch.int64, device=rec.device)
+            ends = torch.searchsorted(rec[:, 0].contiguous(), b).cpu().tolist()
+            counts = [e - s_ for s_, e in zip([0] + ends, ends + [rec.shape[0]])]
+            tick("labels: records")
+            recv = self.comm.alltoall_rows(rec, counts)
+            tick("labels: all_to_all")
+            out = self.ops.label_scatter(recv, start, m)
+            tick("labels: scatter")
+            return out
         gid, cl, fl = self.owned()
+        tick("labels: owned points")
         dev = gid.device
         b = torch.tensor(bounds[1:-1], dtype=torch.int64, device=dev)
         dest = torch.searchsorted(b, gid, right=True)
         counts = torch.bincount(dest, minlength=self.comm.world).cpu().tolist()
         rec = torch.stack([gid, (cl.to(torch.int64) << 8) | fl.to(torch.int64)], 1)
+        tick("labels: records")
         recv = self.comm.alltoall_rows(rec, counts)
+        tick("labels: all_to_all")
         loc = recv[:, 0] - start
         out_cl = torch.zeros(m, dtype=torch.int32, device=dev)
         out_fl = torch.zeros(m, dtype=torch.uint8, device=dev)
         out_cl[loc] = (recv[:, 1] >> 8).to(torch.int32)
         out_fl[loc] = (recv[:, 1] & 255).to(torch.uint8)
+        tick("labels: scatter")
         return out_cl, out_fl
 
     @classmethod
     def synthetic(cls, n_total, noise, dense, seed, eps, min_points, handle, dist,
-                  mode: int = 0, force: bool = False) -> "NodeJob":
+                  mode: int = 0, force: bool = False, tick=None) -> "NodeJob":
         """bench.py setup: every rank generates the same G(n_total) on its GPU (device
         generator), then keeps its slab.  force: Comm.force (collectives at one rank too)."""
         from . import device as D
 
+        tick = tick or (lambda name: None)
         x_all, y_all = D.generate_blobs(n_total, noise, dense, seed, handle)
+        tick("generate")
         comm = Comm(dist)
         comm.force = force
-        job = cls.from_global(x_all, y_all, eps, min_points, mode, comm, HipSlabOps(handle))
+        ops = HipSlabOps(handle)
+        tick("slab ops")
+        job = cls.from_global(x_all, y_all, eps, min_points, mode, comm, ops, tick=tick)
         del x_all, y_all
         torch.cuda.empty_cache()
         return job

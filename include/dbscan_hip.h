@@ -368,6 +368,38 @@ int64_t dbscan_route_slabs_device(dbscan_handle* h, const double* d_x, const dou
                                   double eps, int64_t* d_rows, int64_t capacity,
                                   int64_t* counts_out);
 
+/* NodeJob.from_global's slab selection (dbscan_amd/node.py; the slab plan of dbscan_train_node):
+ * of the n points (device arrays, global visit order), the ones in zone 0/1/2 of slab `rank`
+ * of the x-cuts (node.py zones()), in input order: x, y, zone and input index each, and the
+ * slab indices of its shared points (zone 0/1 of two slabs).  Returns the slab's point count m
+ * (< 0: error) and *n_shared_out; the outputs are written when d_sx is not NULL and capacity
+ * >= m (the shared array must hold *n_shared_out <= m entries).  Synchronizes the handle's
+ * stream. */
+int64_t dbscan_slab_select_device(dbscan_handle* h, const double* d_x, const double* d_y,
+                                  int64_t n, const double* cuts, int32_t n_cuts, int32_t rank,
+                                  double eps, double* d_sx, double* d_sy, uint8_t* d_szone,
+                                  int64_t* d_sgid, int64_t* d_sshared, int64_t capacity,
+                                  int64_t* n_shared_out);
+/* NodeJob.from_chunk's received rows (dbscan_route_slabs_device's layout) into the slab's
+ * columns: x, y, zone and gid of each of the k rows, and the row indices of the shared ones
+ * (d_sshared: capacity k), in row order.  Returns the shared count (< 0: error).
+ * Synchronizes the handle's stream. */
+int64_t dbscan_rows_unpack_device(dbscan_handle* h, const int64_t* d_rows, int64_t k,
+                                  double* d_sx, double* d_sy, uint8_t* d_szone, int64_t* d_sgid,
+                                  int64_t* d_sshared);
+/* NodeJob.chunk_labels' rows: the zone-0 points of a slab's m points in slab order (ascending
+ * gid) as int64 pairs (gid, cluster << 8 | flag).  Returns the row count (< 0: error); writes
+ * when d_rows is not NULL and capacity (pairs) suffices.  Synchronizes the handle's stream for
+ * the count; the rows are written asynchronously on it. */
+int64_t dbscan_owned_rows_device(dbscan_handle* h, const uint8_t* d_zone, const int64_t* d_gid,
+                                 const int32_t* d_cluster, const uint8_t* d_flag, int64_t m,
+                                 int64_t* d_rows, int64_t capacity);
+/* ... and the chunk owner's scatter of the k received pairs into its chunk [start, start + m):
+ * d_cluster[gid - start], d_flag[gid - start] (asynchronous on the handle's stream). */
+int32_t dbscan_label_scatter_device(dbscan_handle* h, const int64_t* d_rows, int64_t k,
+                                    int64_t start, int64_t m, int32_t* d_cluster,
+                                    uint8_t* d_flag);
+
 /* Device-side synthetic generator G(n, noise, dense, seed) of SURVEY.md §8d (32 isotropic
  * Gaussian blobs, splitmix64 + Box-Muller, uniform noise), then a seeded shuffle of the
  * visit order.  Writes d_x, d_y (device).  Used by bench.py so 10^7..10^9 points need no PCIe. */

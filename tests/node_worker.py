@@ -110,7 +110,10 @@ def run(rank, world, port, data_path, out_dir, eps, min_points, mode, use_gpu):
                                       comm, ops)
         k = job.run()
         cl, fl = job.chunk_labels(c0, c1 - c0, bounds)
-        k2 = job.run()
+        cl, fl = cl.clone(), fl.clone()
+        k2 = job.run()  # a second step: the same labels again
+        cl2, fl2 = job.chunk_labels(c0, c1 - c0, bounds)
+        assert torch.equal(cl, cl2) and torch.equal(fl, fl2), "second step's labels differ"
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), gid=np.arange(c0, c1),
                  cluster=cl.cpu().numpy(), flag=fl.cpu().numpy(), k=np.array([k, k2]),
                  n_slab=np.array([job.x.numel()]), cuts=np.array(job.cuts, dtype=np.float64))

@@ -147,12 +147,70 @@ def test_gpu_node_rccl_world1(tmp_path, chunks):
     assert ks == {rk}
 
 
-def test_gpu_node_single_rank(tmp_path):
+@pytest.mark.parametrize("chunks", [False, True], ids=["global", "chunks"])
+def test_gpu_node_single_rank(tmp_path, chunks):
+    """One rank, no forced collectives: the one-rank shortcuts (from_chunk's local form,
+    chunk_labels returning the slab's labels, run() as the direct fit) over two steps: the
+    labels of both steps and both cluster counts equal one oracle fit."""
     x, y = gen_blobs(300_000, noise=0.1, seed=77)
-    cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, 2.55, 10, 0, use_gpu=True)
+    cl, fl, seen, ks, _ = run_ranks(tmp_path, x, y, 1, 2.55, 10, 0, use_gpu=True, chunks=chunks)
+    assert np.all(seen == 1)
     rc, rf, rk = O.fit_grid(x, y, 2.55, 10, 0)
     np.testing.assert_array_equal(cl, rc)
     np.testing.assert_array_equal(fl, rf)
+    assert ks == {rk}
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_slab_select_kernel_equals_torch_zones(world):
+    """dbscan_slab_select_device (HipSlabOps.select, from_global's slab on the GPU) against the
+    torch restatement of node.py zones() + the ordered selection: the same x, y, zone, gid and
+    shared slab indices for every rank, NaN / inf points, points on the cuts and within ulps of
+    the halo margins, coinciding cuts (an empty slab)."""
+    import torch
+
+    import dbscan_amd
+    from dbscan_amd import node
+
+    rng = np.random.default_rng(world + 40)
+    n, eps = 300_000, 2.55
+    x, y = gen_blobs(n, noise=0.2, seed=world + 40)
+    xs = np.sort(x[np.isfinite(x)])
+    cuts = [float(np.floor(xs[k * xs.size // world] / (2 * eps)) * 2 * eps) for k in range(1, world)]
+    if world == 8:
+        cuts[3] = cuts[2]
+    R = node.reach(eps)
+    special = []
+    for c in cuts:
+        m1, m2 = node.margin1(c, R), node.margin2(c, R)
+        for v in (c, c - m1, c + m1, c - m2, c + m2):
+            special += [v, np.nextafter(v, -np.inf), np.nextafter(v, np.inf)]
+    k = len(special)
+    x[:k] = special
+    x[k:k + 5] = [np.nan, np.inf, -np.inf, np.nan, 0.0]
+    y[k + 5] = np.nan
+    p = rng.permutation(n)
+    x, y = x[p], y[p]
+    h = dbscan_amd.Handle(0)
+    ops = node.HipSlabOps(h)
+    try:
+        tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+        for rank in range(world):
+            sx, sy, sz, sg, sh = ops.select(tx, ty, cuts, rank, eps)
+            if cuts:
+                z, shm = node.zones(tx, rank, cuts, eps)
+            else:
+                z = torch.zeros(n, dtype=torch.uint8, device="cuda")
+                shm = torch.zeros(n, dtype=torch.bool, device="cuda")
+            idx = torch.nonzero(z != node.OUT).flatten()
+            assert torch.equal(sg, idx)
+            assert torch.equal(sz, z[idx])
+            assert torch.equal(sx.view(torch.int64), tx[idx].view(torch.int64))
+            assert torch.equal(sy.view(torch.int64), ty[idx].view(torch.int64))
+            assert torch.equal(sh, torch.nonzero(shm[idx]).flatten())
+    finally:
+        ops.close()
+        h.close()
 
 
 def test_gpu_merge_kernels_vs_double():
