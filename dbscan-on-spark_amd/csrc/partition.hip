@@ -242,7 +242,18 @@ bool best_split(const CellGrid& g, const Rect& box, double mrs, Rect* s1, Rect* 
     int64_t lens[2];
     for (int axis = 0; axis < 2; ++axis)
         lens[axis] = range_len((axis == 0 ? box.x : box.y) + mrs, axis == 0 ? box.x2 : box.y2, mrs);
-    const bool trie = lens[0] + lens[1] > 4;  // the candidate Set is a HashTrieSet
+    // the candidate Set (findPossibleSplits' toSet) is a HashTrieSet above 4 DISTINCT
+    // rectangles: a step below ulp(v) repeats a value (the x and y candidates never coincide)
+    const auto distinct = [&](int axis, int64_t cap) {
+        int64_t d = 0;
+        double v = (axis == 0 ? box.x : box.y) + mrs, prev = 0.0;
+        for (int64_t k = 0; k < lens[axis] && d < cap; ++k, v += mrs) {
+            if (k == 0 || v != prev) ++d;
+            prev = v;
+        }
+        return d;
+    };
+    const bool trie = lens[0] + lens[1] > 4 && distinct(0, 5) + distinct(1, 5) > 4;
     uint32_t best_rank = 0;
     for (int axis = 0; axis < 2; ++axis) {
         const double start = (axis == 0 ? box.x : box.y) + mrs;

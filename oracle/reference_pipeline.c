@@ -131,8 +131,17 @@ static int split_rect(const grid_t* g, rect_t box, double mrs, rect_t* s1, rect_
     for (int axis = 0; axis < 2; ++axis)
         cnts[axis] = range_count((axis == 0 ? box.x : box.y) + mrs, axis == 0 ? box.x2 : box.y2,
                                  mrs);
-    /* more than 4 candidates: a HashTrieSet, ties go to the smaller trie rank */
-    const int hashed = cnts[0] + cnts[1] > 4;
+    /* more than 4 distinct candidates (a step below ulp(v) repeats a value; the x and y
+     * candidates never coincide): a HashTrieSet, ties go to the smaller trie rank */
+    int64_t dist[2] = {0, 0};
+    for (int axis = 0; axis < 2 && cnts[0] + cnts[1] > 4; ++axis) {
+        double v = (axis == 0 ? box.x : box.y) + mrs, prev = 0.0;
+        for (int64_t k = 0; k < cnts[axis] && dist[axis] < 5; ++k, v += mrs) {
+            if (k == 0 || v != prev) ++dist[axis];
+            prev = v;
+        }
+    }
+    const int hashed = dist[0] + dist[1] > 4;
     int have_key = 0;
     uint32_t best_key = 0;
     for (int axis = 0; axis < 2; ++axis) {
