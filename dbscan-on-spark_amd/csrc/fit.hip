@@ -368,8 +368,16 @@ __device__ __forceinline__ void heads16(const uint32_t* __restrict__ key, int64_
 __global__ __launch_bounds__(kBlock) void heads_reduce_kernel(const uint32_t* __restrict__ key,
                                                               const int32_t* __restrict__ nf_p,
                                                               int nb,
-                                                              int32_t* __restrict__ partial) {
+                                                              int32_t* __restrict__ partial,
+                                                              const GridParams* __restrict__ gp,
+                                                              int32_t* __restrict__ tmap) {
     __shared__ int wsum[3][kBlock / 64];
+    {  // tmap = -1 over the whole tile grid (tmap_kernel fills it after this launch)
+        const int64_t nt = (int64_t)gp->ntx * gp->nty;
+        for (int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x; u < nt;
+             u += (int64_t)gridDim.x * kBlock)
+            tmap[u] = -1;
+    }
     const int64_t nf = *nf_p;
     const int64_t p0 = (int64_t)blockIdx.x * kHeadTile + (int64_t)threadIdx.x * kHeadPer;
     uint32_t k[kHeadPer], mc, mq, mt;
@@ -3225,8 +3233,65 @@ __device__ bool make_grid(const double* bb, double eps, GridParams* g) {
 // One thread: the grid from the bbox of the finite points (bb = xmin, xmax, ymin, ymax, count),
 // the finite count nf, the radix key width and a sizing error flag.  No finite point: nf = 0
 // and a 1x1 dummy grid (every slot is outside the grid).
-__global__ void grid_kernel(const double* __restrict__ bb, double eps, GridParams* __restrict__ gp,
-                            int32_t* __restrict__ st) {
+// bbox_finite's final reduction of the per-block partials + grid_kernel + the fit state's
+// zeroing, in one single-workgroup launch (three launches before)
+__device__ __forceinline__ double bg_wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double bg_wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ void grid_state(const double* bb, double eps, GridParams* __restrict__ gp,
+                           int32_t* __restrict__ st);
+
+__global__ __launch_bounds__(kBlock) void bbox_grid_kernel(const double* __restrict__ partial,
+                                                           int nb, double* __restrict__ bb,
+                                                           double eps, GridParams* __restrict__ gp,
+                                                           int32_t* __restrict__ st) {
+    __shared__ double sm[kBlock / 64][5];
+    if (threadIdx.x < kStCount) st[threadIdx.x] = 0;
+    double r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY, r4 = 0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        r0 = fmin(r0, partial[b * 5 + 0]);
+        r1 = fmax(r1, partial[b * 5 + 1]);
+        r2 = fmin(r2, partial[b * 5 + 2]);
+        r3 = fmax(r3, partial[b * 5 + 3]);
+        r4 += partial[b * 5 + 4];
+    }
+    r0 = bg_wave_min(r0);
+    r1 = bg_wave_max(r1);
+    r2 = bg_wave_min(r2);
+    r3 = bg_wave_max(r3);
+    for (int o = 32; o > 0; o >>= 1) r4 += __shfl_xor(r4, o, 64);
+    const int w = threadIdx.x >> 6;
+    if (__lane_id() == 0) {
+        sm[w][0] = r0;
+        sm[w][1] = r1;
+        sm[w][2] = r2;
+        sm[w][3] = r3;
+        sm[w][4] = r4;
+    }
+    __syncthreads();  // (st zeroed by this workgroup before thread 0 writes it below)
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kBlock / 64; ++k) {
+            sm[0][0] = fmin(sm[0][0], sm[k][0]);
+            sm[0][1] = fmax(sm[0][1], sm[k][1]);
+            sm[0][2] = fmin(sm[0][2], sm[k][2]);
+            sm[0][3] = fmax(sm[0][3], sm[k][3]);
+            sm[0][4] += sm[k][4];
+        }
+        double v[5];
+        for (int c = 0; c < 5; ++c) v[c] = bb[c] = sm[0][c];
+        grid_state(v, eps, gp, st);
+    }
+}
+
+__device__ void grid_state(const double* bb, double eps, GridParams* __restrict__ gp,
+                           int32_t* __restrict__ st) {
     GridParams g{0, 0, 1, 1, 1, 1, 1, 1, 0};
     const int nf = (int)bb[4];
     int bits = 0;
@@ -3260,14 +3325,6 @@ __global__ void grid_fixed_kernel(int32_t nf, GridParams* __restrict__ gp,
     st[kStBits] = 0;
 }
 
-// tmap = -1 over the whole tile grid (ntx * nty is only known on the device).
-__global__ __launch_bounds__(kBlock) void tmap_clear_kernel(const GridParams* __restrict__ gp,
-                                                            int32_t* __restrict__ tmap) {
-    const int64_t nt = (int64_t)gp->ntx * gp->nty;
-    for (int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x; u < nt;
-         u += (int64_t)gridDim.x * kBlock)
-        tmap[u] = -1;
-}
 
 // The cluster count of a fit into caller memory (asynchronous API).
 __global__ void nclusters_kernel(const int32_t* __restrict__ st, int32_t* __restrict__ out) {
@@ -3429,7 +3486,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         ws.fit_mirrored = true;
         return;
     }
-    DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
+    if (mode != kGridEps || a.batch)  // (eps grids of direct fits: bbox_grid_kernel zeroes it)
+        DBSCAN_HIP_CHECK(hipMemsetAsync(st, 0, kStCount * sizeof(int32_t), s));
 
     // large direct fits sort through the padded bands (bucket_sort: cache-resident random writes)
     const bool bucketed = !a.batch && mode == kGridEps && n >= kBucketMinPoints &&
@@ -3446,8 +3504,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             DBSCAN_HIP_CHECK(hipGetLastError());
         } else {
             StageTimer t(prof, s, "bbox");
-            bbox_finite(s, a.x, a.y, n, misc, ws.scan_tmp);
-            klaunch(prof, "grid", grid_kernel, dim3(1), dim3(1), 0, s, misc, a.eps, gp, st);
+            double* partial = nullptr;
+            const int nbb = bbox_partials(s, a.x, a.y, n, ws.scan_tmp, &partial);
+            // (the fit state zeroed here as well: no fill ahead of this path)
+            klaunch(prof, "grid", bbox_grid_kernel, dim3(1), dim3(kBlock), 0, s,
+                    (const double*)partial, nbb, misc, a.eps, gp, st);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         if (!bucketed) {  // (bucketed: the MSD pass bins x, y itself)
@@ -3568,11 +3629,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 static_cast<int32_t*>(ws.heads.ensure(6 * (size_t)nb * sizeof(int32_t)));
             int32_t* offs = part + 3 * nb;
             klaunch(prof, "heads_reduce", heads_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
-                               part);
+                    part, (const GridParams*)gp, tmap);
             DBSCAN_HIP_CHECK(hipGetLastError());
-            exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan);
-            exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan);
-            exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
+            if (nb <= 4096) {  // (n <= 2^24: the three head counts in one launch)
+                scan3(s, part, nb, nb, offs, &st[kStCells], &st[kStQuarters], &st[kStTiles]);
+            } else {
+                exclusive_scan(s, 0, part, offs, nb, &st[kStCells], ws.scan);
+                exclusive_scan(s, 0, part + nb, offs + nb, nb, &st[kStQuarters], ws.scan);
+                exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
+            }
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
                     offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
             DBSCAN_HIP_CHECK(hipGetLastError());
@@ -3582,7 +3647,6 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         }
         {
             StageTimer t(prof, s, "tables");
-            klaunch(prof, "tmap_clear", tmap_clear_kernel, dim3(1024), dim3(kBlock), 0, s, gp, tmap);
             const unsigned tgrid = (unsigned)std::min<int64_t>(nblk(ntile_bound), 1024);
             klaunch(prof, "tmap", tmap_kernel, dim3(tgrid), dim3(kBlock), 0, s, tkey,
                                &st[kStTiles], tmap);

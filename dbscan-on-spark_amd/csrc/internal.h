@@ -490,8 +490,13 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                  Profiler* prof, const uint8_t* zone = nullptr, const uint8_t* shm = nullptr,
                  const GridParams* gp = nullptr);
 
-// Min/max over finite (x, y) and the finite count: out = {xmin, xmax, ymin, ymax, count}.
-void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
-                 DevBuf& tmp);
+// Per-block partials of the bbox (xmin, xmax, ymin, ymax, count of finite points; 5 doubles
+// per block) for fit.hip's bbox_grid_kernel; returns the block count.
+int bbox_partials(hipStream_t s, const double* x, const double* y, int64_t n, DevBuf& tmp,
+                  double** partial_out);
+// Three independent exclusive scans of n <= 4096 int32 values each (arrays at in + b * stride,
+// results at out + b * stride, totals t0..t2) in one launch.
+void scan3(hipStream_t s, const int32_t* in, int64_t n, int64_t stride, int32_t* out,
+           int32_t* t0, int32_t* t1, int32_t* t2);
 
 }  // namespace dbscan

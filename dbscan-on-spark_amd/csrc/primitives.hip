@@ -7,7 +7,8 @@
 //                      with 64-bit wave ballots (match-any over the 8 digit bits) against
 //                      per-wave running digit counters, sorts the tile in LDS and writes
 //                      each digit run contiguously (coalesced) to its global offset
-//   bbox_finite        min/max of finite coordinates + finite count (grid sizing)
+//   bbox_partials      per-block min/max of finite coordinates + finite counts (grid sizing;
+//                      the final reduction is fit.hip bbox_grid_kernel)
 #include "internal.h"
 
 #include <cmath>
@@ -93,13 +94,12 @@ __device__ __forceinline__ uint64_t scan_status(uint32_t epoch, uint64_t flag, i
 __device__ __forceinline__ int lds_slot(int e) { return e + (e >> 4); }  // e = r*256 + tid
 
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void scan_kernel(const void* in, int64_t n, int32_t* out,
-                                                      int32_t* total, uint64_t* state,
-                                                      uint32_t epoch, int64_t ntiles) {
+__device__ __forceinline__ void scan_body(int t, const void* in, int64_t n, int32_t* out,
+                                          int32_t* total, uint64_t* state, uint32_t epoch,
+                                          int64_t ntiles) {
     __shared__ int wtot[kWaves], wstop[kWaves], wsum[kWaves];
     __shared__ int buf[kBlock * kRow];
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const int t = blockIdx.x;
     const int64_t base = (int64_t)t * kTile;
     int v[kItems];
 #pragma unroll
@@ -176,6 +176,24 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(const void* in, int64_t n,
         const int64_t i = base + r * kBlock + tid;
         if (i < n) out[i] = buf[lds_slot(r * kBlock + tid)];
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void scan_kernel(const void* in, int64_t n, int32_t* out,
+                                                      int32_t* total, uint64_t* state,
+                                                      uint32_t epoch, int64_t ntiles) {
+    scan_body<MODE>(blockIdx.x, in, n, out, total, state, epoch, ntiles);
+}
+
+// Three independent int32 scans of <= kTile elements each in ONE launch, one workgroup each:
+// array b is in[b * stride, b * stride + n), its total to totals[b].
+struct Totals3 {
+    int32_t* t[3];
+};
+__global__ __launch_bounds__(kBlock) void scan3_kernel(const int32_t* in, int64_t n,
+                                                       int64_t stride, int32_t* out, Totals3 tt) {
+    const int b = blockIdx.x;
+    scan_body<0>(0, in + b * stride, n, out + b * stride, tt.t[b], nullptr, 0, 1);
 }
 
 template <int MODE>
@@ -595,9 +613,8 @@ __global__ __launch_bounds__(256) void bucket_table_kernel(const int32_t* __rest
 // Blocks 0..255: the pads after segment d's keys (< 2048 each); blocks 256.. share the tail after
 // the last segment (up to 256 tiles of 2048 keys: one block alone took ~29 us of every fit).
 constexpr int kPadTailBlocks = 64;
-__global__ __launch_bounds__(kBlock) void bucket_pad_kernel(const int32_t* __restrict__ seg,
-                                                            int64_t np_max,
-                                                            uint32_t* __restrict__ key) {
+__device__ __forceinline__ void bucket_pad_body(const int32_t* __restrict__ seg, int64_t np_max,
+                                                uint32_t* __restrict__ key) {
     const int d = blockIdx.x < 256 ? (int)blockIdx.x : 256;
     const int64_t a = (int64_t)seg[kSegPBase + d] + seg[kSegCnt + d];
     const int64_t b = d < 256 ? (int64_t)seg[kSegPBase + d + 1] : np_max;
@@ -607,10 +624,8 @@ __global__ __launch_bounds__(kBlock) void bucket_pad_kernel(const int32_t* __res
 }
 
 // Per padded tile: (padded base - dense base of its segment, end of its real keys).
-__global__ __launch_bounds__(kBlock) void bucket_tseg_kernel(const int32_t* __restrict__ seg,
-                                                             int64_t ntiles,
-                                                             int2* __restrict__ tseg) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__device__ __forceinline__ void bucket_tseg_body(const int32_t* __restrict__ seg, int64_t t,
+                                                 int64_t ntiles, int2* __restrict__ tseg) {
     if (t >= ntiles) return;
     int lo = 0, hi = 257;  // segment s with seg[s] <= t < seg[s + 1] (tail: s = 256)
     while (hi - lo > 1) {
@@ -619,6 +634,20 @@ __global__ __launch_bounds__(kBlock) void bucket_tseg_kernel(const int32_t* __re
     }
     tseg[t] = make_int2(seg[kSegPBase + lo] - seg[kSegDBase + lo],
                         seg[kSegPBase + lo] + seg[kSegCnt + lo]);
+}
+
+// bucket_pad's blocks, then the tile table's (one launch: both read the segment table only)
+__global__ __launch_bounds__(kBlock) void bucket_pad_tseg_kernel(const int32_t* __restrict__ seg,
+                                                                 int64_t np_max,
+                                                                 uint32_t* __restrict__ key,
+                                                                 int64_t ntiles,
+                                                                 int2* __restrict__ tseg) {
+    if (blockIdx.x < 256 + kPadTailBlocks) {
+        bucket_pad_body(seg, np_max, key);
+        return;
+    }
+    bucket_tseg_body(seg, (int64_t)(blockIdx.x - 256 - kPadTailBlocks) * kBlock + threadIdx.x,
+                     ntiles, tseg);
 }
 
 // Per-segment digit offsets for an LSD pass over the padded array: one workgroup per segment
@@ -939,43 +968,6 @@ __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __re
     }
 }
 
-__global__ __launch_bounds__(kBlock) void bbox_final_kernel(const double* partial, int nb,
-                                                            double* out) {
-    __shared__ double sm[kWaves][5];
-    double r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY, r4 = 0;
-    for (int b = threadIdx.x; b < nb; b += kBlock) {
-        r0 = fmin(r0, partial[b * 5 + 0]);
-        r1 = fmax(r1, partial[b * 5 + 1]);
-        r2 = fmin(r2, partial[b * 5 + 2]);
-        r3 = fmax(r3, partial[b * 5 + 3]);
-        r4 += partial[b * 5 + 4];
-    }
-    r0 = wave_min(r0);
-    r1 = wave_max(r1);
-    r2 = wave_min(r2);
-    r3 = wave_max(r3);
-    for (int o = 32; o > 0; o >>= 1) r4 += __shfl_xor(r4, o, 64);
-    const int w = threadIdx.x >> 6;
-    if (lane_id() == 0) {
-        sm[w][0] = r0;
-        sm[w][1] = r1;
-        sm[w][2] = r2;
-        sm[w][3] = r3;
-        sm[w][4] = r4;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < kWaves; ++k) {
-            sm[0][0] = fmin(sm[0][0], sm[k][0]);
-            sm[0][1] = fmax(sm[0][1], sm[k][1]);
-            sm[0][2] = fmin(sm[0][2], sm[k][2]);
-            sm[0][3] = fmax(sm[0][3], sm[k][3]);
-            sm[0][4] += sm[k][4];
-        }
-        for (int c = 0; c < 5; ++c) out[c] = sm[0][c];
-    }
-}
-
 }  // namespace
 
 uint64_t* ScanState::prepare(hipStream_t s, int64_t ntiles) {
@@ -1100,16 +1092,16 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                 -1);
         klaunch(prof, "bucket_table", bucket_table_kernel, dim3(1), dim3(256), 0, s,
                 (const int32_t*)ho, n, np, bits_dev, seg, pshift);
-        klaunch(prof, "bucket_pad", bucket_pad_kernel, dim3(256 + kPadTailBlocks), dim3(kBlock), 0, s,
-                (const int32_t*)seg, np, ka);
+        klaunch(prof, "bucket_pad", bucket_pad_tseg_kernel,
+                dim3((unsigned)(256 + kPadTailBlocks + (ntp + kBlock - 1) / kBlock)), dim3(kBlock),
+                0, s, (const int32_t*)seg, np, ka, ntp, tseg);
+
         const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr, gp};
         klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
                 dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, (int32_t*)nullptr,
                 (uint32_t*)nullptr,
                 (int32_t*)nullptr, n, 0, bits_dev, (const int32_t*)ho, ex);
-        klaunch(prof, "bucket_tseg", bucket_tseg_kernel,
-                dim3((unsigned)((ntp + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                (const int32_t*)seg, ntp, tseg);
+
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
     // LSD passes over the low bits inside the segments (payload: padded place)
@@ -1146,16 +1138,25 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     pass(std::integral_constant<int, 8>{}, 18);
 }
 
-void bbox_finite(hipStream_t s, const double* x, const double* y, int64_t n, double* out_dev,
-                 DevBuf& tmp) {
+int bbox_partials(hipStream_t s, const double* x, const double* y, int64_t n, DevBuf& tmp,
+                  double** partial_out) {
     int nb = (int)((n + kBlock - 1) / kBlock);
     if (nb > 1024) nb = 1024;
     if (nb < 1) nb = 1;
     double* partial = static_cast<double*>(tmp.ensure((size_t)nb * 5 * sizeof(double)));
     hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, s, x, y, n, partial);
     DBSCAN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(kBlock), 0, s, partial, nb, out_dev);
+    *partial_out = partial;
+    return nb;
+}
+
+void scan3(hipStream_t s, const int32_t* in, int64_t n, int64_t stride, int32_t* out,
+           int32_t* t0, int32_t* t1, int32_t* t2) {
+    if (n <= 0 || n > kTile) throw ArgError{"scan3: each array must hold 1..4096 values"};
+    hipLaunchKernelGGL(scan3_kernel, dim3(3), dim3(kBlock), 0, s, in, n, stride, out,
+                       Totals3{{t0, t1, t2}});
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
+
 
 }  // namespace dbscan
