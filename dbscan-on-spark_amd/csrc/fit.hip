@@ -312,8 +312,9 @@ constexpr int kHeadTile = 4096;
 // 0.208 -> 0.193 ms (r12).  The count kernels stay round-robin: their class lists put the dense
 // tiles together, and contiguous ranges unbalanced the XCDs (count32 0.32 -> 0.42 ms).  A
 // bijection of 0..gridDim.x-1 for any grid size.
-__device__ __forceinline__ int xcd_block() {
-    const int G = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ int xcd_block(int G = -1) {  // G: the first G blocks of the grid
+    if (G < 0) G = gridDim.x;
+    const int b = blockIdx.x;
     const int x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
     return x * q + (x < r ? x : r) + j;
 }
@@ -409,8 +410,15 @@ __global__ __launch_bounds__(kBlock) void heads_down_kernel(
     const int32_t* __restrict__ offs,
     int32_t* __restrict__ cell, uint32_t* __restrict__ ckey, int32_t* __restrict__ cstart,
     int32_t* __restrict__ qidx, uint32_t* __restrict__ qkey, int32_t* __restrict__ qstart,
-    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart) {
+    uint32_t* __restrict__ tkey, int32_t* __restrict__ tstart, uint64_t* __restrict__ zero_words,
+    int64_t nzw) {
     __shared__ int wcnt[2][3][kBlock / 64];
+    // the root bits of direct fits (quarter_root / final set them), one 64-bit word per 64 of
+    // this block's kHeadTile slots: zeroed here instead of by a fill launch
+    if (zero_words && threadIdx.x < kHeadTile / 64) {
+        const int64_t wd = (int64_t)blockIdx.x * (kHeadTile / 64) + threadIdx.x;
+        if (wd < nzw) zero_words[wd] = 0ull;
+    }
     const int64_t nf = *nf_p;
     const int64_t base = (int64_t)blockIdx.x * kHeadTile;
     const int w = threadIdx.x >> 6, lane = __lane_id();
@@ -1387,6 +1395,30 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
 // the all-pairs grid): staged tiles count from LDS, the rest from global stencil pieces; every
 // point is its own parent for union_kernel.  Clique grids exit at once: the fp32 count kernels
 // (count_tile32 / count_wave / big_count) count them.
+// slots [nf, n) (outside the grid: never core unless minPoints <= 0), block b of nb
+__device__ __forceinline__ void count_rest_body(int b, int nb, const int32_t* __restrict__ nf_p,
+                                                int64_t n, int32_t min_points,
+                                                uint8_t* __restrict__ core,
+                                                int32_t* __restrict__ parent,
+                                                int32_t* __restrict__ block_cores) {
+    __shared__ int rcores[kBlock / 64];
+    int mine = 0;
+    for (int64_t p = *nf_p + (int64_t)b * kBlock + threadIdx.x; p < n; p += (int64_t)nb * kBlock) {
+        const bool is_core = min_points <= 0;
+        parent[p] = (int32_t)p;
+        core[p] = is_core ? 1 : 0;
+        mine += is_core ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (__lane_id() == 0) rcores[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += rcores[w];
+        block_cores[b] = tot;
+    }
+}
+
 template <int CAP, int MINW>
 __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
@@ -1394,7 +1426,14 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const int2* __restrict__ tstage, const int32_t* __restrict__ ntiles_p, double eps2,
     int32_t min_points, uint8_t* __restrict__ core, int32_t* __restrict__ parent,
     int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr, int nbr_k,
-    const GridParams* __restrict__ gp) {
+    const GridParams* __restrict__ gp, int ntile_blocks, const int32_t* __restrict__ nf_p,
+    int64_t n, int32_t* __restrict__ rest_cores) {
+    // blocks from ntile_blocks: count_rest's job (the slots outside the grid) in this launch
+    if ((int)blockIdx.x >= ntile_blocks) {
+        count_rest_body((int)blockIdx.x - ntile_blocks, (int)gridDim.x - ntile_blocks, nf_p, n,
+                        min_points, core, parent, rest_cores);
+        return;
+    }
     __shared__ TileStage st;
     __shared__ double2 buf[CAP];
     __shared__ int wcores[kBlock / 64];
@@ -1408,9 +1447,9 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile_kernel(
     const int ntiles = *ntiles_p;
     int mine = 0;
     StageMeta meta = stage_meta(blockIdx.x, ntiles, tstage, tstart);
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (int t = blockIdx.x; t < ntiles; t += ntile_blocks) {
         const bool staged = stage_build<CAP>(meta, xy, st, buf);
-        meta = stage_meta(t + gridDim.x, ntiles, tstage, tstart);  // in flight during the scans
+        meta = stage_meta(t + ntile_blocks, ntiles, tstage, tstart);  // in flight during the scans
         if (staged) {
             if (threadIdx.x == 0) {  // own points per row of the tile: prefix over rows
                 int acc = 0;
@@ -2391,23 +2430,7 @@ __global__ __launch_bounds__(kBlock) void count_rest_kernel(const int32_t* __res
                                                             uint8_t* __restrict__ core,
                                                             int32_t* __restrict__ parent,
                                                             int32_t* __restrict__ block_cores) {
-    __shared__ int wcores[kBlock / 64];
-    int mine = 0;
-    for (int64_t p = *nf_p + (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n;
-         p += (int64_t)gridDim.x * kBlock) {
-        const bool is_core = min_points <= 0;
-        parent[p] = (int32_t)p;
-        core[p] = is_core ? 1 : 0;
-        mine += is_core ? 1 : 0;
-    }
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if (__lane_id() == 0) wcores[threadIdx.x >> 6] = mine;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
-        block_cores[blockIdx.x] = tot;
-    }
+    count_rest_body(blockIdx.x, gridDim.x, nf_p, n, min_points, core, parent, block_cores);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2480,19 +2503,17 @@ __device__ int uf_unite_roots(int* par, const int32_t* __restrict__ prio, int ra
 
 // Per-point union (used when quarter cells are not cliques: grown grid, all-pairs mode).
 // Each core-core edge once: from the endpoint with the larger slot.
-__global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict__ xy,
-                                                       const int32_t* __restrict__ cell,
-                                                       const Seg* __restrict__ seg,
-                                                       const int32_t* __restrict__ nf_p,
-                                                       const GridParams* __restrict__ gp,
-                                                       double eps2,
-                                                       const int32_t* __restrict__ perm,
-                                                       const uint8_t* __restrict__ core,
-                                                       int32_t* __restrict__ parent) {
+__device__ __forceinline__ void union_body(int b, int nb, const double2* __restrict__ xy,
+                                           const int32_t* __restrict__ cell,
+                                           const Seg* __restrict__ seg,
+                                           const int32_t* __restrict__ nf_p,
+                                           const GridParams* __restrict__ gp, double eps2,
+                                           const int32_t* __restrict__ perm,
+                                           const uint8_t* __restrict__ core,
+                                           int32_t* __restrict__ parent) {
     if (gp->clique) return;  // quarter-cell unions instead (a small grid: exits at once)
     const int64_t nf = *nf_p;
-    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < nf;
-         p += (int64_t)gridDim.x * kBlock) {
+    for (int64_t p = (int64_t)b * kBlock + threadIdx.x; p < nf; p += (int64_t)nb * kBlock) {
         if (!core[p]) continue;
         const double2 me = xy[p];
         const Seg s = load_seg(seg, cell[p]);
@@ -2507,6 +2528,18 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
             return true;
         });
     }
+}
+
+__global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict__ xy,
+                                                       const int32_t* __restrict__ cell,
+                                                       const Seg* __restrict__ seg,
+                                                       const int32_t* __restrict__ nf_p,
+                                                       const GridParams* __restrict__ gp,
+                                                       double eps2,
+                                                       const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ core,
+                                                       int32_t* __restrict__ parent) {
+    union_body(blockIdx.x, gridDim.x, xy, cell, seg, nf_p, gp, eps2, perm, core, parent);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2551,7 +2584,16 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const int4* __restrict__ qinfo, const int4* __restrict__ qg,
     const int32_t* __restrict__ qcomp, double eps2, const int32_t* __restrict__ perm,
     const uint8_t* __restrict__ core, int32_t* __restrict__ parent,
-    const GridParams* __restrict__ gp, const uint8_t* __restrict__ tcore) {
+    const GridParams* __restrict__ gp, const uint8_t* __restrict__ tcore, int edge_blocks,
+    const int32_t* __restrict__ cell, const Seg* __restrict__ seg,
+    const int32_t* __restrict__ nf_p) {
+    // blocks from edge_blocks: union_kernel's job in this launch (the per-point union of grids
+    // whose quarters are not cliques; the edge blocks then exit, and vice versa)
+    if ((int)blockIdx.x >= edge_blocks) {
+        union_body((int)blockIdx.x - edge_blocks, (int)gridDim.x - edge_blocks, xy, cell, seg,
+                   nf_p, gp, eps2, perm, core, parent);
+        return;
+    }
     if (!gp->clique) return;
     __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
     __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
@@ -2564,8 +2606,8 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
     // one (tile, side) per wave and loop trip: waves never wait for each other
-    for (int tw = xcd_block() * (kBlock / 64) + w; tw < 2 * ntiles;
-         tw += gridDim.x * (kBlock / 64)) {
+    for (int tw = xcd_block(edge_blocks) * (kBlock / 64) + w; tw < 2 * ntiles;
+         tw += edge_blocks * (kBlock / 64)) {
         const int t = tw >> 1, side = tw & 1;
         int nA = 0, ntot = 0;
         {
@@ -3544,6 +3586,11 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
     ws.perm_sorted = perm;
     ws.key_sorted = key;
+    // direct fits: the root bits (quarter_root / final), zeroed by heads_down on eps grids
+    uint64_t* root_words =
+        (!a.zone && mode != kGridNoPairs)
+            ? static_cast<uint64_t*>(ws.is_root.ensure(((n + 63) / 64) * sizeof(uint64_t)))
+            : nullptr;
 
     // Sizes: every nf-sized table is allocated for n; the tile grid holds <= 2^23 tiles.
     const int64_t ntile_bound = std::min<int64_t>(n, kMaxGridTiles);
@@ -3639,7 +3686,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 exclusive_scan(s, 0, part + 2 * nb, offs + 2 * nb, nb, &st[kStTiles], ws.scan);
             }
             klaunch(prof, "heads_down", heads_down_kernel, dim3(nb), dim3(kBlock), 0, s, key, nf_p, nb,
-                    offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart);
+                    offs, cell, ckey, cstart, qidx, qkey, qstart, tkey, tstart, root_words,
+                    root_words ? (n + 63) / 64 : (int64_t)0);
             DBSCAN_HIP_CHECK(hipGetLastError());
             if (tpart)
                 klaunch(prof, "tile_part", tile_part_kernel, dim3(nblk(ntile_bound)),
@@ -3688,10 +3736,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
     // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
-        ws.blockcnt.ensure(2 * ((size_t)6 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
+        ws.blockcnt.ensure(2 * ((size_t)5 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
+    const int64_t nmain = (f32 ? 5 : 1) * (int64_t)tile_grid;
+    bool rest_done = false;  // count_rest's blocks ran inside the fp64 count launch
     {
         StageTimer t(prof, s, "count");
         if (mode != kGridNoPairs) {
@@ -3715,7 +3765,6 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                                           kSmallBuckets - kTinyBucket0>,
                         dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
                         a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
-                DBSCAN_HIP_CHECK(hipMemsetAsync(bc + 2 * tile_grid, 0, tile_grid * sizeof(int32_t), s));
                 klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
                         dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
                         a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
@@ -3726,20 +3775,24 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 // it a second serial turn)
                 klaunch(prof, "big_union", big_union_kernel, dim3(tile_grid), dim3(kBlock), 0, s, xy,
                         (const uint8_t*)core, eps2, parent, fa);
-                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid), dim3(kBlock),
-                        0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2, a.min_points,
-                        core, parent, block_cores + 2 * tile_grid, nbr, nbr_k, (const GridParams*)gp);
+                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid + rest_grid),
+                        dim3(kBlock), 0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2,
+                        a.min_points, core, parent, block_cores + 2 * tile_grid, nbr, nbr_k,
+                        (const GridParams*)gp, (int)tile_grid, nf_p, n, block_cores + nmain);
+                rest_done = true;
             } else {
-                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid), dim3(kBlock),
-                        0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2, a.min_points,
-                        core, parent, block_cores, nbr, nbr_k, (const GridParams*)gp);
+                klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid + rest_grid),
+                        dim3(kBlock), 0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2,
+                        a.min_points, core, parent, block_cores, nbr, nbr_k, (const GridParams*)gp,
+                        (int)tile_grid, nf_p, n, block_cores + nmain);
+                rest_done = true;
             }
         } else {
             DBSCAN_HIP_CHECK(hipMemsetAsync(block_cores, 0, tile_grid * sizeof(int32_t), s));
         }
-        const int64_t nmain = (f32 ? 6 : 1) * (int64_t)tile_grid;
-        klaunch(prof, "count_rest", count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s, nf_p, n,
-                           a.min_points, core, parent, block_cores + nmain);
+        if (!rest_done)
+            klaunch(prof, "count_rest", count_rest_kernel, dim3(rest_grid), dim3(kBlock), 0, s,
+                    nf_p, n, a.min_points, core, parent, block_cores + nmain);
         DBSCAN_HIP_CHECK(hipGetLastError());
         const int64_t nb = nmain + rest_grid;
         exclusive_scan(s, 0, block_cores, block_cores + nb + 1, nb, &st[kStCore], ws.scan);
@@ -3758,21 +3811,23 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (fuse) {  // quarter-cell unions across tiles (no-ops unless the grid made them cliques)
         {
             StageTimer t(prof, s, "union_edge");
-            klaunch(prof, "edge_union", edge_union_kernel<6>, dim3(tile_grid), dim3(kBlock), 0, s, xy,
-                    &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
-                    (const uint8_t*)tcore);
+            // (+ union_kernel's blocks: a no-op on clique grids, the only union on the others)
+            const unsigned ug = std::min(nblk(n), 2048u);
+            klaunch(prof, "edge_union", edge_union_kernel<6>, dim3(tile_grid + ug), dim3(kBlock), 0,
+                    s, xy, &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
+                    (const uint8_t*)tcore, (int)tile_grid, cell, seg, nf_p);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
         // direct fits (fused quarter unions): the roots' visit indices per quarter (into the
         // dead qcomp) and the root flags, for final_kernel
-        if (qlab_bits) DBSCAN_HIP_CHECK(hipMemsetAsync(qlab_bits, 0, ((n + 63) / 64) * sizeof(uint64_t), s));
+        // (qlab_bits: zeroed by heads_down)
         klaunch(prof, "quarter_root", quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
                 &st[kStQuarters], gp, parent, perm, qlab_bits ? qcomp : (int32_t*)nullptr,
                 reinterpret_cast<unsigned long long*>(qlab_bits));
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
-    if (mode != kGridNoPairs) {  // per-point union (a no-op when the quarter path ran)
+    if (mode != kGridNoPairs && !fuse) {  // per-point union (fuse: inside the edge_union launch)
         StageTimer t(prof, s, "union");
         if (box) {
             klaunch(prof, "box_union", box_union_kernel, dim3(std::min(nblk(n), 4096u)),
@@ -3790,7 +3845,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         int32_t* word_rank = static_cast<int32_t*>(ws.rank.ensure(nw * sizeof(int32_t)));
         {
             StageTimer t(prof, s, "final");
-            if (!qlab_bits) DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
+            if (!root_words)  // (eps grids: zeroed by heads_down)
+                DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
             klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
                                reinterpret_cast<unsigned long long*>(root_bits), (int32_t*)nullptr,
