@@ -623,10 +623,10 @@ def seam(args, h, threads):
                  arrays, PCIe included) and dbscan_fit_device (device-resident, synchronous),
                  median of repeated calls, and capi_us: the dbscan_fit_device call alone as a JNI
                  caller makes it (no torch stream sync); the plain columns are the LDS kernels
-                 (small.hip) up to 8192 points, 'tiled' is the same call through the tiled
-                 pipeline (dbscan_set_small_max 0); a handle's default routes single fits of
-                 <= DBSCAN_SMALL_DEFAULT_POINTS (8192) points to the LDS kernels, from
-                 DBSCAN_SPREAD_DEFAULT_POINTS (512) the multi-workgroup form
+                 (small.hip): up to 8192 points the whole partition in each workgroup, from
+                 DBSCAN_SPREAD_DEFAULT_POINTS (512) over several workgroups, above 8192 (to
+                 DBSCAN_BAND_DEFAULT_POINTS, 65536) the band form; 'tiled' is the same call
+                 through the tiled pipeline (dbscan_set_small_max 0)
       train      G(10^7) (config 2) cut by the reference's EvenSplitPartitioner with
                  maxPointsPerPartition 8192 and duplicated into eps-grown partitions
                  (DBSCAN.scala:105-137): every partition fitted (a) by one dbscan_fit_h call each
@@ -661,8 +661,6 @@ def seam(args, h, threads):
                      ctypes.c_void_p(dfl.data_ptr()), ctypes.byref(kk))
         torch.cuda.synchronize()
         for tag, small in (("", 8192), ("tiled_", 0)):
-            if small == 0 and m > 8192:
-                continue
             h.set_small_max(small)
             reps = 30 if m <= 8192 else 10
             for kind in ("host", "device", "capi"):

@@ -186,6 +186,7 @@ struct dbscan_handle {
     hipEvent_t bcopied = nullptr;     // the last batch tables' upload (pinned buffer reusable)
     int64_t small_max = DBSCAN_SMALL_DEFAULT_POINTS;  // one-workgroup fits up to this many points
     int64_t spread_min = DBSCAN_SPREAD_DEFAULT_POINTS;  // LDS fits from here: several workgroups
+    int64_t band_max = DBSCAN_BAND_DEFAULT_POINTS;      // band fits above the LDS capacity
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     int32_t* pending_nk = nullptr;    // ... and the device word its cluster count went to
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
@@ -396,6 +397,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
                           nullptr, nullptr};
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
+        a.band_max = h->band_max;
         h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
@@ -433,6 +435,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
                           nullptr, nullptr};
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
+        a.band_max = h->band_max;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
@@ -480,6 +483,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
                               reinterpret_cast<uint8_t*>(dout + 4 * (size_t)n), nullptr, nullptr};
             a.small_max = h->small_max;
             a.spread_min = h->spread_min;
+        a.band_max = h->band_max;
             h->prepared = false;
             dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
             DBSCAN_HIP_CHECK(
@@ -515,6 +519,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         dbscan::FitArgs a{dx, dy, nullptr, n, eps, min_points, mode, dcl, dfl, nullptr, nullptr};
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
+        a.band_max = h->band_max;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         {
@@ -1069,6 +1074,17 @@ int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points) {
     std::lock_guard<std::mutex> lk(h->mu);
     const int64_t prev = h->spread_min;
     h->spread_min = std::max<int64_t>(min_points, 0);
+    return prev;
+}
+
+int64_t dbscan_set_band_max(dbscan_handle* h, int64_t max_points) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int64_t prev = h->band_max;
+    h->band_max = std::max<int64_t>(0, std::min<int64_t>(max_points, DBSCAN_BAND_MAX_POINTS));
     return prev;
 }
 

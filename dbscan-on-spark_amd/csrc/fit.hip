@@ -3494,6 +3494,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (slab) slab->valid = false;
     ws.fit_mirrored = false;
     ws.spread_recall.valid = false;
+    ws.recall_band = false;
     const int64_t n = a.n;
     const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
     const int mode =
@@ -3525,6 +3526,16 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         else
             enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
                                a.mode, a.cluster, a.flag, nullptr, gp, st, mirror);
+        ws.fit_mirrored = true;
+        return;
+    }
+    // partitions above the LDS capacity (the seam's dense rectangles): one launch over bands
+    if (!a.zone && !a.batch && a.small_max >= kSmallMaxPoints && n <= a.band_max &&
+        band_fit_eligible(n, a.eps, a.mode, a.min_points)) {
+        StageTimer t(prof, s, "band_fit");
+        double* mirror = stats_mirror(ws);
+        enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
+                         a.flag, gp, st, mirror);
         ws.fit_mirrored = true;
         return;
     }

@@ -176,7 +176,7 @@ struct Workspace {
         is_root, rank, misc, qidx, qkey, qstart, qrep, qmask, blockcnt, heads, tkey, tstart, tmap,
         tslot, qcomp, nbr, tq, tnb, tstage, inv, packed, slab_lor, own_flag, bigt, zs, tclass, tsz,
         key3, perm3, lroots, box_edges, box_map, tcore, tpart, pbox, ptab, shm, route, route_tab,
-        spread;
+        spread, band;
     bool spread_ready = false;  // spread.p holds zeroed barrier words (small.hip)
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
     double* stats_dev = nullptr;   // ... its device address (LDS fits write it directly)
@@ -196,6 +196,8 @@ struct Workspace {
         int32_t* st = nullptr;
         double* mirror = nullptr;
     } spread_recall;
+    bool recall_band = false;               // ... and it was a band fit (band_fit_kernel)
+    bool band_ready = false;                // band.p holds zeroed barrier words (small.hip)
     uint32_t spread_spin_limit = 1u << 21;  // barrier polls before giving up (0: at once; tests)
     int64_t spread_fallbacks = 0;           // spread fits re-run by the one-workgroup kernel
     bool spread_recovered = false;          // the last read_fit_stats re-ran the fit
@@ -218,9 +220,10 @@ struct Workspace {
                           &qcomp, &nbr, &tq, &tnb, &tstage, &inv, &packed, &slab_lor,
                           &own_flag, &bigt, &zs, &tclass, &tsz, &key3, &perm3, &lroots,
                           &box_edges, &box_map, &tcore, &tpart, &pbox, &ptab, &shm, &route,
-                          &route_tab, &spread})
+                          &route_tab, &spread, &band})
             b->release();
         spread_ready = false;
+        band_ready = false;
         if (stats_host) (void)hipHostFree(stats_host);
         stats_host = nullptr;
         stats_dev = nullptr;
@@ -308,6 +311,9 @@ struct FitArgs {
     int64_t small_max = 0;  // (0: the tiled pipeline; entry points opt in from the handle)
     // ... of which fits of >= spread_min points spread over several workgroups of one launch
     int64_t spread_min = INT64_MAX;
+    // ... and, when small_max covers the LDS capacity, fits up to band_max points run the band
+    // form (small.hip band_fit_kernel)
+    int64_t band_max = 0;
     // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
     const BatchFit* batch = nullptr;
 };
@@ -449,6 +455,16 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
                         const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
                         double* mirror = nullptr);
+// Partitions of kSmallMaxPoints < n <= kBandMaxPoints in ONE launch, each of G workgroups
+// staging a band of cell rows (small.hip band_fit_kernel); statistics into st / gp / mirror as
+// the spread fit, st[kStError] = 2 (barrier gave up) or 3 (a band over the staging capacity):
+// read_fit_stats then re-runs the fit through the tiled pipeline.
+constexpr int64_t kBandMaxPoints = 65536;
+bool band_fit_eligible(int64_t n, double eps, int32_t mode, int32_t min_points);
+void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
+                      const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
+                      int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
+                      double* mirror = nullptr);
 // After the stream has drained: the last fit was a spread fit whose grid barrier gave up ->
 // re-run it through the one-workgroup kernel (synchronously), count it, return true.
 bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws);

@@ -387,8 +387,10 @@ __device__ __forceinline__ SmCtx sm_ctx(const SmLds& L, const double* px, const 
     return {px, py, eps2, L.G.lo, L.G.hi, L.G.nx, L.G.ny, L.G.exact_only != 0};
 }
 
-// neighbour test of slots p (record me) and q (record rq)
-__device__ __forceinline__ bool sm_pair(const SmLds& L, const SmCtx& c, int p, float2 me, int q,
+// neighbour test of slots p (record me) and q (record rq).  (The stencil helpers take the LDS
+// layout as a template: SmLds, the whole partition; BandLds, one band of it.)
+template <class LT>
+__device__ __forceinline__ bool sm_pair(const LT& L, const SmCtx& c, int p, float2 me, int q,
                                         float2 rq) {
     if (!c.exact_only) {
         const float F = sm_d2(me, rq);
@@ -405,8 +407,8 @@ __device__ __forceinline__ bool sm_pair(const SmLds& L, const SmCtx& c, int p, f
 // a time (their LDS reads in flight together: the walks are bound by the latency of dependent
 // LDS reads, not by their count).  only = 0..2: that row alone (row-split phases), -1: all three.
 constexpr int kSmBatch = 4;
-template <class F>
-__device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_, int p, int qmin,
+template <class LT, class F>
+__device__ __forceinline__ void sm_for_stencil(const LT& L, const SmCtx& cx_, int p, int qmin,
                                                F&& f, int only) {
     const int nx = cx_.nx, ny = cx_.ny;
     const int c = (int)(L.info[p] & kCellMask);
@@ -438,7 +440,8 @@ __device__ __forceinline__ void sm_for_stencil(const SmLds& L, const SmCtx& cx_,
 }
 
 // |N(p)| capped at minPoints over stencil row `only` (-1: all rows; LocalDBSCANNaive.scala:52-56)
-__device__ __forceinline__ int sm_count(const SmLds& L, const SmCtx& c, int p, int min_points,
+template <class LT>
+__device__ __forceinline__ int sm_count(const LT& L, const SmCtx& c, int p, int min_points,
                                         int only) {
     const float2 me = L.rec[p];
     int cnt = 0;
@@ -456,7 +459,8 @@ __device__ __forceinline__ int sm_count(const SmLds& L, const SmCtx& c, int p, i
 // are chained (each to the next core of its quarter), and a pair p < q within eps makes p unite
 // with some core of q's quarter.  So a dense cell costs a few unions per point instead of one
 // per neighbour.  reach_k: record -> cell-local coordinate offsets (clique grids).
-__device__ __forceinline__ void sm_union_walk(SmLds& L, const SmCtx& cx_, int p, int only,
+template <class LT>
+__device__ __forceinline__ void sm_union_walk(LT& L, const SmCtx& cx_, int p, int only,
                                               bool quarters, double reach_kx, double reach_ky) {
     const int nx = cx_.nx, ny = cx_.ny;
     const float2 me = L.rec[p];
@@ -851,7 +855,8 @@ __device__ __forceinline__ void sm_unite_v(int* par, int a, int b) {
 
 // The wave-cooperative walks of the spread form: p is the same in every lane of the wave.
 // |N(p)| capped at minPoints: 64 candidates of a stencil row per step, hits by ballot.
-__device__ __forceinline__ int sp_count_wave(const SmLds& L, const SmCtx& c, int p,
+template <class LT>
+__device__ __forceinline__ int sp_count_wave(const LT& L, const SmCtx& c, int p,
                                              int min_points) {
     const int lane = (int)(threadIdx.x & 63);
     const float2 me = L.rec[p];
@@ -1124,6 +1129,560 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Partitions above the one-workgroup capacity (kSmallMaxPoints < m <= kBandMaxPoints: a dense
+// region's rectangle plus its eps halo, DBSCAN.scala:116-137) in ONE launch (band_fit_kernel):
+// the tiled pipeline's ~45 kernel boundaries cost ~5 us each on the GPU whatever enqueues them.
+// G workgroups (one per CU by their LDS), each owning a BAND of cell rows holding ~m/G points
+// and staging only that band plus one cell row on either side (the 3x3 stencil of an owned
+// point never leaves the staged rows):
+//   stage   every workgroup reads all m points: the bbox and the grid (cells of side >= eps,
+//           grown only while the grid is too large for the band tables), the points per cell
+//           row, the bands (row ranges at count quantiles, alike in every workgroup); then its
+//           staged rows' points, counting-sorted by cell in LDS (fp32 records as small.hip)
+//   count   its own points, one wave each (sp_count_wave); core flags by input index
+//   -- grid barrier 1 --
+//   union   the staged slots' core flags; its own cores' stencil walks (sm_union_walk) into an
+//           LDS forest over the staged slots; every non-root staged core published as
+//           (input index, its root's input index).  An edge between two bands is walked by the
+//           lower band's workgroup (the upper row is its halo) -- every closed-form edge by the
+//           owner of the smaller cell, as in spread_fit_kernel
+//   -- grid barrier 2 --
+//   merge   the published pairs united in a union-find over input indices in global memory
+//           (larger index hooked under the smaller: a root IS s(K))
+//   -- grid barrier 3 --
+//   roots   each own core's root (its s(K)) by input index; roots flagged
+//   -- grid barrier 4 --
+//   label   root flags -> popcount ranks (cluster id = 1 + roots before s(K)); own cores their
+//           root's id, own non-cores the min s(K) over their staged core neighbours + the Naive /
+//           Archery rule; the non-finite points noise (the last workgroup)
+// Same results bit for bit as every other form (the GPU tests compare them with the oracle).
+// A band over the staging capacity (a row too dense, or too many sparse rows), or a barrier
+// that gives up, flags st[kStError] (3 / 2): the host then re-runs the fit through the tiled
+// pipeline in the same call.
+constexpr int kBandT = 1024;
+constexpr int kBandCap = 7168;    // staged points per workgroup (and staged cells)
+constexpr int kBandCells = kBandCap;
+constexpr int kBandMaxWG = 64;
+constexpr int kBandWords = (int)(kBandMaxPoints / 32);
+static_assert(kBandMaxPoints <= 65536, "16-bit visit indices");
+static_assert(kBandCells <= 8191, "13-bit cells in info");
+
+struct BandLds {
+    float2 rec[kBandCap];
+    uint32_t info[kBandCap];  // visit << 16 | quadrant << 13 | staged cell; first: cell counts
+    int par[kBandCap];        // row counts, then sort cursors, then the LDS union-find
+    uint8_t core[kBandCap];
+    uint16_t cst[kBandCells + 2];
+    uint32_t rbits[kBandWords];
+    int wrank[kBandWords];
+    double red[5][kBandT / 64];
+    int wsc[kBandT / 64 + 1];
+    int meta[16];
+    SmGrid G;
+};
+
+struct BandArgs {
+    uint8_t* core;    // [m] core flags by input index
+    int32_t* lab;     // [m] own cores: the root's input index
+    int32_t* par;     // [m] union-find over input indices
+    uint32_t* rbits;  // [m/32 + 1] roots by input index
+    uint32_t* pairs;  // [G][kBandCap] published (input index << 16 | root input index)
+    int32_t* npairs;  // [G]
+    int32_t* cnt;     // [2] cores, occupied cells
+    uint32_t* bar;    // [2] arrivals, departures (zero between launches)
+};
+
+// The band grid (one thread): sides as sm_make_grid, doubled along the axis over its share of
+// the limits until nx <= kBandCells / 3 and ny < kBandCap (row counts live in par) and the
+// whole grid holds <= 24 * kBandCells cells: with kBandMaxWG bands of ~1/G of the cost below
+// (points + cells) each band fits its tables with room for its halo rows
+__device__ void band_make_grid(double xmin, double xmax, double ymin, double ymax, int nf,
+                               double eps, double eps2, SmGrid* g) {
+    g->nf = nf;
+    g->bad = 0;
+    g->exact_only = 0;
+    g->nx = g->ny = g->ncells = 1;
+    g->clique = 0;
+    if (nf == 0) return;
+    double R = fabs(eps) * (1.0 + 0x1p-40);
+    if (R < 0x1p-500) R = 0x1p-500;
+    const double h0 = R * (1.0 + 0x1p-16);
+    double hx = h0, hy = h0;
+    auto cells = [](double vmax, double vmin, double h) {
+        return floor((vmax * 0.5 - vmin * 0.5) * (2.0 / h)) + 1.0;
+    };
+    // (ny + 1 row counts live in par[kBandCap])
+    constexpr double kNx = kBandCells / 3, kNy = kBandCap - 1, kAll = 24.0 * kBandCells;
+    bool ok = false;
+    double cx = 1, cy = 1;
+    for (int it = 0; it < 4096; ++it) {
+        cx = cells(xmax, xmin, hx);
+        cy = cells(ymax, ymin, hy);
+        if (cx <= kNx && cy <= kNy && cx * cy <= kAll) {
+            ok = true;
+            break;
+        }
+        if (cx / kNx >= cy / kNy) hx *= 2.0; else hy *= 2.0;
+    }
+    if (!ok) {
+        g->bad = 1;
+        return;
+    }
+    g->nx = (int)cx;
+    g->ny = (int)cy;
+    g->clique = (hx == h0 && hy == h0 && h0 <= fabs(eps) * (1.0 + 0x1p-14)) ? 1 : 0;
+    g->ncells = g->nx * g->ny;
+    g->xmin2 = xmin * 0.5;
+    g->ymin2 = ymin * 0.5;
+    g->invx = 2.0 / hx;
+    g->invy = 2.0 / hy;
+    g->cx2 = xmin * 0.5 + (xmax * 0.5 - xmin * 0.5) * 0.5;
+    g->cy2 = ymin * 0.5 + (ymax * 0.5 - ymin * 0.5) * 0.5;
+    g->invs = 2.0 / h0;
+    const double rr = fmax((xmax * 0.5 - xmin * 0.5), (ymax * 0.5 - ymin * 0.5)) * g->invs * 0.5 +
+                      1.0;
+    const double e2 = eps2 * (0.5 * g->invs) * (0.5 * g->invs);
+    if (!(rr <= 0x1p20) || !(e2 <= 0x1p20)) {
+        g->exact_only = 1;
+        g->lo = 0.f;
+        g->hi = 0.f;
+        return;
+    }
+    const double M = (rr + 4.0) * 0x1p-20 + e2 * 0x1p-20;
+    g->lo = __double2float_rd(e2 - M);
+    g->hi = __double2float_ru(e2 + M);
+}
+
+// Global union-find over input indices (the merge): agent-scope loads, CAS hooks of the larger
+// root under the smaller
+__device__ __forceinline__ int bd_find(int32_t* par, int x) {
+    while (true) {
+        const int p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p == x) return x;
+        x = p;
+    }
+}
+__device__ __forceinline__ void bd_unite(int32_t* par, int a, int b) {
+    while (true) {
+        a = bd_find(par, a);
+        b = bd_find(par, b);
+        if (a == b) return;
+        if (a < b) {
+            const int t = a;
+            a = b;
+            b = t;
+        }
+        int expected = a;
+        if (__hip_atomic_compare_exchange_strong(par + a, &expected, b, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+    }
+}
+
+// f(i, x[i], y[i]) for every point i of the partition, kBandU per thread per step with all
+// their loads in flight together (each workgroup reads the whole partition four times)
+constexpr int kBandU = 8;
+template <class F>
+__device__ __forceinline__ void band_pass(const double* __restrict__ x,
+                                          const double* __restrict__ y, int m, F&& f) {
+    for (int i0 = threadIdx.x; i0 < m; i0 += kBandT * kBandU) {
+        double a[kBandU], b[kBandU];
+#pragma unroll
+        for (int u = 0; u < kBandU; ++u) {
+            const int i = i0 + u * kBandT;
+            a[u] = i < m ? x[i] : 0.0;
+            b[u] = i < m ? y[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kBandU; ++u)
+            if (i0 + u * kBandT < m) f(i0 + u * kBandT, a[u], b[u]);
+    }
+}
+
+__global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
+    const double* __restrict__ x, const double* __restrict__ y, int m, double eps, double eps2,
+    int min_points, int mode, int32_t* __restrict__ cluster, uint8_t* __restrict__ flag,
+    GridParams* __restrict__ gp, int32_t* st, double* mirror, BandArgs ba, uint32_t spin_limit) {
+    __shared__ BandLds L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int g = blockIdx.x, G = gridDim.x;
+    constexpr int kW = kBandT / 64;
+    SM_STAMP(0);
+    // (the fit state: kStError is cleared by the host before the launch, see spread_fit_kernel)
+    if (g == 0 && tid != kStError) sm_zero_stats(st, mirror, tid);
+    if (g == 0 && tid < 2) ba.cnt[tid] = 0;  // (added to after barrier 1 only)
+
+    // ---- bbox and grid (every workgroup alike) ----
+    {
+        double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, nfin = 0;
+        band_pass(x, y, m, [&](int, double a, double b) {
+            if (isfinite(a) && isfinite(b)) {
+                mnx = fmin(mnx, a);
+                mxx = fmax(mxx, a);
+                mny = fmin(mny, b);
+                mxy = fmax(mxy, b);
+                nfin += 1;
+            }
+        });
+        const int w = tid >> 6;
+        mnx = wave_min(mnx);
+        mxx = wave_max(mxx);
+        mny = wave_min(mny);
+        mxy = wave_max(mxy);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nfin += __shfl_xor(nfin, o, 64);
+        if (lane == 0) {
+            L.red[0][w] = mnx;
+            L.red[1][w] = mxx;
+            L.red[2][w] = mny;
+            L.red[3][w] = mxy;
+            L.red[4][w] = nfin;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 1; k < kW; ++k) {
+                L.red[0][0] = fmin(L.red[0][0], L.red[0][k]);
+                L.red[1][0] = fmax(L.red[1][0], L.red[1][k]);
+                L.red[2][0] = fmin(L.red[2][0], L.red[2][k]);
+                L.red[3][0] = fmax(L.red[3][0], L.red[3][k]);
+                L.red[4][0] += L.red[4][k];
+            }
+            band_make_grid(L.red[0][0], L.red[1][0], L.red[2][0], L.red[3][0], (int)L.red[4][0],
+                           eps, eps2, &L.G);
+        }
+        __syncthreads();
+    }
+    SM_STAMP(1);
+    const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny;
+    // the cell of a finite point (quarter bits << 13 above the cell is the caller's)
+    const auto cell_of = [&](double a, double b, int& row, int& col, int& quad) {
+        int qx = (int)floor(2.0 * ((a * 0.5 - L.G.xmin2) * L.G.invx));
+        int qy = (int)floor(2.0 * ((b * 0.5 - L.G.ymin2) * L.G.invy));
+        qx = min(max(qx, 0), 2 * nx - 1);
+        qy = min(max(qy, 0), 2 * ny - 1);
+        row = qy >> 1;
+        col = qx >> 1;
+        quad = ((qy & 1) << 1) | (qx & 1);
+    };
+    bool bad = L.G.bad != 0;  // (unreachable for finite bboxes)
+
+    // ---- the bands: points per row, their prefix, this workgroup's rows ----
+    int ra = 0, rb = 0, sa = 0, sb = 0, own0 = 0, own1 = 0;
+    if (!bad && nf > 0) {
+        for (int r = tid; r <= ny; r += kBandT) L.par[r] = 0;
+        __syncthreads();
+        band_pass(x, y, m, [&](int, double a, double b) {
+            if (isfinite(a) && isfinite(b)) {
+                int row, col, quad;
+                cell_of(a, b, row, col, quad);
+                atomicAdd(&L.par[row], 1);
+            }
+        });
+        __syncthreads();
+        {  // exclusive prefix over the rows: par[r] = points in rows < r, par[ny] = nf
+            constexpr int kRowsPer = (kBandCap + kBandT - 1) / kBandT;
+            int v[kRowsPer], sum = 0;
+#pragma unroll
+            for (int k = 0; k < kRowsPer; ++k) {
+                const int r = tid * kRowsPer + k;
+                v[k] = r < ny ? L.par[r] : 0;
+                sum += v[k];
+            }
+            int tot = 0;
+            int run = sm_excl_scan(sum, L.wsc, &tot);
+#pragma unroll
+            for (int k = 0; k < kRowsPer; ++k) {
+                const int r = tid * kRowsPer + k;
+                if (r < ny) L.par[r] = run;
+                run += v[k];
+            }
+            if (tid == 0) L.par[ny] = nf;
+            __syncthreads();
+        }
+        if (tid < 2) {
+            // band g: the rows from the first row whose cost prefix reaches g / G of the total;
+            // a row costs its points plus its cells (both fill a band's tables of kBandCap)
+            const int64_t total = (int64_t)nf + (int64_t)ny * nx;
+            const int64_t want = (int64_t)(g + tid) * total / G;
+            int lo = 0, hi = ny;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)L.par[mid] + (int64_t)mid * nx >= want) hi = mid; else lo = mid + 1;
+            }
+            L.meta[tid] = g + tid == G ? ny : lo;
+        }
+        __syncthreads();
+        ra = L.meta[0];
+        rb = L.meta[1];
+        sa = ra > 0 ? ra - 1 : 0;
+        sb = rb < ny ? rb + 1 : ny;
+        if (ra >= rb) sa = sb = ra;  // (an empty band stages nothing)
+        own0 = L.par[ra];
+        own1 = L.par[rb];
+        const int staged = L.par[sb] - L.par[sa];
+        if (staged > kBandCap || (sb - sa) * nx > kBandCells) bad = true;
+        __syncthreads();
+    }
+    const int srows = sb - sa, scells = srows * nx;
+    const int S = (bad || nf == 0) ? 0 : L.par[sb] - L.par[sa];
+    if (bad && tid == 0) {
+        __hip_atomic_store(st + kStError, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (mirror)
+            __hip_atomic_store(reinterpret_cast<int32_t*>(mirror + kMiscState) + kStError, 3,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+
+    SM_STAMP(2);
+    // ---- stage the rows [sa, sb): counting sort by staged cell ----
+    int occupied = 0;
+    if (S > 0) {
+        for (int c = tid; c < scells; c += kBandT) L.info[c] = 0;
+        __syncthreads();
+        band_pass(x, y, m, [&](int, double a, double b) {
+            if (isfinite(a) && isfinite(b)) {
+                int row, col, quad;
+                cell_of(a, b, row, col, quad);
+                if (row >= sa && row < sb) atomicAdd(&L.info[(row - sa) * nx + col], 1u);
+            }
+        });
+        __syncthreads();
+        {
+            constexpr int kCellPer = (kBandCells + kBandT - 1) / kBandT;
+            int cnt[kCellPer], sum = 0;
+#pragma unroll
+            for (int k = 0; k < kCellPer; ++k) {
+                const int c = tid * kCellPer + k;
+                cnt[k] = c < scells ? (int)L.info[c] : 0;
+                sum += cnt[k];
+            }
+            int tot = 0;
+            int run = sm_excl_scan(sum, L.wsc, &tot);
+#pragma unroll
+            for (int k = 0; k < kCellPer; ++k) {
+                const int c = tid * kCellPer + k;
+                if (c < scells) {
+                    L.par[c] = run;
+                    L.cst[c] = (uint16_t)run;
+                    // owned cells only (the statistics' occupied cells)
+                    const int row = sa + c / nx;
+                    occupied += (cnt[k] > 0 && row >= ra && row < rb) ? 1 : 0;
+                }
+                run += cnt[k];
+            }
+            if (tid == 0) L.cst[scells] = (uint16_t)S;
+        }
+        __syncthreads();
+        band_pass(x, y, m, [&](int i, double a, double b) {
+            if (isfinite(a) && isfinite(b)) {
+                int row, col, quad;
+                cell_of(a, b, row, col, quad);
+                if (row >= sa && row < sb) {
+                    const int c = (row - sa) * nx + col;
+                    const int s = atomicAdd(&L.par[c], 1);
+                    L.rec[s] = make_float2((float)((a * 0.5 - L.G.cx2) * L.G.invs),
+                                           (float)((b * 0.5 - L.G.cy2) * L.G.invs));
+                    L.info[s] = ((uint32_t)i << 16) | ((uint32_t)quad << 13) | (uint32_t)c;
+                }
+            }
+        });
+        __syncthreads();
+    }
+    SM_STAMP(3);
+    // the staged stencil context: rows [sa, sb) as rows 0 .. srows - 1
+    const SmCtx c{x, y, eps2, L.G.lo, L.G.hi, nx, srows, L.G.exact_only != 0};
+    // own slots: the rows [ra, rb)
+    const int s0 = S > 0 ? (int)L.cst[(ra - sa) * nx] : 0;
+    const int s1 = S > 0 ? (int)L.cst[(rb - sa) * nx] : 0;
+    (void)own0;
+    (void)own1;
+
+    // ---- count (own points): a thread each when they fill a quarter of the workgroup, else
+    // a wave each (64 candidates per step, ballot counts) ----
+    int ncore = 0;
+    if (s1 - s0 >= kBandT / 4) {
+        for (int p = s0 + tid; p < s1; p += kBandT) {
+            const bool cc = sm_count(L, c, p, min_points, -1) >= min_points;
+            const int v = (int)(L.info[p] >> 16);
+            ba.core[v] = cc ? 1 : 0;
+            ba.par[v] = v;
+            ncore += cc ? 1 : 0;
+        }
+    } else {
+        for (int p = s0 + (tid >> 6); p < s1; p += kW) {
+            const bool cc = sp_count_wave(L, c, p, min_points) >= min_points;
+            if (lane == 0) {
+                const int v = (int)(L.info[p] >> 16);
+                ba.core[v] = cc ? 1 : 0;
+                ba.par[v] = v;
+                ncore += cc ? 1 : 0;
+            }
+        }
+    }
+    SM_STAMP(4);
+    // this workgroup's share of the root words, zeroed for the roots phase
+    for (int k = g * kBandT + tid; k < (m + 31) / 32; k += G * kBandT) ba.rbits[k] = 0u;
+    sp_grid_sync(ba.bar, (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(5);
+
+    // ---- union: the staged core flags, own cores' walks, the forest published ----
+    {
+        int tot = 0, occ = 0;
+        (void)sm_excl_scan(ncore, L.wsc, &tot);
+        (void)sm_excl_scan(occupied, L.wsc, &occ);
+        if (tid == 0) {
+            if (tot) atomicAdd(&ba.cnt[0], tot);
+            if (occ) atomicAdd(&ba.cnt[1], occ);
+        }
+    }
+    for (int p = tid; p < S; p += kBandT) {
+        L.core[p] = ba.core[L.info[p] >> 16];
+        L.par[p] = p;
+    }
+    if (tid == 0) L.meta[2] = 0;
+    __syncthreads();
+    const bool quarters = L.G.clique != 0;
+    const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
+    const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy - (double)sa;  // (staged rows)
+    for (int it = tid; it < (s1 - s0) * 3; it += kBandT) {
+        const int i = it / 3;
+        if (L.core[s0 + i]) sm_union_walk(L, c, s0 + i, it - 3 * i, quarters, reach_kx, reach_ky);
+    }
+    __syncthreads();
+    SM_STAMP(6);
+    uint32_t* mine = ba.pairs + (int64_t)g * kBandCap;
+    for (int p = tid; p < S; p += kBandT) {
+        if (!L.core[p] || L.par[p] == p) continue;
+        int r = p;
+        for (int u = L.par[r]; u != r; u = L.par[r]) r = u;
+        const int k = atomicAdd(&L.meta[2], 1);
+        mine[k] = (L.info[p] & 0xFFFF0000u) | (L.info[r] >> 16);
+    }
+    __syncthreads();
+    const int npairs = L.meta[2];
+    SM_STAMP(7);
+    sp_grid_sync(ba.bar, 2u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(8);
+
+    // ---- merge: this workgroup's pairs into the global union-find over input indices ----
+    for (int k = tid; k < npairs; k += kBandT) {
+        const uint32_t w = mine[k];
+        bd_unite(ba.par, (int)(w >> 16), (int)(w & 0xFFFFu));
+    }
+    SM_STAMP(9);
+    sp_grid_sync(ba.bar, 3u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(10);
+
+    // ---- roots of the own cores (read-only walks: every union is done) ----
+    for (int p = s0 + tid; p < s1; p += kBandT) {
+        if (!L.core[p]) continue;
+        const int v = (int)(L.info[p] >> 16);
+        int r = v;
+        for (int u = ba.par[r]; u != r; u = ba.par[r]) r = u;
+        ba.lab[v] = r;
+        if (r == v) atomicOr(&ba.rbits[v >> 5], 1u << (v & 31));
+    }
+    SM_STAMP(11);
+    sp_grid_sync(ba.bar, 4u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(12);
+
+    // ---- numbering and labels ----
+    const int nw = (m + 31) / 32;
+    int nclust = 0;
+    {
+        constexpr int kWPer = kBandWords / kBandT;
+        int v[kWPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kWPer; ++k) {
+            const int wd = tid * kWPer + k;
+            const uint32_t bits =
+                wd < nw ? __hip_atomic_load(ba.rbits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0u;
+            if (wd < kBandWords) L.rbits[wd] = bits;
+            v[k] = __popc(bits);
+            sum += v[k];
+        }
+        int run = sm_excl_scan(sum, L.wsc, &nclust);
+#pragma unroll
+        for (int k = 0; k < kWPer; ++k) {
+            const int wd = tid * kWPer + k;
+            if (wd < kBandWords) L.wrank[wd] = run;
+            run += v[k];
+        }
+        __syncthreads();
+    }
+    SM_STAMP(13);
+    const auto cluster_of = [&](uint32_t s) {
+        return L.wrank[s >> 5] + __popc(L.rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
+    };
+    for (int p = s0 + tid; p < s1; p += kBandT) {  // cores: one thread each
+        if (!L.core[p]) continue;
+        const uint32_t v = L.info[p] >> 16;
+        cluster[v] = cluster_of((uint32_t)ba.lab[v]);
+        flag[v] = DBSCAN_FLAG_CORE;
+    }
+    for (int p = s0 + (tid >> 6); p < s1; p += kW) {  // non-cores: a wave each
+        if (L.core[p]) continue;
+        const float2 me = L.rec[p];
+        const int cc = (int)(L.info[p] & kCellMask);
+        const int cy = cc / nx, cx = cc - cy * nx;
+        const int x0 = max(cx - 1, 0), x1 = min(cx + 1, nx - 1);
+        uint32_t best = 0xFFFFFFFFu;
+        for (int d = 0; d < 3; ++d) {
+            const int r = d == 0 ? cy : (d == 1 ? cy - 1 : cy + 1);
+            if (r < 0 || r >= srows) continue;
+            const int e = L.cst[r * nx + x1 + 1];
+            for (int q = L.cst[r * nx + x0] + lane; q < e; q += 64) {
+                if (!L.core[q]) continue;
+                const uint32_t s = (uint32_t)ba.lab[L.info[q] >> 16];
+                if (s < best && sm_pair(L, c, p, me, q, L.rec[q])) best = s;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+        if (lane == 0) {
+            const uint32_t v = L.info[p] >> 16;
+            int cid = 0;
+            uint8_t f = DBSCAN_FLAG_NOISE;
+            if (best != 0xFFFFFFFFu && (mode != DBSCAN_MODE_NAIVE || best < v)) {
+                cid = cluster_of(best);
+                f = DBSCAN_FLAG_BORDER;
+            }
+            cluster[v] = cid;
+            flag[v] = f;
+        }
+    }
+    if (g == G - 1) {  // the non-finite points: nobody's neighbour, noise (minPoints >= 1)
+        for (int i = tid; i < m; i += kBandT)
+            if (!(isfinite(x[i]) && isfinite(y[i]))) {
+                cluster[i] = 0;
+                flag[i] = DBSCAN_FLAG_NOISE;
+            }
+    }
+    SM_STAMP(14);
+    // ---- statistics (workgroup 0) and the barrier reset (the last workgroup to leave) ----
+    if (g == 0 && tid == 0) {
+        sm_set_stat(st, mirror, kStNf, nf);
+        sm_set_stat(st, mirror, kStCore, __hip_atomic_load(&ba.cnt[0], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+        sm_set_stat(st, mirror, kStClusters, nclust);
+        sm_set_stat(st, mirror, kStCells, nf > 0 ? __hip_atomic_load(&ba.cnt[1], __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                                 : 0);
+        GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
+                      1u, 1u, 0};
+        *gp = gg;
+        if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
+    }
+    if (tid == 0 &&
+        __hip_atomic_fetch_add(ba.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (uint32_t)G - 1) {
+        __hip_atomic_store(ba.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ba.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace
 
 #if DBSCAN_AB_STAMPS
@@ -1187,10 +1746,74 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
+bool band_fit_eligible(int64_t n, double eps, int32_t mode, int32_t min_points) {
+    const double eps2 = eps * eps;
+    return n > kSmallMaxPoints && n <= kBandMaxPoints && std::isfinite(eps2) &&
+           (mode == DBSCAN_MODE_NAIVE || mode == DBSCAN_MODE_ARCHERY) && min_points >= 1;
+}
+
+void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
+                      const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
+                      int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
+                      double* mirror) {
+    // kBandMaxWG workgroups whatever n: the band cost bound of band_make_grid assumes it, and
+    // more bands keep each workgroup's count and union walks short
+    const int G = kBandMaxWG;
+    (void)n;
+    // scratch: barrier words (zero between launches), counters, per input index core flags,
+    // labels and the union-find, root words, the published pairs
+    constexpr size_t kHead = 512;  // bar[2] at 0, cnt[2] at 64, npairs[kBandMaxWG] at 128
+    const size_t words = (size_t)(kBandMaxPoints / 32 + 1);
+    const size_t bytes = kHead + (size_t)kBandMaxPoints * (1 + 4 + 4) + words * 4 +
+                         (size_t)kBandMaxWG * kBandCap * 4;
+    if (ws.band.bytes < bytes || !ws.band_ready) {
+        char* p = static_cast<char*>(ws.band.ensure(bytes));
+        DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, kHead, s));  // the barrier words, once
+        ws.band_ready = true;
+    }
+    char* base = static_cast<char*>(ws.band.p);
+    BandArgs ba;
+    ba.bar = reinterpret_cast<uint32_t*>(base);
+    ba.cnt = reinterpret_cast<int32_t*>(base + 64);
+    ba.npairs = reinterpret_cast<int32_t*>(base + 128);
+    char* q = base + kHead;
+    ba.core = reinterpret_cast<uint8_t*>(q);
+    q += kBandMaxPoints;
+    ba.lab = reinterpret_cast<int32_t*>(q);
+    q += (size_t)kBandMaxPoints * 4;
+    ba.par = reinterpret_cast<int32_t*>(q);
+    q += (size_t)kBandMaxPoints * 4;
+    ba.rbits = reinterpret_cast<uint32_t*>(q);
+    q += words * 4;
+    ba.pairs = reinterpret_cast<uint32_t*>(q);
+    // kStError cleared ahead of the launch, in the device state and the pinned mirror
+    DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
+    if (mirror && ws.stats_host)
+        reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
+    ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
+                                               gp, st, mirror};
+    ws.recall_band = true;
+    klaunch(prof, "band_fit", band_fit_kernel, dim3(G), dim3(kBandT), 0, s, x, y, (int)n, eps,
+            eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, ba,
+            ws.spread_spin_limit);
+    DBSCAN_HIP_CHECK(hipGetLastError());
+}
+
 bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws) {
     Workspace::SpreadRecall& r = ws.spread_recall;
     if (!ws.fit_mirrored || !r.valid || !ws.stats_host) return false;
     int32_t* v = reinterpret_cast<int32_t*>(ws.stats_host + kMiscState);
+    if (ws.recall_band) {  // a band fit: barrier gave up (2) or a band overflowed (3)
+        if (v[kStError] != 2 && v[kStError] != 3) return false;
+        FitArgs b{r.x, r.y, nullptr, r.n, r.eps, r.min_points, r.mode, r.cluster, r.flag,
+                  nullptr, nullptr};
+        b.small_max = 0;  // the tiled pipeline (no LDS fit, no band fit)
+        enqueue_fit(s, ws, prof, b, nullptr);
+        enqueue_fit_stats_copy(s, ws, ws.stats_host);
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        ++ws.spread_fallbacks;
+        return true;
+    }
     if (v[kStError] != 2) return false;
     // the one-workgroup kernel: no grid barrier, every label and statistic rewritten
     enqueue_small_fits(s, prof, r.x, r.y, nullptr, nullptr, 1, r.n, r.eps, r.min_points, r.mode,

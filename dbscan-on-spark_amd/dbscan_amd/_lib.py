@@ -66,6 +66,7 @@ SIGNATURES = [
     ("dbscan_generate_blobs_device", _i32, [_vp, _vp, _vp, _i64, _d, _d, _u64]),
     ("dbscan_set_small_max", _i64, [_vp, _i64]),
     ("dbscan_set_spread_min", _i64, [_vp, _i64]),
+    ("dbscan_set_band_max", _i64, [_vp, _i64]),
     ("dbscan_set_spread_spin_limit", _i64, [_vp, _i64]),
     ("dbscan_spread_fallbacks", _i64, [_vp]),
     ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
@@ -178,6 +179,14 @@ class Handle:
         spread_fit_kernel); above DBSCAN_SMALL_MAX_POINTS every LDS fit keeps one workgroup.
         Returns the previous value."""
         r = load().dbscan_set_spread_min(self._h, int(min_points))
+        if r < 0:
+            check(int(r))
+        return int(r)
+
+    def set_band_max(self, max_points: int) -> int:
+        """Full fits above the LDS capacity and up to max_points points run the band form
+        (one launch; 0: never).  Returns the previous value."""
+        r = load().dbscan_set_band_max(self._h, int(max_points))
         if r < 0:
             check(int(r))
         return int(r)

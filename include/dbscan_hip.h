@@ -211,11 +211,24 @@ int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
  * fails for it.  Such re-runs are counted (dbscan_spread_fallbacks). */
 #define DBSCAN_SPREAD_DEFAULT_POINTS 512
 int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
+/* Full fits above the LDS fits' capacity (DBSCAN_SMALL_MAX_POINTS, with small_max at that
+ * ceiling) and up to dbscan_set_band_max(h, ...) points (default and ceiling
+ * DBSCAN_BAND_MAX_POINTS; 0: never) in modes NAIVE and ARCHERY with minPoints >= 1 run in ONE
+ * launch instead of the tiled pipeline's ~45: up to 64 workgroups, each staging a band of cell
+ * rows (plus one row either side) in its LDS, meeting at four grid barriers, the clusters
+ * merged in a union-find over input indices -- same results bit for bit.  A band over the
+ * staging capacity (very dense rows) or a barrier that gives up re-runs the fit through the
+ * tiled pipeline in the same call (counted by dbscan_spread_fallbacks).  Returns the previous
+ * value. */
+#define DBSCAN_BAND_MAX_POINTS 65536
+#define DBSCAN_BAND_DEFAULT_POINTS 65536
+int64_t dbscan_set_band_max(dbscan_handle* h, int64_t max_points);
 /* Test hook: the spread fit's barrier poll bound (default 2^21 polls, ~seconds); 0 makes every
  * barrier give up at once, so every spread fit takes the one-workgroup re-run.  Returns the
  * previous bound (negative: an error code). */
 int64_t dbscan_set_spread_spin_limit(dbscan_handle* h, int64_t polls);
-/* Spread fits of this handle re-run by the one-workgroup kernel so far (negative: an error). */
+/* Spread and band fits of this handle re-run by the fallback (the one-workgroup kernel, the
+ * tiled pipeline) so far (negative: an error). */
 int64_t dbscan_spread_fallbacks(dbscan_handle* h);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is

@@ -1,0 +1,172 @@
+"""Partitions above the one-workgroup LDS capacity in ONE launch (small.hip band_fit_kernel):
+8192 < m <= 65536 points, up to 64 workgroups each staging a band of cell rows plus one row
+either side, four grid barriers, the clusters merged over input indices.  Every result must
+equal the oracle (LocalDBSCANNaive.scala:37-118 / LocalDBSCANArchery.scala:36-112 restated,
+visit order = array order) and the tiled pipeline (dbscan_set_band_max 0) bit for bit; bands
+over the staging capacity and barriers that give up fall back to the tiled pipeline."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dbscan_amd
+
+    if dbscan_amd.load().dbscan_device_count() < 1:
+        pytest.fail("no GPU visible to libdbscan_hip.so")
+    return dbscan_amd
+
+
+def _set(rng, m, spread=3.0):
+    k = int(rng.integers(2, 10))
+    c = rng.uniform(-spread, spread, size=(k, 2))
+    nb = m - m // 5
+    pts = c[rng.integers(0, k, nb)] + rng.normal(0, rng.uniform(0.05, 0.4), size=(nb, 2))
+    pts = np.concatenate([pts, rng.uniform(-spread - 1, spread + 1, size=(m - nb, 2))])
+    pts = pts[rng.permutation(m)] * np.sqrt(m / 8192.0)
+    return pts[:, 0].copy(), pts[:, 1].copy()
+
+
+def _eq(got, ref, what):
+    cl, fl, k = got
+    rc, rf, rk = ref
+    assert k == rk, f"{what}: {k} clusters, oracle {rk}"
+    bad = np.flatnonzero((cl != rc) | (fl != rf))
+    assert bad.size == 0, f"{what}: {bad.size} mismatches, first {bad[:10]}"
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_band_sizes_vs_oracle(dm, mode):
+    """Sizes from just above the LDS capacity to the band ceiling, through dbscan_fit_h and
+    dbscan_fit_device (the densest of these sets overflow a band and take the fallback; the
+    others do not)."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(800 + mode)
+    h = dm.Handle(0)
+    try:
+        before = h.spread_fallbacks()
+        for m in (8193, 9000, 12345, 16384, 20000, 33333, 50000, 65535, 65536):
+            x, y = _set(rng, m)
+            eps, mp = (0.12, 6) if m % 2 else (0.2, 10)
+            ref = O.fit_grid(x, y, eps, mp, mode)
+            _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=h), ref, f"fit_h m={m}")
+            tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+            cl, fl, k = D.fit_tensors(tx, ty, eps, mp, mode, h)
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), k), ref, f"device m={m}")
+        assert h.spread_fallbacks() - before <= 4
+    finally:
+        h.close()
+
+
+def test_band_sparse_partitions_take_no_fallback(dm):
+    """Partitions shaped like the seam's halo-grown ones above 8192 points (blobs over tens of
+    eps cells per side, rows of a few hundred points): the band form serves them all."""
+    rng = np.random.default_rng(42)
+    h = dm.Handle(0)
+    try:
+        before = h.spread_fallbacks()
+        for m in (9000, 15000, 19273):
+            side = 25 * 2.55
+            c = rng.uniform(0, side, size=(6, 2))
+            pts = c[rng.integers(0, 6, m)] + rng.normal(0, side / 6, size=(m, 2))
+            x, y = pts[:, 0].copy(), pts[:, 1].copy()
+            _eq(dm.fit_arrays(x, y, 2.55, 10, 0, handle=h), O.fit_grid(x, y, 2.55, 10, 0),
+                f"m={m}")
+        assert h.spread_fallbacks() == before
+    finally:
+        h.close()
+
+
+def test_band_equals_tiled_and_edge_inputs(dm):
+    """Non-finite points, minPoints 1, a large eps (few wide cells), duplicates, visit-order
+    permutations; the tiled pipeline (band_max 0) bit for bit."""
+    rng = np.random.default_rng(91)
+    h = dm.Handle(0)
+    try:
+        for m, eps, mp in ((15000, 0.12, 1), (30000, 2.0, 25), (40000, 0.05, 3)):
+            x, y = _set(rng, m)
+            x[::1013] = np.nan
+            y[7::2027] = -np.inf
+            x[100:200] = x[300:400]  # duplicates
+            y[100:200] = y[300:400]
+            ref = O.fit_grid(x, y, eps, mp, 0)
+            got = dm.fit_arrays(x, y, eps, mp, 0, handle=h)
+            _eq(got, ref, f"band m={m}")
+            prev = h.set_band_max(0)
+            _eq(dm.fit_arrays(x, y, eps, mp, 0, handle=h), ref, f"tiled m={m}")
+            h.set_band_max(prev)
+            p = rng.permutation(m)
+            refp = O.fit_grid(x[p], y[p], eps, mp, 0)
+            _eq(dm.fit_arrays(x[p], y[p], eps, mp, 0, handle=h), refp, f"permuted m={m}")
+            np.testing.assert_array_equal(refp[1] == 1, ref[1][p] == 1)  # core flags move along
+    finally:
+        h.close()
+
+
+def test_band_overflow_and_barrier_fallbacks(dm):
+    """A row denser than a band's staging capacity (20000 points in one thin strip) and a
+    forced barrier give-up (poll bound 0) both re-run through the tiled pipeline in the same
+    call, counted, equal to the oracle."""
+    rng = np.random.default_rng(5)
+    h = dm.Handle(0)
+    try:
+        m = 20000
+        x = rng.uniform(0, 50, m)
+        y = rng.uniform(0, 0.05, m)
+        ref = O.fit_grid(x, y, 0.2, 10, 0)
+        before = h.spread_fallbacks()
+        _eq(dm.fit_arrays(x, y, 0.2, 10, 0, handle=h), ref, "dense strip")
+        assert h.spread_fallbacks() == before + 1
+        x2, y2 = _set(rng, 30000)
+        ref2 = O.fit_grid(x2, y2, 0.12, 6, 1)
+        h.set_spread_spin_limit(0)
+        _eq(dm.fit_arrays(x2, y2, 0.12, 6, 1, handle=h), ref2, "barrier give-up")
+        assert h.spread_fallbacks() == before + 2
+        h.set_spread_spin_limit(1 << 21)
+        _eq(dm.fit_arrays(x2, y2, 0.12, 6, 1, handle=h), ref2, "default bound")
+        assert h.spread_fallbacks() == before + 2
+    finally:
+        h.close()
+
+
+def test_band_from_concurrent_handles(dm):
+    """Four executor threads, a handle each, band fits at once (4 x up to 64 workgroups of
+    one CU each): every fit equals its oracle fit."""
+    import threading
+
+    rng = np.random.default_rng(606)
+    sets = []
+    for m in (9000, 20000, 40000, 65536, 12000, 30000, 50000, 16000):
+        x, y = _set(rng, m)
+        sets.append((x, y))
+    refs = [O.fit_grid(x, y, 0.12, 6, 0) for x, y in sets]
+    handles = [dm.Handle(0) for _ in range(4)]
+    errors = []
+
+    def worker(t):
+        try:
+            for rep in range(2):
+                for k in range(t, len(sets), 4):
+                    x, y = sets[k]
+                    _eq(dm.fit_arrays(x, y, 0.12, 6, 0, handle=handles[t]), refs[k],
+                        f"thread {t} set {k} rep {rep}")
+        except Exception as exc:
+            errors.append(exc)
+
+    try:
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for hh in handles:
+            hh.close()
+    assert not errors, errors[0]

@@ -1,0 +1,35 @@
+"""Phase times of the band LDS fit (small.hip band_fit_kernel) from a DBSCAN_AB_STAMPS=1
+timing build:
+    ABFLAGS=-DDBSCAN_AB_STAMPS=1 tools/build_ab.sh stamps WORKTREE
+    DBSCAN_LIB_PATH=dbscan-on-spark_amd/lib_ab/stamps/libdbscan_hip.so python tools/band_stamps.py
+Thread 0 of workgroup 0 stamps the 100 MHz clock at the phase boundaries (its barrier waits
+hold the other workgroups' lag)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "dbscan-on-spark_amd"))
+import dbscan_amd  # noqa: E402
+from dbscan_amd import device as D  # noqa: E402
+
+PH = ["grid", "bands", "stage", "count", "barrier1", "union walks", "publish", "barrier2",
+      "merge", "barrier3", "roots", "barrier4", "numbering", "labels"]
+lib = dbscan_amd.load()
+f = lib.dbscan_ab_small_stamps
+f.argtypes = [ctypes.c_void_p]
+h = dbscan_amd.Handle(0)
+buf = (ctypes.c_longlong * 16)()
+for m in [int(a) for a in (sys.argv[1:] or ["12000", "20000", "40000", "65536"])]:
+    tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
+    rows = []
+    for _ in range(7):
+        D.fit_tensors(tx, ty, 2.55, 10, 0, h)
+        f(buf)
+        rows.append(np.diff(np.array([buf[i] for i in range(15)], dtype=np.int64)) / 100.0)
+    r = np.median(np.array(rows), axis=0)
+    print(f"m={m}: " + ", ".join(f"{p} {v:.1f}" for p, v in zip(PH, r)) +
+          f"  kernel {r.sum():.1f} us", flush=True)

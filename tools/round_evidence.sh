@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round-end evidence in one GPU call: smoke, the default bench (config 2 with the CPU baseline and
 # the end-to-end leg and the seam leg), the node path at N = 1 on config 3's per-GPU share, its
-# one-rank RCCL rehearsal (--force-collectives), configs 3/4/5 per-GPU shares, then tools/profile.sh (kernel trace + PMC passes).
+# one-rank RCCL rehearsal (--force-collectives), configs 3/4/5 per-GPU shares, config 5 itself
+# through dbscan_train_node (phase trace), the node path's phase trace with RCCL forced, then
+# tools/profile.sh (kernel trace + PMC passes).
 # Each step under its own limit; the first failure ends the script.  NO_PROFILE=1: benches only;
 # TAG names the profile summaries (gpurun_out/ev/profiles/<TAG>_*, copy them to profiles/).
 set -o pipefail
@@ -18,6 +20,9 @@ run bench_rccl 300 python bench.py --force-collectives --config 3 --steps 10 --w
 run bench_noise 300 python bench.py --config 3 --steps 10 --warmup 3 --no-cpu-baseline --no-seam
 run bench_dense 300 python bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline --no-seam
 run bench_big 300 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 2 --no-seam
+# config 5 itself (10^9 points) through the one-process whole-node entry, phase trace on stderr
+DBSCAN_NODE_TRACE=1 run train_node_config5 400 python -u tools/train_node_probe.py 1e9 8
+run node_phase_trace 300 python -u tools/node_phase_trace.py
 grep -h '^{' gpurun_out/ev/bench_*.log | cut -c1-200
 [ "${NO_PROFILE:-0}" = 1 ] && exit 0
 # the raw traces exceed gpurun's 64 MiB return limit: summarize here, keep the summaries only
