@@ -63,12 +63,22 @@ static_assert(kSmN % kSmT == 0 && kSmCells % kSmT == 0, "whole rounds per thread
 // DBSCAN_AB_STAMPS (timing builds only, never the shipped library): thread 0 of workgroup 0
 // records the 100 MHz clock at the phase boundaries (dbscan_ab_small_stamps).
 #if DBSCAN_AB_STAMPS
-__device__ long long g_sm_stamps[16];
+__device__ long long g_sm_stamps[24];
 #define SM_STAMP(k)                                                               \
     do {                                                                          \
         if (threadIdx.x == 0 && blockIdx.x == 0) g_sm_stamps[(k)] = wall_clock64(); \
     } while (0)
+// band_fit_kernel, every workgroup: [g][0..5] = clock at the stage's end, the count's end,
+// after barrier 1, at barrier 2's arrival; own points, staged points
+__device__ long long g_band_wg[64 * 8];
+#define BAND_WG(k, v)                                           \
+    do {                                                        \
+        if (threadIdx.x == 0) g_band_wg[blockIdx.x * 8 + (k)] = (v); \
+    } while (0)
 #else
+#define BAND_WG(k, v) \
+    do {              \
+    } while (0)
 #define SM_STAMP(k) \
     do {            \
     } while (0)
@@ -482,8 +492,11 @@ __device__ __forceinline__ void sm_union_walk(LT& L, const SmCtx& cx_, int p, in
         const float ty = (float)((double)me.y + reach_ky - (double)cy);
         const float mg = (fabsf(me.x) + fabsf(me.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
         const float rr = (sqrtf(cx_.hi) + mg) * (sqrtf(cx_.hi) + mg);
+        // (one stencil row: only its two quarter rows of the window)
+        const int wa = only < 0 ? -1 : (only == 0 ? 1 : (only == 1 ? 0 : 2));
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
+            if (wa >= 0 && (a >> 1) != wa) continue;
             const float y0 = 0.5f * (float)a - 1.0f,
                         dy = fmaxf(0.0f, fmaxf(y0 - ty, ty - (y0 + 0.5f)));
 #pragma unroll
@@ -685,7 +698,9 @@ __global__ __launch_bounds__(kSmT, 1) void small_fit_kernel(
     const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy;
     const int R = split ? 3 : 1;  // stencil rows per work item
     for (int it = tid; it < nf * R; it += kSmT) {
-        const int p = split ? it / 3 : it, only = split ? it - 3 * (it / 3) : -1;
+        // (row-major items, as band_fit_kernel: 250 / 2000 points 56.5 / 99.7 -> 51.7 / 89.8
+        // us per call)
+        const int p = split ? it % nf : it, only = split ? it / nf : -1;
         if (L.core[p]) sm_union_walk(L, c, p, only, quarters, reach_kx, reach_ky);
     }
     __syncthreads();
@@ -1003,9 +1018,9 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
     // (one thread per stencil row: the wave-cooperative form, a serial unite per joined quarter,
     // measured 48 -> 92 us at 8192 points)
     for (int it = tid; it < nb * 3; it += kSmT) {
-        const int i = it / 3;
-        if (L.core[s0 + i])
-            sm_union_walk(L, c, s0 + i, it - 3 * i, quarters, reach_kx, reach_ky);
+        // (row-major items, as band_fit_kernel: 8192 points 155 -> 137 us per call)
+        const int d = it / nb, i = it - d * nb;
+        if (L.core[s0 + i]) sm_union_walk(L, c, s0 + i, d, quarters, reach_kx, reach_ky);
     }
     __syncthreads();
     SM_STAMP(9);
@@ -1133,19 +1148,27 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 // Partitions above the one-workgroup capacity (kSmallMaxPoints < m <= kBandMaxPoints: a dense
 // region's rectangle plus its eps halo, DBSCAN.scala:116-137) in ONE launch (band_fit_kernel):
 // the tiled pipeline's ~45 kernel boundaries cost ~5 us each on the GPU whatever enqueues them.
-// G workgroups (one per CU by their LDS), each owning a BAND of cell rows holding ~m/G points
-// and staging only that band plus one cell row on either side (the 3x3 stencil of an owned
-// point never leaves the staged rows):
-//   stage   every workgroup reads all m points: the bbox and the grid (cells of side >= eps,
-//           grown only while the grid is too large for the band tables), the points per cell
-//           row, the bands (row ranges at count quantiles, alike in every workgroup); then its
-//           staged rows' points, counting-sorted by cell in LDS (fp32 records as small.hip)
-//   count   its own points, one wave each (sp_count_wave); core flags by input index
+// G = 64 workgroups (one per CU by their LDS), each owning a range of cells of ~1/G of the
+// partition's cost (below) and staging only the rows of those cells plus one cell row on
+// either side (the 3x3 stencil of an owned point never leaves the staged rows):
+//   slice   each workgroup reads ~m/G points, one per thread: the non-finite ones labelled
+//           noise, the slice's bbox published
+//   -- grid barrier A --
+//   grid    the G boxes reduced in one order (the same grid everywhere; cells of side >= eps,
+//           grown only while the grid is too large for the band tables); the slice's points
+//           per cell row added to global row counts
+//   -- grid barrier B --
+//   bands   the row counts -> cost prefix -> this workgroup's cell range (alike everywhere);
+//           the slice's points scattered to a global row-sorted array (each row's piece
+//           claimed once per workgroup)
+//   -- grid barrier C --
+//   stage   the staged rows' records (one contiguous piece of the row-sorted array) counting-
+//           sorted by cell in LDS (fp32 records as small.hip)
+//   count   its own points (a thread or a wave each); core flags by input index
 //   -- grid barrier 1 --
 //   union   the staged slots' core flags; its own cores' stencil walks (sm_union_walk) into an
 //           LDS forest over the staged slots; every non-root staged core published as
-//           (input index, its root's input index).  An edge between two bands is walked by the
-//           lower band's workgroup (the upper row is its halo) -- every closed-form edge by the
+//           (input index, its root's input index).  An edge between two ranges is walked by the
 //           owner of the smaller cell, as in spread_fit_kernel
 //   -- grid barrier 2 --
 //   merge   the published pairs united in a union-find over input indices in global memory
@@ -1155,15 +1178,16 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 //   -- grid barrier 4 --
 //   label   root flags -> popcount ranks (cluster id = 1 + roots before s(K)); own cores their
 //           root's id, own non-cores the min s(K) over their staged core neighbours + the Naive /
-//           Archery rule; the non-finite points noise (the last workgroup)
+//           Archery rule
 // Same results bit for bit as every other form (the GPU tests compare them with the oracle).
-// A band over the staging capacity (a row too dense, or too many sparse rows), or a barrier
+// A range over the staging capacity (rows too dense, or too many sparse rows), or a barrier
 // that gives up, flags st[kStError] (3 / 2): the host then re-runs the fit through the tiled
 // pipeline in the same call.
 constexpr int kBandT = 1024;
 constexpr int kBandCap = 7168;    // staged points per workgroup (and staged cells)
 constexpr int kBandCells = kBandCap;
 constexpr int kBandMaxWG = 64;
+constexpr int kBandC0 = 2;  // a point's count + walk work without neighbours, in cell densities
 constexpr int kBandWords = (int)(kBandMaxPoints / 32);
 static_assert(kBandMaxPoints <= 65536, "16-bit visit indices");
 static_assert(kBandCells <= 8191, "13-bit cells in info");
@@ -1191,12 +1215,17 @@ struct BandArgs {
     int32_t* npairs;  // [G]
     int32_t* cnt;     // [2] cores, occupied cells
     uint32_t* bar;    // [2] arrivals, departures (zero between launches)
+    double* box;      // [G][5] the slices' min x, max x, min y, max y, finite count
+    uint32_t* rowcnt; // [kBandCap] points per grid row (zero between launches)
+    uint32_t* rowcur; // [kBandCap] claimed per grid row (zero between launches)
+    double2* rxy;     // [m] the finite points' coordinates sorted by grid row
+    int32_t* ridx;    // [m] their input indices
 };
 
 // The band grid (one thread): sides as sm_make_grid, doubled along the axis over its share of
 // the limits until nx <= kBandCells / 3 and ny < kBandCap (row counts live in par) and the
-// whole grid holds <= 24 * kBandCells cells: with kBandMaxWG bands of ~1/G of the cost below
-// (points + cells) each band fits its tables with room for its halo rows
+// whole grid holds <= 24 * kBandCells cells: with kBandMaxWG ranges of ~1/G of the cost below
+// (at most twice the points + cells) each range fits its tables with room for its halo rows
 __device__ void band_make_grid(double xmin, double xmax, double ymin, double ymax, int nf,
                                double eps, double eps2, SmGrid* g) {
     g->nf = nf;
@@ -1254,17 +1283,52 @@ __device__ void band_make_grid(double xmin, double xmax, double ymin, double yma
     g->hi = __double2float_ru(e2 + M);
 }
 
+// Exclusive prefix of an int64 over the workgroup (kBandT threads); ws: kBandT / 64 + 1 slots
+__device__ int64_t bd_scan64(int64_t v, int64_t* ws, int64_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int k = 0; k < kBandT / 64; ++k) {
+            const int64_t t = ws[k];
+            ws[k] = run;
+            run += t;
+        }
+        ws[kBandT / 64] = run;
+    }
+    __syncthreads();
+    const int64_t r = ws[w] + incl - v;
+    *total = ws[kBandT / 64];
+    __syncthreads();
+    return r;
+}
+
 // Global union-find over input indices (the merge): agent-scope loads, CAS hooks of the larger
 // root under the smaller
+// (parents only decrease along a path; the bound keeps a forest of a run whose barrier gave
+// up, and whose result is discarded, from looping)
 __device__ __forceinline__ int bd_find(int32_t* par, int x) {
-    while (true) {
+    for (int k = 0; k < kBandMaxPoints; ++k) {
         const int p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (p == x) return x;
+        if (p == x || (unsigned)p >= (unsigned)kBandMaxPoints) return x;
         x = p;
     }
+    return x;
+}
+__device__ __forceinline__ double bd_load(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ __forceinline__ void bd_unite(int32_t* par, int a, int b) {
-    while (true) {
+    for (int k = 0; k < kBandMaxPoints; ++k) {
         a = bd_find(par, a);
         b = bd_find(par, b);
         if (a == b) return;
@@ -1280,25 +1344,7 @@ __device__ __forceinline__ void bd_unite(int32_t* par, int a, int b) {
     }
 }
 
-// f(i, x[i], y[i]) for every point i of the partition, kBandU per thread per step with all
-// their loads in flight together (each workgroup reads the whole partition four times)
-constexpr int kBandU = 8;
-template <class F>
-__device__ __forceinline__ void band_pass(const double* __restrict__ x,
-                                          const double* __restrict__ y, int m, F&& f) {
-    for (int i0 = threadIdx.x; i0 < m; i0 += kBandT * kBandU) {
-        double a[kBandU], b[kBandU];
-#pragma unroll
-        for (int u = 0; u < kBandU; ++u) {
-            const int i = i0 + u * kBandT;
-            a[u] = i < m ? x[i] : 0.0;
-            b[u] = i < m ? y[i] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kBandU; ++u)
-            if (i0 + u * kBandT < m) f(i0 + u * kBandT, a[u], b[u]);
-    }
-}
+static_assert(kBandMaxPoints <= (int64_t)kBandMaxWG * kBandT, "one slice point per thread");
 
 __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     const double* __restrict__ x, const double* __restrict__ y, int m, double eps, double eps2,
@@ -1313,18 +1359,25 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     if (g == 0 && tid != kStError) sm_zero_stats(st, mirror, tid);
     if (g == 0 && tid < 2) ba.cnt[tid] = 0;  // (added to after barrier 1 only)
 
-    // ---- bbox and grid (every workgroup alike) ----
+    // ---- this workgroup's slice of the input, one point per thread: the non-finite points'
+    // labels, the slice's bbox published ----
+    const int chunk = (m + G - 1) / G;  // (<= kBandT: m <= kBandMaxPoints = kBandMaxWG * kBandT)
+    const int pi = g * chunk + tid;
+    const bool have = tid < chunk && pi < m;
+    double px = 0.0, py = 0.0;
+    bool fin = false;
+    if (have) {
+        px = x[pi];
+        py = y[pi];
+        fin = isfinite(px) && isfinite(py);
+        if (!fin) {  // nobody's neighbour: noise (minPoints >= 1)
+            cluster[pi] = 0;
+            flag[pi] = DBSCAN_FLAG_NOISE;
+        }
+    }
     {
-        double mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, nfin = 0;
-        band_pass(x, y, m, [&](int, double a, double b) {
-            if (isfinite(a) && isfinite(b)) {
-                mnx = fmin(mnx, a);
-                mxx = fmax(mxx, a);
-                mny = fmin(mny, b);
-                mxy = fmax(mxy, b);
-                nfin += 1;
-            }
-        });
+        double mnx = fin ? px : INFINITY, mxx = fin ? px : -INFINITY;
+        double mny = fin ? py : INFINITY, mxy = fin ? py : -INFINITY, nfin = fin ? 1.0 : 0.0;
         const int w = tid >> 6;
         mnx = wave_min(mnx);
         mxx = wave_max(mxx);
@@ -1340,20 +1393,36 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             L.red[4][w] = nfin;
         }
         __syncthreads();
-        if (tid == 0) {
+        if (tid < 5) {
+            double v = L.red[tid][0];
             for (int k = 1; k < kW; ++k) {
-                L.red[0][0] = fmin(L.red[0][0], L.red[0][k]);
-                L.red[1][0] = fmax(L.red[1][0], L.red[1][k]);
-                L.red[2][0] = fmin(L.red[2][0], L.red[2][k]);
-                L.red[3][0] = fmax(L.red[3][0], L.red[3][k]);
-                L.red[4][0] += L.red[4][k];
+                const double u = L.red[tid][k];
+                v = tid == 4 ? v + u : ((tid & 1) ? fmax(v, u) : fmin(v, u));
             }
-            band_make_grid(L.red[0][0], L.red[1][0], L.red[2][0], L.red[3][0], (int)L.red[4][0],
-                           eps, eps2, &L.G);
+            ba.box[g * 5 + tid] = v;
         }
-        __syncthreads();
     }
     SM_STAMP(1);
+    sp_grid_sync(ba.bar, 1u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(2);
+
+    // ---- the grid from the G partial boxes (one reduction tree: the same grid everywhere) ----
+    if (tid < 5 * 64) {  // wave j reduces quantity j over the G <= 64 boxes, one per lane
+        const int j = tid >> 6;
+        double v = lane < G ? bd_load(ba.box + lane * 5 + j)
+                            : (j == 4 ? 0.0 : ((j & 1) ? -INFINITY : INFINITY));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double u = __shfl_xor(v, o, 64);
+            v = j == 4 ? v + u : ((j & 1) ? fmax(v, u) : fmin(v, u));
+        }
+        if (lane == 0) L.red[j][0] = v;
+    }
+    __syncthreads();
+    if (tid == 0)
+        band_make_grid(L.red[0][0], L.red[1][0], L.red[2][0], L.red[3][0], (int)L.red[4][0], eps,
+                       eps2, &L.G);
+    __syncthreads();
     const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny;
     // the cell of a finite point (quarter bits << 13 above the cell is the caller's)
     const auto cell_of = [&](double a, double b, int& row, int& col, int& quad) {
@@ -1365,138 +1434,264 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         col = qx >> 1;
         quad = ((qy & 1) << 1) | (qx & 1);
     };
-    bool bad = L.G.bad != 0;  // (unreachable for finite bboxes)
+    const bool gbad = L.G.bad != 0 || nf == 0;  // (bad: unreachable for finite bboxes)
+    int prow = -1, pcol = 0, pquad = 0;
+    if (fin && !gbad) cell_of(px, py, prow, pcol, pquad);
+    // the slice's row histogram (LDS), added to the global row counts
+    if (!gbad) {
+        for (int r = tid; r < ny; r += kBandT) L.info[r] = 0u;
+        __syncthreads();
+        if (prow >= 0) atomicAdd(&L.info[prow], 1u);
+        __syncthreads();
+        for (int r = tid; r < ny; r += kBandT)
+            if (L.info[r]) atomicAdd(ba.rowcnt + r, L.info[r]);
+    }
+    SM_STAMP(3);
+    sp_grid_sync(ba.bar, 2u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(4);
 
-    // ---- the bands: points per row, their prefix, this workgroup's rows ----
-    int ra = 0, rb = 0, sa = 0, sb = 0, own0 = 0, own1 = 0;
-    if (!bad && nf > 0) {
-        for (int r = tid; r <= ny; r += kBandT) L.par[r] = 0;
-        __syncthreads();
-        band_pass(x, y, m, [&](int, double a, double b) {
-            if (isfinite(a) && isfinite(b)) {
-                int row, col, quad;
-                cell_of(a, b, row, col, quad);
-                atomicAdd(&L.par[row], 1);
-            }
-        });
-        __syncthreads();
-        {  // exclusive prefix over the rows: par[r] = points in rows < r, par[ny] = nf
+    // ---- the bands: cell ranges of equal cost ----
+    // A cell of row r holding n points costs n a(r) + b.  The work: a point's count and walks,
+    // ~ kBandC0 + the row's points per cell (its stencil's density), so a(r) >= kBandC0 nx +
+    // pts(r) (in units of 1 / nx), and a cell's table entry, b >= nx.  The floors a(r) >= fp
+    // and b >= fr / nx, with fp = 3 Tw / (G Pmax) and fr = 3 Tw / (G Rmax) (Tw: the total work
+    // alone), keep each range within Pmax = kBandCap / 2 own points and Rmax = kBandCells / nx
+    // - 2 own rows (the halo rows take the rest).  Workgroup g owns the cells whose cost offset
+    // (row-major) lies in [g T / G, (g + 1) T / G); it stages the rows of those cells and one
+    // halo row either side.  Dense rows shared by several workgroups are staged by each of
+    // them, with the cells split between them.
+    int ra = 0, rb = 0, sa = 0, sb = 0, p_ra = 0, p_rb = 0;
+    int64_t lo_g = 0, hi_g = 0, c_ra = 0, c_rb = 0, fpt = 0, bcell = 1;
+    bool bad = gbad;
+    if (!gbad) {
+        int64_t* C = reinterpret_cast<int64_t*>(L.rec);  // [ny + 1] cost prefix (until staging)
+        int64_t* ws64 = reinterpret_cast<int64_t*>(&L.red[0][0]);
+        {  // exclusive prefixes over the rows: par[r] = points in rows < r, C[r] = their cost
             constexpr int kRowsPer = (kBandCap + kBandT - 1) / kBandT;
             int v[kRowsPer], sum = 0;
+            int64_t q = 0;
 #pragma unroll
             for (int k = 0; k < kRowsPer; ++k) {
                 const int r = tid * kRowsPer + k;
-                v[k] = r < ny ? L.par[r] : 0;
+                v[k] = r < ny ? (int)__hip_atomic_load(ba.rowcnt + r, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                              : 0;
+                v[k] = min(max(v[k], 0), kBandMaxPoints);  // (a gave-up barrier: stay in bounds)
                 sum += v[k];
+                q += (int64_t)v[k] * ((int64_t)kBandC0 * nx + v[k]);
             }
+            int64_t qtot = 0;
+            (void)bd_scan64(q, ws64, &qtot);
+            const int64_t tw = qtot + (int64_t)nx * nx * ny;
+            const int64_t rmax = max(1, kBandCells / nx - 2), pmax = kBandCap / 2;
+            fpt = (3 * tw + G * pmax - 1) / (G * pmax);
+            const int64_t fr = (3 * tw + G * rmax - 1) / (G * rmax);
+            bcell = max((int64_t)nx, (fr + nx - 1) / nx);
+            const auto a_of = [&](int pts) {
+                return max((int64_t)kBandC0 * nx + pts, fpt);
+            };
+            int64_t cs = 0;
+#pragma unroll
+            for (int k = 0; k < kRowsPer; ++k)
+                if (tid * kRowsPer + k < ny) cs += (int64_t)v[k] * a_of(v[k]) + nx * bcell;
+            int64_t T = 0;
+            int64_t crun = bd_scan64(cs, ws64, &T);
             int tot = 0;
             int run = sm_excl_scan(sum, L.wsc, &tot);
 #pragma unroll
             for (int k = 0; k < kRowsPer; ++k) {
                 const int r = tid * kRowsPer + k;
-                if (r < ny) L.par[r] = run;
+                if (r < ny) {
+                    L.par[r] = run;
+                    C[r] = crun;
+                    crun += (int64_t)v[k] * a_of(v[k]) + nx * bcell;
+                }
                 run += v[k];
             }
-            if (tid == 0) L.par[ny] = nf;
+            if (tid == 0) {
+                L.par[ny] = tot;
+                C[ny] = T;
+            }
             __syncthreads();
+            // (the row counts of every slice add up to nf unless a barrier gave up)
+            if (tot != nf) bad = true;
         }
+        const int64_t T = C[ny];
+        lo_g = (int64_t)g * T / G;
+        hi_g = g + 1 == G ? T : (int64_t)(g + 1) * T / G;
         if (tid < 2) {
-            // band g: the rows from the first row whose cost prefix reaches g / G of the total;
-            // a row costs its points plus its cells (both fill a band's tables of kBandCap)
-            const int64_t total = (int64_t)nf + (int64_t)ny * nx;
-            const int64_t want = (int64_t)(g + tid) * total / G;
+            // the last row r with C[r] <= the offset (costs are > 0: C increases strictly)
+            const int64_t want = tid ? hi_g : lo_g;
             int lo = 0, hi = ny;
             while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if ((int64_t)L.par[mid] + (int64_t)mid * nx >= want) hi = mid; else lo = mid + 1;
+                const int mid = (lo + hi + 1) >> 1;
+                if (C[mid] <= want) lo = mid; else hi = mid - 1;
             }
-            L.meta[tid] = g + tid == G ? ny : lo;
+            L.meta[tid] = lo;
+        }
+        // each of the slice's rows: its piece of the row-sorted records claimed (info: cursor)
+        for (int r = tid; r < ny; r += kBandT) {
+            const uint32_t k = L.info[r];
+            if (k) L.info[r] = (uint32_t)L.par[r] + atomicAdd(ba.rowcur + r, k);
         }
         __syncthreads();
         ra = L.meta[0];
-        rb = L.meta[1];
-        sa = ra > 0 ? ra - 1 : 0;
-        sb = rb < ny ? rb + 1 : ny;
-        if (ra >= rb) sa = sb = ra;  // (an empty band stages nothing)
-        own0 = L.par[ra];
-        own1 = L.par[rb];
-        const int staged = L.par[sb] - L.par[sa];
-        if (staged > kBandCap || (sb - sa) * nx > kBandCells) bad = true;
-        __syncthreads();
+        rb = L.meta[1];  // (ny: the range runs to the end)
+        if (lo_g < hi_g) {
+            sa = ra > 0 ? ra - 1 : 0;
+            sb = rb + 2 < ny ? rb + 2 : ny;
+        } else {
+            sa = sb = ra;  // (an empty range stages nothing)
+        }
+        c_ra = C[ra];
+        p_ra = L.par[ra + 1] - L.par[ra];
+        c_rb = rb < ny ? C[rb] : T;
+        p_rb = rb < ny ? L.par[rb + 1] - L.par[rb] : 0;
+        // the slice's records to their rows' pieces
+        if (prow >= 0) {
+            const uint32_t k = atomicAdd(&L.info[prow], 1u);
+            if (k < (uint32_t)L.par[prow + 1] && k < (uint32_t)m) {
+                ba.rxy[k] = make_double2(px, py);
+                ba.ridx[k] = pi;
+            }
+        }
     }
-    const int srows = sb - sa, scells = srows * nx;
-    const int S = (bad || nf == 0) ? 0 : L.par[sb] - L.par[sa];
-    if (bad && tid == 0) {
+    const int row0 = bad ? 0 : L.par[sa];
+    int S = bad ? 0 : L.par[sb] - L.par[sa];
+    if (S > kBandCap || (sb - sa) * nx > kBandCells) {  // over the staging capacity
+        bad = true;
+        S = 0;
+    }
+    if (bad && !gbad && tid == 0) {
         __hip_atomic_store(st + kStError, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (mirror)
             __hip_atomic_store(reinterpret_cast<int32_t*>(mirror + kMiscState) + kStError, 3,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __syncthreads();
+    SM_STAMP(5);
+    sp_grid_sync(ba.bar, 3u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(6);
+    // (every workgroup has read the row counts and claimed its pieces: this workgroup's share
+    // of them zeroed for the next launch)
+    for (int r = g * kBandT + tid; r < kBandCap; r += G * kBandT) {
+        ba.rowcnt[r] = 0u;
+        ba.rowcur[r] = 0u;
+    }
 
-    SM_STAMP(2);
-    // ---- stage the rows [sa, sb): counting sort by staged cell ----
-    int occupied = 0;
+    // ---- stage the rows [sa, sb): their records, a counting sort by staged cell ----
+    const int srows = sb - sa, scells = srows * nx;
+    constexpr int kStPer = kBandCap / kBandT;
+    // each thread's staged points in registers: the fp32 record and the info word (input index
+    // << 16 | quadrant << 13 | staged cell; ~0u: none)
+    float2 srec[kStPer];
+    uint32_t sinf[kStPer];
     if (S > 0) {
-        for (int c = tid; c < scells; c += kBandT) L.info[c] = 0;
-        __syncthreads();
-        band_pass(x, y, m, [&](int, double a, double b) {
-            if (isfinite(a) && isfinite(b)) {
-                int row, col, quad;
-                cell_of(a, b, row, col, quad);
-                if (row >= sa && row < sb) atomicAdd(&L.info[(row - sa) * nx + col], 1u);
+        for (int cc = tid; cc < scells; cc += kBandT) L.info[cc] = 0u;
+#pragma unroll
+        for (int k = 0; k < kStPer; ++k) {
+            const int j = tid + k * kBandT;
+            sinf[k] = ~0u;
+            srec[k] = make_float2(0.f, 0.f);
+            if (j < S) {
+                const double2 r = ba.rxy[row0 + j];
+                const int i = ba.ridx[row0 + j];
+                if (i >= 0 && i < m && isfinite(r.x) && isfinite(r.y)) {
+                    int row, col, quad;
+                    cell_of(r.x, r.y, row, col, quad);
+                    if (row >= sa && row < sb) {  // (always, unless a barrier gave up)
+                        sinf[k] = ((uint32_t)i << 16) | ((uint32_t)quad << 13) |
+                                  (uint32_t)((row - sa) * nx + col);
+                        srec[k] = make_float2((float)((r.x * 0.5 - L.G.cx2) * L.G.invs),
+                                              (float)((r.y * 0.5 - L.G.cy2) * L.G.invs));
+                    }
+                }
             }
-        });
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kStPer; ++k)
+            if (sinf[k] != ~0u) atomicAdd(&L.info[sinf[k] & kCellMask], 1u);
         __syncthreads();
         {
             constexpr int kCellPer = (kBandCells + kBandT - 1) / kBandT;
             int cnt[kCellPer], sum = 0;
 #pragma unroll
             for (int k = 0; k < kCellPer; ++k) {
-                const int c = tid * kCellPer + k;
-                cnt[k] = c < scells ? (int)L.info[c] : 0;
+                const int cc = tid * kCellPer + k;
+                cnt[k] = cc < scells ? (int)L.info[cc] : 0;
                 sum += cnt[k];
             }
             int tot = 0;
             int run = sm_excl_scan(sum, L.wsc, &tot);
 #pragma unroll
             for (int k = 0; k < kCellPer; ++k) {
-                const int c = tid * kCellPer + k;
-                if (c < scells) {
-                    L.par[c] = run;
-                    L.cst[c] = (uint16_t)run;
-                    // owned cells only (the statistics' occupied cells)
-                    const int row = sa + c / nx;
-                    occupied += (cnt[k] > 0 && row >= ra && row < rb) ? 1 : 0;
+                const int cc = tid * kCellPer + k;
+                if (cc < scells) {
+                    L.par[cc] = run;
+                    L.cst[cc] = (uint16_t)run;
                 }
                 run += cnt[k];
             }
-            if (tid == 0) L.cst[scells] = (uint16_t)S;
+            if (tid == 0) L.cst[scells] = (uint16_t)tot;
+            S = tot;  // (the records placed: S unless a barrier gave up)
         }
         __syncthreads();
-        band_pass(x, y, m, [&](int i, double a, double b) {
-            if (isfinite(a) && isfinite(b)) {
-                int row, col, quad;
-                cell_of(a, b, row, col, quad);
-                if (row >= sa && row < sb) {
-                    const int c = (row - sa) * nx + col;
-                    const int s = atomicAdd(&L.par[c], 1);
-                    L.rec[s] = make_float2((float)((a * 0.5 - L.G.cx2) * L.G.invs),
-                                           (float)((b * 0.5 - L.G.cy2) * L.G.invs));
-                    L.info[s] = ((uint32_t)i << 16) | ((uint32_t)quad << 13) | (uint32_t)c;
+#pragma unroll
+        for (int k = 0; k < kStPer; ++k) {
+            if (sinf[k] != ~0u) {
+                const int s = atomicAdd(&L.par[sinf[k] & kCellMask], 1);
+                L.rec[s] = srec[k];
+                L.info[s] = sinf[k];
+            }
+        }
+        // own cells [ca, cb) (staged numbering): the first cells of rows ra / rb whose cost
+        // offset reaches lo_g / hi_g, one wave each
+        if (tid < 128) {
+            const int w = tid >> 6, lane = tid & 63;
+            const int row = w ? rb : ra;
+            int res = scells;  // (rb == ny: to the end)
+            if (row < ny) {
+                const int64_t target = w ? hi_g : lo_g;
+                const int pr = w ? p_rb : p_ra;
+                const int64_t ar = max((int64_t)kBandC0 * nx + pr, fpt);
+                int64_t base = w ? c_rb : c_ra;
+                const int c0 = (row - sa) * nx;
+                res = c0 + nx;  // (none in the row: the next row's first cell)
+                for (int j0 = 0; j0 < nx; j0 += 64) {
+                    const int j = j0 + lane;
+                    int64_t cost = 0;
+                    if (j < nx) {
+                        const int n = (int)L.cst[c0 + j + 1] - (int)L.cst[c0 + j];
+                        cost = (int64_t)n * ar + bcell;
+                    }
+                    int64_t incl = cost;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const int64_t t = __shfl_up(incl, d, 64);
+                        if (lane >= d) incl += t;
+                    }
+                    const uint64_t hit = __ballot(j < nx && base + incl - cost >= target);
+                    if (hit) {
+                        res = c0 + j0 + __ffsll((unsigned long long)hit) - 1;
+                        break;
+                    }
+                    base += __shfl(incl, 63, 64);
                 }
             }
-        });
+            if (lane == 0) L.meta[4 + w] = res;
+        }
         __syncthreads();
     }
-    SM_STAMP(3);
+    SM_STAMP(7);
+    BAND_WG(0, wall_clock64());
     // the staged stencil context: rows [sa, sb) as rows 0 .. srows - 1
     const SmCtx c{x, y, eps2, L.G.lo, L.G.hi, nx, srows, L.G.exact_only != 0};
-    // own slots: the rows [ra, rb)
-    const int s0 = S > 0 ? (int)L.cst[(ra - sa) * nx] : 0;
-    const int s1 = S > 0 ? (int)L.cst[(rb - sa) * nx] : 0;
-    (void)own0;
-    (void)own1;
+    // own slots: the cells [ca, cb)
+    const int ca = S > 0 ? L.meta[4] : 0, cb = S > 0 ? L.meta[5] : 0;
+    const int s0 = S > 0 ? (int)L.cst[ca] : 0;
+    const int s1 = S > 0 ? (int)L.cst[cb] : 0;
+    int occupied = 0;
+    for (int cc = ca + tid; cc < cb; cc += kBandT) occupied += L.cst[cc + 1] > L.cst[cc] ? 1 : 0;
 
     // ---- count (own points): a thread each when they fill a quarter of the workgroup, else
     // a wave each (64 candidates per step, ballot counts) ----
@@ -1520,11 +1715,13 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             }
         }
     }
-    SM_STAMP(4);
+    SM_STAMP(8);
+    BAND_WG(1, wall_clock64());
     // this workgroup's share of the root words, zeroed for the roots phase
     for (int k = g * kBandT + tid; k < (m + 31) / 32; k += G * kBandT) ba.rbits[k] = 0u;
-    sp_grid_sync(ba.bar, (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(5);
+    sp_grid_sync(ba.bar, 4u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(9);
+    BAND_WG(2, wall_clock64());
 
     // ---- union: the staged core flags, own cores' walks, the forest published ----
     {
@@ -1545,12 +1742,15 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     const bool quarters = L.G.clique != 0;
     const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
     const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy - (double)sa;  // (staged rows)
+    // (row-major items: the lanes of a wave walk one stencil row of consecutive points, mostly
+    // of one cell, so their LDS reads coincide: walks 107 -> 58 us per workgroup at 65536
+    // points against point-major items)
     for (int it = tid; it < (s1 - s0) * 3; it += kBandT) {
-        const int i = it / 3;
-        if (L.core[s0 + i]) sm_union_walk(L, c, s0 + i, it - 3 * i, quarters, reach_kx, reach_ky);
+        const int d = it / (s1 - s0), i = it - d * (s1 - s0);
+        if (L.core[s0 + i]) sm_union_walk(L, c, s0 + i, d, quarters, reach_kx, reach_ky);
     }
     __syncthreads();
-    SM_STAMP(6);
+    SM_STAMP(10);
     uint32_t* mine = ba.pairs + (int64_t)g * kBandCap;
     for (int p = tid; p < S; p += kBandT) {
         if (!L.core[p] || L.par[p] == p) continue;
@@ -1561,18 +1761,21 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     }
     __syncthreads();
     const int npairs = L.meta[2];
-    SM_STAMP(7);
-    sp_grid_sync(ba.bar, 2u * (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(8);
+    SM_STAMP(11);
+    BAND_WG(3, wall_clock64());
+    BAND_WG(4, s1 - s0);
+    BAND_WG(5, S);
+    sp_grid_sync(ba.bar, 5u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(12);
 
     // ---- merge: this workgroup's pairs into the global union-find over input indices ----
     for (int k = tid; k < npairs; k += kBandT) {
         const uint32_t w = mine[k];
         bd_unite(ba.par, (int)(w >> 16), (int)(w & 0xFFFFu));
     }
-    SM_STAMP(9);
-    sp_grid_sync(ba.bar, 3u * (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(10);
+    SM_STAMP(13);
+    sp_grid_sync(ba.bar, 6u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(14);
 
     // ---- roots of the own cores (read-only walks: every union is done) ----
     for (int p = s0 + tid; p < s1; p += kBandT) {
@@ -1583,9 +1786,9 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         ba.lab[v] = r;
         if (r == v) atomicOr(&ba.rbits[v >> 5], 1u << (v & 31));
     }
-    SM_STAMP(11);
-    sp_grid_sync(ba.bar, 4u * (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(12);
+    SM_STAMP(15);
+    sp_grid_sync(ba.bar, 7u * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(16);
 
     // ---- numbering and labels ----
     const int nw = (m + 31) / 32;
@@ -1612,7 +1815,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         }
         __syncthreads();
     }
-    SM_STAMP(13);
+    SM_STAMP(17);
     const auto cluster_of = [&](uint32_t s) {
         return L.wrank[s >> 5] + __popc(L.rbits[s >> 5] & ((1u << (s & 31u)) - 1u)) + 1;
     };
@@ -1653,14 +1856,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             flag[v] = f;
         }
     }
-    if (g == G - 1) {  // the non-finite points: nobody's neighbour, noise (minPoints >= 1)
-        for (int i = tid; i < m; i += kBandT)
-            if (!(isfinite(x[i]) && isfinite(y[i]))) {
-                cluster[i] = 0;
-                flag[i] = DBSCAN_FLAG_NOISE;
-            }
-    }
-    SM_STAMP(14);
+    SM_STAMP(18);
     // ---- statistics (workgroup 0) and the barrier reset (the last workgroup to leave) ----
     if (g == 0 && tid == 0) {
         sm_set_stat(st, mirror, kStNf, nf);
@@ -1687,7 +1883,12 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
 
 #if DBSCAN_AB_STAMPS
 extern "C" int dbscan_ab_small_stamps(long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), 16 * sizeof(long long)) == hipSuccess
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), 24 * sizeof(long long)) == hipSuccess
+               ? 0 : -1;
+}
+extern "C" int dbscan_ab_band_wg(long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_wg), 64 * 8 * sizeof(long long)) ==
+                   hipSuccess
                ? 0 : -1;
 }
 #endif
@@ -1762,13 +1963,16 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     (void)n;
     // scratch: barrier words (zero between launches), counters, per input index core flags,
     // labels and the union-find, root words, the published pairs
-    constexpr size_t kHead = 512;  // bar[2] at 0, cnt[2] at 64, npairs[kBandMaxWG] at 128
+    // (zeroed once, then by the kernel itself: bar[2] at 0, cnt[2] at 64, npairs[kBandMaxWG]
+    // at 128, the row counts and claims; then the slices' boxes)
+    constexpr size_t kHead = 512, kRows = (size_t)kBandCap * 4, kZero = kHead + 2 * kRows;
+    constexpr size_t kBox = (size_t)kBandMaxWG * 5 * 8;
     const size_t words = (size_t)(kBandMaxPoints / 32 + 1);
-    const size_t bytes = kHead + (size_t)kBandMaxPoints * (1 + 4 + 4) + words * 4 +
-                         (size_t)kBandMaxWG * kBandCap * 4;
+    const size_t bytes = kZero + kBox + (size_t)kBandMaxPoints * (1 + 4 + 4 + 16 + 4) +
+                         words * 4 + (size_t)kBandMaxWG * kBandCap * 4;
     if (ws.band.bytes < bytes || !ws.band_ready) {
         char* p = static_cast<char*>(ws.band.ensure(bytes));
-        DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, kHead, s));  // the barrier words, once
+        DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, kZero, s));
         ws.band_ready = true;
     }
     char* base = static_cast<char*>(ws.band.p);
@@ -1776,7 +1980,14 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     ba.bar = reinterpret_cast<uint32_t*>(base);
     ba.cnt = reinterpret_cast<int32_t*>(base + 64);
     ba.npairs = reinterpret_cast<int32_t*>(base + 128);
-    char* q = base + kHead;
+    ba.rowcnt = reinterpret_cast<uint32_t*>(base + kHead);
+    ba.rowcur = reinterpret_cast<uint32_t*>(base + kHead + kRows);
+    ba.box = reinterpret_cast<double*>(base + kZero);
+    char* q = base + kZero + kBox;
+    ba.rxy = reinterpret_cast<double2*>(q);
+    q += (size_t)kBandMaxPoints * 16;
+    ba.ridx = reinterpret_cast<int32_t*>(q);
+    q += (size_t)kBandMaxPoints * 4;
     ba.core = reinterpret_cast<uint8_t*>(q);
     q += kBandMaxPoints;
     ba.lab = reinterpret_cast<int32_t*>(q);
@@ -1805,6 +2016,7 @@ bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws) {
     int32_t* v = reinterpret_cast<int32_t*>(ws.stats_host + kMiscState);
     if (ws.recall_band) {  // a band fit: barrier gave up (2) or a band overflowed (3)
         if (v[kStError] != 2 && v[kStError] != 3) return false;
+        ws.band_ready = false;  // (a barrier that gave up may leave row counts: zeroed again)
         FitArgs b{r.x, r.y, nullptr, r.n, r.eps, r.min_points, r.mode, r.cluster, r.flag,
                   nullptr, nullptr};
         b.small_max = 0;  // the tiled pipeline (no LDS fit, no band fit)

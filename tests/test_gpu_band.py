@@ -60,7 +60,9 @@ def test_band_sizes_vs_oracle(dm, mode):
             tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
             cl, fl, k = D.fit_tensors(tx, ty, eps, mp, mode, h)
             _eq((cl.cpu().numpy(), fl.cpu().numpy(), k), ref, f"device m={m}")
-        assert h.spread_fallbacks() - before <= 4
+        # (the densest sets stage rows of > kBandCap / 3 points: those fits take the tiled
+        # recall; parity above covers both forms)
+        assert h.spread_fallbacks() - before <= 8
     finally:
         h.close()
 

@@ -19,7 +19,7 @@ f = lib.dbscan_ab_small_stamps
 f.argtypes = [ctypes.c_void_p]
 h = dbscan_amd.Handle(0)
 h.set_small_max(8192)  # every size through the one-workgroup kernel
-buf = (ctypes.c_longlong * 16)()
+buf = (ctypes.c_longlong * 24)()
 for m in (250, 2000, 8192):
     tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
     cl = torch.empty(m, dtype=torch.int32, device="cuda")

@@ -25,7 +25,7 @@ if f is not None:
 h = dbscan_amd.Handle(0)
 h.set_small_max(8192)
 h.set_spread_min(0)
-buf = (ctypes.c_longlong * 16)()
+buf = (ctypes.c_longlong * 24)()
 for m in [int(a) for a in (sys.argv[1:] or ["2000", "8192"])]:
     tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
     cl = torch.empty(m, dtype=torch.int32, device="cuda")
