@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
             sm_set_stat(st, mirror, kStClusters, nclust);
             sm_set_stat(st, mirror, kStCells, nf > 0 ? occ : 0);
             GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
-                          1u, 1u, 0};
+                          1u, 1u, L.G.clique};
             *gp = gg;
             if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
         }
@@ -1867,7 +1867,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                                                                      __HIP_MEMORY_SCOPE_AGENT)
                                                  : 0);
         GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
-                      1u, 1u, 0};
+                      1u, 1u, L.G.clique};
         *gp = gg;
         if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
     }

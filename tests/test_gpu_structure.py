@@ -28,6 +28,7 @@ def dm():
 @pytest.fixture(scope="module")
 def handle(dm):
     h = dm.Handle(0)
+    h.set_band_max(0)  # (this module drives the tiled pipeline; tests/test_gpu_band.py the band)
     yield h
     h.close()
 
@@ -137,6 +138,13 @@ def test_lattice_pairs_at_exactly_eps(dm, handle, div, mp):
     p = rng.permutation(x.size)
     _check(dm, handle, x[p].copy(), y[p].copy(), eps, mp)
     assert handle.stats()["clique"] == 1
+    # the same lattices through the band LDS fit (its own fp32 pre-filter and exact fallback)
+    hb = dm.Handle(0)
+    try:
+        _check(dm, hb, x[p].copy(), y[p].copy(), eps, mp)
+        assert hb.stats()["clique"] == 1
+    finally:
+        hb.close()
 
 
 @pytest.mark.parametrize("offset,eps", [(1e12, 1e-3), (-3e9, 0.05), (0.0, 1e-150)])
