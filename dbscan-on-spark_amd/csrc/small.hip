@@ -1187,7 +1187,9 @@ constexpr int kBandT = 1024;
 constexpr int kBandCap = 7168;    // staged points per workgroup (and staged cells)
 constexpr int kBandCells = kBandCap;
 constexpr int kBandMaxWG = 64;
-constexpr int kBandC0 = 2;  // a point's count + walk work without neighbours, in cell densities
+// a point's count + walk work without neighbours, in cell densities (0, 1 and 4 measured within
+// 2% of 2 at 12k-65k points)
+constexpr int kBandC0 = 2;
 constexpr int kBandWords = (int)(kBandMaxPoints / 32);
 static_assert(kBandMaxPoints <= 65536, "16-bit visit indices");
 static_assert(kBandCells <= 8191, "13-bit cells in info");
