@@ -68,8 +68,9 @@ __device__ long long g_sm_stamps[24];
     do {                                                                          \
         if (threadIdx.x == 0 && blockIdx.x == 0) g_sm_stamps[(k)] = wall_clock64(); \
     } while (0)
-// band_fit_kernel, every workgroup: [g][0..5] = clock at the stage's end, the count's end,
-// after barrier 1, at barrier 2's arrival; own points, staged points
+// band_fit_kernel, every workgroup: [g][0..7] = clock at the stage's end, the count's end,
+// after barrier 1, at barrier 2's arrival; own points, staged points; clock before and after
+// the union walks
 __device__ long long g_band_wg[64 * 8];
 #define BAND_WG(k, v)                                           \
     do {                                                        \
@@ -1638,6 +1639,19 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             S = tot;  // (the records placed: S unless a barrier gave up)
         }
         __syncthreads();
+        // placed one quadrant after the other: each cell's slots grouped by quarter, in order
+        for (uint32_t qq = 0; qq < 3u; ++qq) {
+#pragma unroll
+            for (int k = 0; k < kStPer; ++k) {
+                if (sinf[k] != ~0u && ((sinf[k] >> 13) & 3u) == qq) {
+                    const int s = atomicAdd(&L.par[sinf[k] & kCellMask], 1);
+                    L.rec[s] = srec[k];
+                    L.info[s] = sinf[k];
+                    sinf[k] = ~0u;
+                }
+            }
+            __syncthreads();
+        }
 #pragma unroll
         for (int k = 0; k < kStPer; ++k) {
             if (sinf[k] != ~0u) {
@@ -1741,18 +1755,144 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     }
     if (tid == 0) L.meta[2] = 0;
     __syncthreads();
+    BAND_WG(6, wall_clock64());
     const bool quarters = L.G.clique != 0;
     const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
     const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy - (double)sa;  // (staged rows)
-    // (row-major items: the lanes of a wave walk one stencil row of consecutive points, mostly
-    // of one cell, so their LDS reads coincide: walks 107 -> 58 us per workgroup at 65536
-    // points against point-major items)
-    for (int it = tid; it < (s1 - s0) * 3; it += kBandT) {
+    // Quarter-level unions (clique grids: a quarter cell's cores are one clique; the staged
+    // slots of a cell are grouped by quarter): each own core chained to the previous core of
+    // its quarter; then for each own quarter holding a core and each of the 12 quarters after
+    // it (quarter-grid offsets within 2, row-major order) a core pair within eps searched and
+    // united -- adjacent quarters first, then (after a barrier) the distance-2 ones, skipped
+    // when already in one set, their far cores pruned by the other quarter's box.  Every
+    // quarter pair is tested by the owner of its smaller quarter, which stages both.  Against
+    // the per-core stencil walks: 133 / 147 / 171 / 191 -> 112 / 138 / 155 / 178 us per kernel
+    // at 12k / 20k / 40k / 65k points (the walks repeat each quarter's work for every core).
+    bool walked = false;
+    if (quarters) {
+        uint32_t* qlist = L.rbits;  // (rbits and wrank are free until the numbering)
+        constexpr int kQMax = 2 * kBandWords;
+        static_assert(sizeof(L.rbits) + sizeof(L.wrank) == kQMax * sizeof(uint32_t) &&
+                          offsetof(BandLds, wrank) == offsetof(BandLds, rbits) + sizeof(L.rbits),
+                      "qlist spans rbits and wrank");
+        if (tid == 0) L.meta[6] = 0;
+        __syncthreads();
+        for (int sl = s0 + tid; sl < s1; sl += kBandT) {
+            const uint32_t inf = L.info[sl];
+            const int cell = (int)(inf & kCellMask);
+            const uint32_t qd = (inf >> 13) & 3u;
+            const int cb0 = L.cst[cell];
+            const bool start = sl == cb0 || ((L.info[sl - 1] >> 13) & 3u) != qd;
+            // each core chained to the previous core of its quarter (one union per thread)
+            if (L.core[sl]) {
+                for (int t = sl - 1; t >= cb0 && ((L.info[t] >> 13) & 3u) == qd; --t)
+                    if (L.core[t]) {
+                        (void)sm_unite_from(L.par, L.info, t, sl);
+                        break;
+                    }
+            }
+            if (!start) continue;
+            const int ce = L.cst[cell + 1];
+            int e = sl + 1;
+            bool any = L.core[sl] != 0;
+            while (e < ce && ((L.info[e] >> 13) & 3u) == qd) {
+                any = any || L.core[e] != 0;
+                ++e;
+            }
+            if (any) {
+                const int k = atomicAdd(&L.meta[6], 1);
+                if (k < kQMax) qlist[k] = (uint32_t)sl | ((uint32_t)e << 16);
+            }
+        }
+        __syncthreads();
+        const int nq = L.meta[6];
+        if (nq <= kQMax) {
+            walked = true;
+            const auto run_of = [&](int cell, uint32_t qd, int& b, int& e) {
+                int lo = L.cst[cell], hi = L.cst[cell + 1];
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (((L.info[mid] >> 13) & 3u) < qd) lo = mid + 1; else hi = mid;
+                }
+                b = lo;
+                hi = L.cst[cell + 1];
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (((L.info[mid] >> 13) & 3u) <= qd) lo = mid + 1; else hi = mid;
+                }
+                e = lo;
+            };
+            for (int pass = 0; pass < 2; ++pass) {
+                const int K = pass ? 8 : 4;
+                for (int it = tid; it < nq * K; it += kBandT) {
+                    const int k = it / nq, qi = it - k * nq;
+                    const uint32_t rq = qlist[qi];
+                    const int qs = (int)(rq & 0xFFFFu), qe = (int)(rq >> 16);
+                    const uint32_t inf = L.info[qs];
+                    const int cell = (int)(inf & kCellMask);
+                    const int qd = (int)((inf >> 13) & 3u);
+                    const int cy = cell / nx, cx = cell - cy * nx;
+                    // forward offsets (dx, dy): adjacent (1,0) (-1,1) (0,1) (1,1); distance 2
+                    // (2,0) (-2,1) (2,1) (-2,2) (-1,2) (0,2) (1,2) (2,2)
+                    const int dx = pass ? (k == 0 ? 2 : (k == 1 ? -2 : (k == 2 ? 2 : k - 5)))
+                                        : (k == 0 ? 1 : k - 2);
+                    const int dy = pass ? (k == 0 ? 0 : (k < 3 ? 1 : 2)) : (k == 0 ? 0 : 1);
+                    const int hx = 2 * cx + (qd & 1) + dx, hy = 2 * cy + (qd >> 1) + dy;
+                    if (hx < 0 || hx >= 2 * nx || hy < 0 || hy >= 2 * srows) continue;
+                    int b2, e2;
+                    run_of((hy >> 1) * nx + (hx >> 1), (uint32_t)(((hy & 1) << 1) | (hx & 1)), b2,
+                           e2);
+                    int fb = -1;
+                    for (int t = b2; t < e2; ++t)
+                        if (L.core[t]) {
+                            fb = t;
+                            break;
+                        }
+                    if (fb < 0) continue;
+                    int fa = qs;
+                    while (!L.core[fa]) ++fa;
+                    if (sm_find(L.par, fa) == sm_find(L.par, fb)) continue;
+                    // the other quarter's box in the records' cell units, and a squared reach
+                    // over the fp32 threshold with the records' error margin
+                    const double bx0 = 0.5 * (double)hx - reach_kx;
+                    const double by0 = 0.5 * (double)hy - reach_ky;
+                    bool found = false;
+                    for (int a = fa; a < qe && !found; ++a) {
+                        if (!L.core[a]) continue;
+                        const float2 ra = L.rec[a];
+                        if (pass && !c.exact_only) {
+                            const float ddx = (float)fmax(0.0, fmax(bx0 - (double)ra.x,
+                                                                    (double)ra.x - (bx0 + 0.5)));
+                            const float ddy = (float)fmax(0.0, fmax(by0 - (double)ra.y,
+                                                                    (double)ra.y - (by0 + 0.5)));
+                            const float mg = (fabsf(ra.x) + fabsf(ra.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
+                            const float rr = (sqrtf(c.hi) + mg) * (sqrtf(c.hi) + mg);
+                            if (ddx * ddx + ddy * ddy > rr) continue;
+                        }
+                        for (int b = fb; b < e2; ++b) {
+                            if (!L.core[b]) continue;
+                            if (sm_pair(L, c, a, ra, b, L.rec[b])) {
+                                (void)sm_unite_from(L.par, L.info, a, b);
+                                found = true;
+                                break;
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    // (other grids, or more own quarters than the list holds: per-core stencil walks; row-
+    // major items: the lanes of a wave walk one stencil row of consecutive points, mostly of
+    // one cell, so their LDS reads coincide: 107 -> 58 us per workgroup at 65536 points)
+    for (int it = walked ? 0x7FFFFFFF : tid; it < (s1 - s0) * 3; it += kBandT) {
         const int d = it / (s1 - s0), i = it - d * (s1 - s0);
         if (L.core[s0 + i]) sm_union_walk(L, c, s0 + i, d, quarters, reach_kx, reach_ky);
     }
     __syncthreads();
     SM_STAMP(10);
+    BAND_WG(7, wall_clock64());
     uint32_t* mine = ba.pairs + (int64_t)g * kBandCap;
     for (int p = tid; p < S; p += kBandT) {
         if (!L.core[p] || L.par[p] == p) continue;

@@ -42,7 +42,11 @@ for m in [int(a) for a in (sys.argv[1:] or ["12000", "20000", "40000", "65536"])
     a = np.array(list(wg), dtype=np.int64).reshape(64, 8)
     tc = (a[:, 1] - a[:, 0]) / 100.0
     tw = (a[:, 3] - a[:, 2]) / 100.0
-    for name, t in (("count", tc), ("walks", tw)):
+    tl = (a[:, 6] - a[:, 2]) / 100.0
+    tu = (a[:, 7] - a[:, 6]) / 100.0
+    tp = (a[:, 3] - a[:, 7]) / 100.0
+    for name, t in (("count", tc), ("core load + walks + publish", tw), ("core load", tl),
+                    ("walks alone", tu), ("publish", tp)):
         k = int(np.argmax(t))
         print(f"  {name} per workgroup: max {t.max():.1f} us (wg {k}: own {a[k, 4]}, staged "
               f"{a[k, 5]}), median {np.median(t):.1f}; slowest 5: " +
