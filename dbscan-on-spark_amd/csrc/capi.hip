@@ -187,6 +187,7 @@ struct dbscan_handle {
     int64_t small_max = DBSCAN_SMALL_DEFAULT_POINTS;  // one-workgroup fits up to this many points
     int64_t spread_min = DBSCAN_SPREAD_DEFAULT_POINTS;  // LDS fits from here: several workgroups
     int64_t band_max = DBSCAN_BAND_DEFAULT_POINTS;      // band fits above the LDS capacity
+    int64_t band_min = DBSCAN_BAND_MIN_DEFAULT_POINTS;  // ... and inside it from this many points
     bool pending = false;             // an asynchronous fit whose stats are not read yet
     int32_t* pending_nk = nullptr;    // ... and the device word its cluster count went to
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
@@ -398,6 +399,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
         a.band_max = h->band_max;
+        a.band_min = h->band_min;
         h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
@@ -436,6 +438,7 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
         a.band_max = h->band_max;
+        a.band_min = h->band_min;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         h->prof.flush();
@@ -484,6 +487,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
             a.small_max = h->small_max;
             a.spread_min = h->spread_min;
         a.band_max = h->band_max;
+        a.band_min = h->band_min;
             h->prepared = false;
             dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
             DBSCAN_HIP_CHECK(
@@ -520,6 +524,7 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
         a.small_max = h->small_max;
         a.spread_min = h->spread_min;
         a.band_max = h->band_max;
+        a.band_min = h->band_min;
         h->prepared = false;
         int64_t k = dbscan::run_fit(h->stream, h->ws, &h->prof, a, &h->stats, &h->slab);
         {
@@ -1085,6 +1090,17 @@ int64_t dbscan_set_band_max(dbscan_handle* h, int64_t max_points) {
     std::lock_guard<std::mutex> lk(h->mu);
     const int64_t prev = h->band_max;
     h->band_max = std::max<int64_t>(0, std::min<int64_t>(max_points, DBSCAN_BAND_MAX_POINTS));
+    return prev;
+}
+
+int64_t dbscan_set_band_min(dbscan_handle* h, int64_t min_points) {
+    if (!h) {
+        set_err("NULL handle");
+        return DBSCAN_EARG;
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int64_t prev = h->band_min;
+    h->band_min = std::max<int64_t>(min_points, 0);
     return prev;
 }
 

@@ -314,6 +314,7 @@ struct FitArgs {
     // ... and, when small_max covers the LDS capacity, fits up to band_max points run the band
     // form (small.hip band_fit_kernel)
     int64_t band_max = 0;
+    int64_t band_min = 0;  // (LDS-sized fits of >= band_min points also take the band form)
     // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
     const BatchFit* batch = nullptr;
 };

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("dbscan_set_small_max", _i64, [_vp, _i64]),
     ("dbscan_set_spread_min", _i64, [_vp, _i64]),
     ("dbscan_set_band_max", _i64, [_vp, _i64]),
+    ("dbscan_set_band_min", _i64, [_vp, _i64]),
     ("dbscan_set_spread_spin_limit", _i64, [_vp, _i64]),
     ("dbscan_spread_fallbacks", _i64, [_vp]),
     ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
@@ -187,6 +188,14 @@ class Handle:
         """Full fits above the LDS capacity and up to max_points points run the band form
         (one launch; 0: never).  Returns the previous value."""
         r = load().dbscan_set_band_max(self._h, int(max_points))
+        if r < 0:
+            check(int(r))
+        return int(r)
+
+    def set_band_min(self, min_points: int) -> int:
+        """Fits inside the LDS capacity of >= min_points points also take the band form (0:
+        every eligible fit; 1 << 30: none).  Returns the previous value."""
+        r = load().dbscan_set_band_min(self._h, int(min_points))
         if r < 0:
             check(int(r))
         return int(r)

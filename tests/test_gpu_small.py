@@ -42,25 +42,30 @@ def _eq(got, ref, what=""):
 
 
 ONE_WG = 1 << 30  # dbscan_set_spread_min: every LDS fit on one workgroup
+NO_BAND = 1 << 30  # dbscan_set_band_min: no LDS-sized fit takes the band form
+BAND_MIN = 3072  # DBSCAN_BAND_MIN_DEFAULT_POINTS
 
 
 def _lds_forms(handle):
-    """(name, spread_min) of the two LDS fit forms: one workgroup, spread from 0 points"""
-    return (("small", ONE_WG), ("spread", 0))
+    """(name, spread_min, band_min) of the three one-launch forms for LDS-sized fits: one
+    workgroup, spread from 0 points, the band form from 1 point (where eligible)"""
+    return (("small", ONE_WG, NO_BAND), ("spread", 0, NO_BAND), ("band", 0, 0))
 
 
 def _both_paths(dm, handle, x, y, eps, mp, mode, ref):
     """The one-workgroup fit, the spread fit and the tiled pipeline, each against ref."""
     try:
-        for name, spread in _lds_forms(handle):
+        for name, spread, band in _lds_forms(handle):
             handle.set_small_max(8192)
             handle.set_spread_min(spread)
+            handle.set_band_min(band)
             _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, f"{name} path")
         handle.set_small_max(0)
         _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, "tiled path")
     finally:
         handle.set_small_max(8192)
         handle.set_spread_min(512)
+        handle.set_band_min(BAND_MIN)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -129,11 +134,13 @@ def test_fuzz_sizes(dm, handle, m):
             for x, y, eps, mp in sets:
                 ref = (O.fit_sequential(x, y, eps, mp, mode) if m <= 3000
                        else O.fit_grid(x, y, eps, mp, mode))
-                for name, spread in _lds_forms(handle):
+                for name, spread, band in _lds_forms(handle):
                     handle.set_spread_min(spread)
+                    handle.set_band_min(band)
                     _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=handle), ref, f"{name} m={m}")
     finally:
         handle.set_spread_min(512)
+        handle.set_band_min(BAND_MIN)
     # one batch of equal-eps partitions
     x = np.concatenate([s[0] for s in sets])
     y = np.concatenate([s[1] for s in sets])
@@ -247,10 +254,12 @@ def test_blob_partitions_batch(dm, handle):
     assert len(offs) - 1 > 100
 
 
-def test_spread_fits_from_concurrent_handles(dm):
+@pytest.mark.parametrize("band_min", [BAND_MIN, NO_BAND])
+def test_spread_fits_from_concurrent_handles(dm, band_min):
     """Four executor threads, a handle each, fitting partitions concurrently through the spread
-    form (each launch holds its workgroups at two grid barriers while the other handles' launches
-    share the GPU): every fit equals its oracle fit, no barrier times out."""
+    and band forms (each launch holds its workgroups at grid barriers while the other handles'
+    launches share the GPU; NO_BAND: the spread form alone): every fit equals its oracle fit,
+    no barrier times out."""
     import threading
 
     rng = np.random.default_rng(404)
@@ -260,6 +269,8 @@ def test_spread_fits_from_concurrent_handles(dm):
         sets.append((x, y, float(rng.uniform(0.05, 0.3)), int(rng.integers(2, 12))))
     refs = [O.fit_grid(x, y, e, mp, 0) for x, y, e, mp in sets]
     handles = [dm.Handle(0) for _ in range(4)]
+    for hh in handles:
+        hh.set_band_min(band_min)
     errors = []
 
     def worker(t):
@@ -315,6 +326,7 @@ def test_spread_fit_barrier_give_up_falls_back(dm):
     h = dm.Handle(0)
     try:
         h.set_spread_min(0)
+        h.set_band_min(NO_BAND)  # (the band form's own give-up: tests/test_gpu_band.py)
         assert h.set_spread_spin_limit(0) == 1 << 21
         before = h.spread_fallbacks()
         expect = before
