@@ -1175,11 +1175,10 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
 //   merge   the published pairs united in a union-find over input indices in global memory
 //           (larger index hooked under the smaller: a root IS s(K))
 //   -- grid barrier 3 --
-//   roots   each own core's root (its s(K)) by input index; roots flagged
-//   -- grid barrier 4 --
-//   label   root flags -> popcount ranks (cluster id = 1 + roots before s(K)); own cores their
-//           root's id, own non-cores the min s(K) over their staged core neighbours + the Naive /
-//           Archery rule
+//   label   each staged core's root (its s(K)) into LDS; the root flags of all points read
+//           from the global forest (a core is a root iff it is its own parent) -> popcount ranks
+//           (cluster id = 1 + roots before s(K)); own cores their root's id, own non-cores the
+//           min s(K) over their staged core neighbours + the Naive / Archery rule
 // Same results bit for bit as every other form (the GPU tests compare them with the oracle).
 // A range over the staging capacity (rows too dense, or too many sparse rows), or a barrier
 // that gives up, flags st[kStError] (3 / 2): the host then re-runs the fit through the tiled
@@ -1211,9 +1210,7 @@ struct BandLds {
 
 struct BandArgs {
     uint8_t* core;    // [m] core flags by input index
-    int32_t* lab;     // [m] own cores: the root's input index
     int32_t* par;     // [m] union-find over input indices
-    uint32_t* rbits;  // [m/32 + 1] roots by input index
     uint32_t* pairs;  // [G][kBandCap] published (input index << 16 | root input index)
     int32_t* npairs;  // [G]
     int32_t* cnt;     // [2] cores, occupied cells
@@ -1376,6 +1373,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         if (!fin) {  // nobody's neighbour: noise (minPoints >= 1)
             cluster[pi] = 0;
             flag[pi] = DBSCAN_FLAG_NOISE;
+            ba.core[pi] = 0;  // (the numbering reads every point's core flag)
         }
     }
     {
@@ -1733,8 +1731,6 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     }
     SM_STAMP(8);
     BAND_WG(1, wall_clock64());
-    // this workgroup's share of the root words, zeroed for the roots phase
-    for (int k = g * kBandT + tid; k < (m + 31) / 32; k += G * kBandT) ba.rbits[k] = 0u;
     sp_grid_sync(ba.bar, 4u * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(9);
     BAND_WG(2, wall_clock64());
@@ -1919,32 +1915,60 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     sp_grid_sync(ba.bar, 6u * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(14);
 
-    // ---- roots of the own cores (read-only walks: every union is done) ----
-    for (int p = s0 + tid; p < s1; p += kBandT) {
+    // ---- roots of every staged core (read-only walks: every union is done) into L.par (the
+    // LDS forest is published); root bits of all points straight from the global forest (a
+    // core is a root iff it is its own parent), so no barrier between roots and numbering ----
+    // (plain loads: the forest is final after the barrier, which invalidated the L1)
+    for (int p = tid; p < S; p += kBandT) {
         if (!L.core[p]) continue;
-        const int v = (int)(L.info[p] >> 16);
-        int r = v;
-        for (int u = ba.par[r]; u != r; u = ba.par[r]) r = u;
-        ba.lab[v] = r;
-        if (r == v) atomicOr(&ba.rbits[v >> 5], 1u << (v & 31));
+        int r = (int)(L.info[p] >> 16);
+        for (int k = 0; k < kBandMaxPoints; ++k) {
+            const int u = ba.par[r];
+            if (u == r || (unsigned)u >= (unsigned)kBandMaxPoints) break;
+            r = u;
+        }
+        L.par[p] = r;
     }
     SM_STAMP(15);
-    sp_grid_sync(ba.bar, 7u * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(16);
-
-    // ---- numbering and labels ----
     const int nw = (m + 31) / 32;
     int nclust = 0;
     {
+        // (four points per thread by one 4-byte and one 16-byte load, two steps' loads in
+        // flight together; a root word from 8 lanes' nibbles)
+        constexpr int kChunk = 4 * kBandT;
+        for (int u0 = 0; u0 < nw * 32; u0 += 2 * kChunk) {
+            uint32_t cw[2];
+            int4 pv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ub = u0 + h * kChunk + 4 * tid;
+                cw[h] = ub < m ? *reinterpret_cast<const uint32_t*>(ba.core + ub) : 0u;
+                pv[h] = ub < m ? *reinterpret_cast<const int4*>(ba.par + ub) : make_int4(-1, -1, -1, -1);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ub = u0 + h * kChunk + 4 * tid;
+                uint32_t nib = 0;
+                nib |= ((cw[h] & 0xFFu) && pv[h].x == ub && ub < m) ? 1u : 0u;
+                nib |= ((cw[h] & 0xFF00u) && pv[h].y == ub + 1 && ub + 1 < m) ? 2u : 0u;
+                nib |= ((cw[h] & 0xFF0000u) && pv[h].z == ub + 2 && ub + 2 < m) ? 4u : 0u;
+                nib |= ((cw[h] & 0xFF000000u) && pv[h].w == ub + 3 && ub + 3 < m) ? 8u : 0u;
+                uint32_t wv = nib << (4 * (lane & 7));
+                wv |= (uint32_t)__shfl_xor((int)wv, 1, 64);
+                wv |= (uint32_t)__shfl_xor((int)wv, 2, 64);
+                wv |= (uint32_t)__shfl_xor((int)wv, 4, 64);
+                if ((lane & 7) == 0 && ub < nw * 32) L.rbits[ub >> 5] = wv;
+            }
+        }
+        __syncthreads();
         constexpr int kWPer = kBandWords / kBandT;
         int v[kWPer], sum = 0;
 #pragma unroll
         for (int k = 0; k < kWPer; ++k) {
             const int wd = tid * kWPer + k;
-            const uint32_t bits =
-                wd < nw ? __hip_atomic_load(ba.rbits + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : 0u;
-            if (wd < kBandWords) L.rbits[wd] = bits;
+            const uint32_t bits = wd < nw ? L.rbits[wd] : 0u;
+            if (wd >= nw && wd < kBandWords) L.rbits[wd] = 0u;
             v[k] = __popc(bits);
             sum += v[k];
         }
@@ -1964,7 +1988,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     for (int p = s0 + tid; p < s1; p += kBandT) {  // cores: one thread each
         if (!L.core[p]) continue;
         const uint32_t v = L.info[p] >> 16;
-        cluster[v] = cluster_of((uint32_t)ba.lab[v]);
+        cluster[v] = cluster_of((uint32_t)L.par[p]);
         flag[v] = DBSCAN_FLAG_CORE;
     }
     for (int p = s0 + (tid >> 6); p < s1; p += kW) {  // non-cores: a wave each
@@ -1980,7 +2004,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             const int e = L.cst[r * nx + x1 + 1];
             for (int q = L.cst[r * nx + x0] + lane; q < e; q += 64) {
                 if (!L.core[q]) continue;
-                const uint32_t s = (uint32_t)ba.lab[L.info[q] >> 16];
+                const uint32_t s = (uint32_t)L.par[q];
                 if (s < best && sm_pair(L, c, p, me, q, L.rec[q])) best = s;
             }
         }
@@ -2109,9 +2133,8 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     // at 128, the row counts and claims; then the slices' boxes)
     constexpr size_t kHead = 512, kRows = (size_t)kBandCap * 4, kZero = kHead + 2 * kRows;
     constexpr size_t kBox = (size_t)kBandMaxWG * 5 * 8;
-    const size_t words = (size_t)(kBandMaxPoints / 32 + 1);
-    const size_t bytes = kZero + kBox + (size_t)kBandMaxPoints * (1 + 4 + 4 + 16 + 4) +
-                         words * 4 + (size_t)kBandMaxWG * kBandCap * 4;
+    const size_t bytes = kZero + kBox + (size_t)kBandMaxPoints * (1 + 4 + 16 + 4) +
+                         (size_t)kBandMaxWG * kBandCap * 4;
     if (ws.band.bytes < bytes || !ws.band_ready) {
         char* p = static_cast<char*>(ws.band.ensure(bytes));
         DBSCAN_HIP_CHECK(hipMemsetAsync(p, 0, kZero, s));
@@ -2132,12 +2155,8 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     q += (size_t)kBandMaxPoints * 4;
     ba.core = reinterpret_cast<uint8_t*>(q);
     q += kBandMaxPoints;
-    ba.lab = reinterpret_cast<int32_t*>(q);
-    q += (size_t)kBandMaxPoints * 4;
     ba.par = reinterpret_cast<int32_t*>(q);
     q += (size_t)kBandMaxPoints * 4;
-    ba.rbits = reinterpret_cast<uint32_t*>(q);
-    q += words * 4;
     ba.pairs = reinterpret_cast<uint32_t*>(q);
     // kStError cleared ahead of the launch, in the device state and the pinned mirror
     DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));

@@ -216,7 +216,7 @@ int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
  * DBSCAN_BAND_MAX_POINTS; 0: never) in modes NAIVE and ARCHERY with minPoints >= 1 run in ONE
  * launch instead of the tiled pipeline's ~45: 64 workgroups, each owning a range of eps cells of
  * ~1/64 of the estimated work and staging those cells' rows (plus one row either side) in its
- * LDS, meeting at seven grid barriers, the clusters merged in a union-find over input indices
+ * LDS, meeting at six grid barriers, the clusters merged in a union-find over input indices
  * -- same results bit for bit.  A range over the staging capacity (very dense rows) or a
  * barrier that gives up re-runs the fit through the tiled pipeline in the same call (counted
  * by dbscan_spread_fallbacks).  Returns the previous value. */
