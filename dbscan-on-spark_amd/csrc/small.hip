@@ -1187,6 +1187,7 @@ constexpr int kBandT = 1024;
 constexpr int kBandCap = 7168;    // staged points per workgroup (and staged cells)
 constexpr int kBandCells = kBandCap;
 constexpr int kBandMaxWG = 64;
+constexpr int kBandFullBox = 16384;  // up to here every workgroup reduces the whole bbox
 // a point's count + walk work without neighbours, in cell densities (0, 1 and 4 measured within
 // 2% of 2 at 12k-65k points)
 constexpr int kBandC0 = 2;
@@ -1376,9 +1377,36 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             ba.core[pi] = 0;  // (the numbering reads every point's core flag)
         }
     }
+    // (up to kBandFullBox points every workgroup reduces the whole bbox itself, from L2, instead
+    // of publishing its slice's and meeting at a barrier)
+    const bool fullbox = m <= kBandFullBox;
+    uint32_t nbar = 0;  // grid barriers met so far
     {
         double mnx = fin ? px : INFINITY, mxx = fin ? px : -INFINITY;
         double mny = fin ? py : INFINITY, mxy = fin ? py : -INFINITY, nfin = fin ? 1.0 : 0.0;
+        if (fullbox) {
+            mnx = mny = INFINITY;
+            mxx = mxy = -INFINITY;
+            nfin = 0.0;
+            for (int i0 = tid; i0 < m; i0 += 4 * kBandT) {
+                double a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + u * kBandT;
+                    a[u] = i < m ? x[i] : NAN;
+                    b[u] = i < m ? y[i] : NAN;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (isfinite(a[u]) && isfinite(b[u])) {
+                        mnx = fmin(mnx, a[u]);
+                        mxx = fmax(mxx, a[u]);
+                        mny = fmin(mny, b[u]);
+                        mxy = fmax(mxy, b[u]);
+                        nfin += 1.0;
+                    }
+            }
+        }
         const int w = tid >> 6;
         mnx = wave_min(mnx);
         mxx = wave_max(mxx);
@@ -1400,15 +1428,15 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                 const double u = L.red[tid][k];
                 v = tid == 4 ? v + u : ((tid & 1) ? fmax(v, u) : fmin(v, u));
             }
-            ba.box[g * 5 + tid] = v;
+            if (fullbox) L.red[tid][0] = v; else ba.box[g * 5 + tid] = v;
         }
     }
     SM_STAMP(1);
-    sp_grid_sync(ba.bar, 1u * (uint32_t)G, st, mirror, spin_limit);
+    if (!fullbox) sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(2);
 
     // ---- the grid from the G partial boxes (one reduction tree: the same grid everywhere) ----
-    if (tid < 5 * 64) {  // wave j reduces quantity j over the G <= 64 boxes, one per lane
+    if (!fullbox && tid < 5 * 64) {  // wave j reduces quantity j over the G <= 64 boxes
         const int j = tid >> 6;
         double v = lane < G ? bd_load(ba.box + lane * 5 + j)
                             : (j == 4 ? 0.0 : ((j & 1) ? -INFINITY : INFINITY));
@@ -1448,7 +1476,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             if (L.info[r]) atomicAdd(ba.rowcnt + r, L.info[r]);
     }
     SM_STAMP(3);
-    sp_grid_sync(ba.bar, 2u * (uint32_t)G, st, mirror, spin_limit);
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(4);
 
     // ---- the bands: cell ranges of equal cost ----
@@ -1570,7 +1598,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     SM_STAMP(5);
-    sp_grid_sync(ba.bar, 3u * (uint32_t)G, st, mirror, spin_limit);
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(6);
     // (every workgroup has read the row counts and claimed its pieces: this workgroup's share
     // of them zeroed for the next launch)
@@ -1731,7 +1759,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     }
     SM_STAMP(8);
     BAND_WG(1, wall_clock64());
-    sp_grid_sync(ba.bar, 4u * (uint32_t)G, st, mirror, spin_limit);
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(9);
     BAND_WG(2, wall_clock64());
 
@@ -1903,7 +1931,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     BAND_WG(3, wall_clock64());
     BAND_WG(4, s1 - s0);
     BAND_WG(5, S);
-    sp_grid_sync(ba.bar, 5u * (uint32_t)G, st, mirror, spin_limit);
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(12);
 
     // ---- merge: this workgroup's pairs into the global union-find over input indices ----
@@ -1912,7 +1940,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         bd_unite(ba.par, (int)(w >> 16), (int)(w & 0xFFFFu));
     }
     SM_STAMP(13);
-    sp_grid_sync(ba.bar, 6u * (uint32_t)G, st, mirror, spin_limit);
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
     SM_STAMP(14);
 
     // ---- roots of every staged core (read-only walks: every union is done) into L.par (the
