@@ -71,10 +71,10 @@ __device__ long long g_sm_stamps[24];
 // band_fit_kernel, every workgroup: [g][0..7] = clock at the stage's end, the count's end,
 // after barrier 1, at barrier 2's arrival; own points, staged points; clock before and after
 // the union walks
-__device__ long long g_band_wg[64 * 8];
+__device__ long long g_band_wg[64 * 12];
 #define BAND_WG(k, v)                                           \
     do {                                                        \
-        if (threadIdx.x == 0) g_band_wg[blockIdx.x * 8 + (k)] = (v); \
+        if (threadIdx.x == 0) g_band_wg[blockIdx.x * 12 + (k)] = (v); \
     } while (0)
 #else
 #define BAND_WG(k, v) \
@@ -1801,13 +1801,15 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                       "qlist spans rbits and wrank");
         if (tid == 0) L.meta[6] = 0;
         __syncthreads();
+        // each own core chained to the previous core of its quarter (one union per thread), own
+        // quarter runs holding a core listed.  (Chaining the halo quarters too made the
+        // distance-2 pass shorter but published ~2x the pairs: 65536 points 222 -> 241 us.)
         for (int sl = s0 + tid; sl < s1; sl += kBandT) {
             const uint32_t inf = L.info[sl];
             const int cell = (int)(inf & kCellMask);
             const uint32_t qd = (inf >> 13) & 3u;
             const int cb0 = L.cst[cell];
             const bool start = sl == cb0 || ((L.info[sl - 1] >> 13) & 3u) != qd;
-            // each core chained to the previous core of its quarter (one union per thread)
             if (L.core[sl]) {
                 for (int t = sl - 1; t >= cb0 && ((L.info[t] >> 13) & 3u) == qd; --t)
                     if (L.core[t]) {
@@ -1830,6 +1832,8 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         }
         __syncthreads();
         const int nq = L.meta[6];
+        BAND_WG(8, wall_clock64());
+        BAND_WG(10, nq);
         if (nq <= kQMax) {
             walked = true;
             const auto run_of = [&](int cell, uint32_t qd, int& b, int& e) {
@@ -1904,6 +1908,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                     }
                 }
                 __syncthreads();
+                BAND_WG(9 + 2 * pass, wall_clock64());
             }
         }
     }
@@ -2081,7 +2086,7 @@ extern "C" int dbscan_ab_small_stamps(long long* out) {
                ? 0 : -1;
 }
 extern "C" int dbscan_ab_band_wg(long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_wg), 64 * 8 * sizeof(long long)) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_wg), 64 * 12 * sizeof(long long)) ==
                    hipSuccess
                ? 0 : -1;
 }

@@ -27,7 +27,7 @@ h = dbscan_amd.Handle(0)
 buf = (ctypes.c_longlong * 24)()
 fw = lib.dbscan_ab_band_wg
 fw.argtypes = [ctypes.c_void_p]
-wg = (ctypes.c_longlong * 512)()
+wg = (ctypes.c_longlong * 768)()
 for m in [int(a) for a in (sys.argv[1:] or ["12000", "20000", "40000", "65536"])]:
     tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
     rows = []
@@ -39,14 +39,20 @@ for m in [int(a) for a in (sys.argv[1:] or ["12000", "20000", "40000", "65536"])
     r = np.median(np.array(rows), axis=0)
     print(f"m={m}: " + ", ".join(f"{p} {v:.1f}" for p, v in zip(PH, r)) +
           f"  kernel {r.sum():.1f} us", flush=True)
-    a = np.array(list(wg), dtype=np.int64).reshape(64, 8)
+    a = np.array(list(wg), dtype=np.int64).reshape(64, 12)
+    gw = int((a[:, 4] > 0).sum())  # (workgroups of this launch: the rest are stale rows)
+    a = a[:max(gw, 1)]
     tc = (a[:, 1] - a[:, 0]) / 100.0
     tw = (a[:, 3] - a[:, 2]) / 100.0
     tl = (a[:, 6] - a[:, 2]) / 100.0
     tu = (a[:, 7] - a[:, 6]) / 100.0
     tp = (a[:, 3] - a[:, 7]) / 100.0
+    tq = (a[:, 8] - a[:, 6]) / 100.0
+    t0 = (a[:, 9] - a[:, 8]) / 100.0
+    t1 = (a[:, 11] - a[:, 9]) / 100.0
     for name, t in (("count", tc), ("core load + walks + publish", tw), ("core load", tl),
-                    ("walks alone", tu), ("publish", tp)):
+                    ("walks alone", tu), ("publish", tp), ("chains + quarter list", tq),
+                    ("adjacent pass", t0), ("distance-2 pass", t1)):
         k = int(np.argmax(t))
         print(f"  {name} per workgroup: max {t.max():.1f} us (wg {k}: own {a[k, 4]}, staged "
               f"{a[k, 5]}), median {np.median(t):.1f}; slowest 5: " +
