@@ -1940,9 +1940,15 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     SM_STAMP(12);
 
     // ---- merge: this workgroup's pairs into the global union-find over input indices ----
+    // (v's local root r is the smallest index of its LDS set, r < v: while v is still a
+    // global root, one CAS hooks it under r; otherwise the full union)
     for (int k = tid; k < npairs; k += kBandT) {
         const uint32_t w = mine[k];
-        bd_unite(ba.par, (int)(w >> 16), (int)(w & 0xFFFFu));
+        const int v = (int)(w >> 16), r = (int)(w & 0xFFFFu);
+        int expected = v;
+        if (!__hip_atomic_compare_exchange_strong(ba.par + v, &expected, r, __ATOMIC_RELAXED,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            bd_unite(ba.par, v, r);
     }
     SM_STAMP(13);
     sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
