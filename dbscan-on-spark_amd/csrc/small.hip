@@ -1738,6 +1738,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     // ---- count (own points): a thread each when they fill a quarter of the workgroup, else
     // a wave each (64 candidates per step, ballot counts) ----
     int ncore = 0;
+    // (a thread per point from 256 own points: 128, 64 and always measured within 1-4%)
     if (s1 - s0 >= kBandT / 4) {
         for (int p = s0 + tid; p < s1; p += kBandT) {
             const bool cc = sm_count(L, c, p, min_points, -1) >= min_points;
