@@ -2140,11 +2140,14 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     sa.core = reinterpret_cast<uint8_t*>(base + kSpreadHead);
     sa.pairs = reinterpret_cast<uint32_t*>(base + kSpreadHead + kSmN);
     const int G = (int)std::min<int64_t>(kSpreadMaxWG, std::max<int64_t>(1, n / kSpreadPer));
-    // kStError cleared ahead of the launch (the kernel never clears it): in the device state
-    // and, without waiting on the device, in the pinned mirror the host reads
-    DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
+    // kStError cleared ahead of the launch (the kernel never clears it): without waiting on
+    // the device, in the pinned mirror the host reads; in the device state only when there is
+    // no mirror (its host reads copy the device state then; a memset is one more GPU command
+    // per call: ~3 us)
     if (mirror && ws.stats_host)
         reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
+    else
+        DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
     ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
                                                gp, st, mirror};
     klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
@@ -2198,10 +2201,12 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     ba.par = reinterpret_cast<int32_t*>(q);
     q += (size_t)kBandMaxPoints * 4;
     ba.pairs = reinterpret_cast<uint32_t*>(q);
-    // kStError cleared ahead of the launch, in the device state and the pinned mirror
-    DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
+    // kStError cleared ahead of the launch: in the pinned mirror, or the device state when
+    // there is no mirror (as enqueue_spread_fit)
     if (mirror && ws.stats_host)
         reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
+    else
+        DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
     ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
                                                gp, st, mirror};
     ws.recall_band = true;
