@@ -486,8 +486,8 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
                               reinterpret_cast<uint8_t*>(dout + 4 * (size_t)n), nullptr, nullptr};
             a.small_max = h->small_max;
             a.spread_min = h->spread_min;
-        a.band_max = h->band_max;
-        a.band_min = h->band_min;
+            a.band_max = h->band_max;
+            a.band_min = h->band_min;
             h->prepared = false;
             dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
             DBSCAN_HIP_CHECK(
