@@ -1886,6 +1886,27 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                     const double bx0 = 0.5 * (double)hx - reach_kx;
                     const double by0 = 0.5 * (double)hy - reach_ky;
                     bool found = false;
+                    // (far pairs: the other quarter's cores near this quarter's box, as a mask;
+                    // 16384 / 20000 / 65536 points 135 / 149 / 216 -> 127 / 138 / 192 us)
+                    uint64_t bm = ~0ull;
+                    const bool masked = pass && !c.exact_only && e2 - fb <= 64;
+                    if (masked) {
+                        const double ax0 = 0.5 * (double)(2 * cx + (qd & 1)) - reach_kx;
+                        const double ay0 = 0.5 * (double)(2 * cy + (qd >> 1)) - reach_ky;
+                        bm = 0ull;
+                        for (int b = fb; b < e2; ++b) {
+                            if (!L.core[b]) continue;
+                            const float2 rb = L.rec[b];
+                            const float ddx = (float)fmax(0.0, fmax(ax0 - (double)rb.x,
+                                                                    (double)rb.x - (ax0 + 0.5)));
+                            const float ddy = (float)fmax(0.0, fmax(ay0 - (double)rb.y,
+                                                                    (double)rb.y - (ay0 + 0.5)));
+                            const float mg = (fabsf(rb.x) + fabsf(rb.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
+                            const float rr = (sqrtf(c.hi) + mg) * (sqrtf(c.hi) + mg);
+                            if (ddx * ddx + ddy * ddy <= rr) bm |= 1ull << (b - fb);
+                        }
+                        if (!bm) continue;
+                    }
                     for (int a = fa; a < qe && !found; ++a) {
                         if (!L.core[a]) continue;
                         const float2 ra = L.rec[a];
@@ -1897,6 +1918,17 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                             const float mg = (fabsf(ra.x) + fabsf(ra.y) + 4.0f) * 0x1p-18f + 0x1p-12f;
                             const float rr = (sqrtf(c.hi) + mg) * (sqrtf(c.hi) + mg);
                             if (ddx * ddx + ddy * ddy > rr) continue;
+                        }
+                        if (masked) {
+                            for (uint64_t mm = bm; mm; mm &= mm - 1) {
+                                const int b = fb + __ffsll((unsigned long long)mm) - 1;
+                                if (sm_pair(L, c, a, ra, b, L.rec[b])) {
+                                    (void)sm_unite_from(L.par, L.info, a, b);
+                                    found = true;
+                                    break;
+                                }
+                            }
+                            continue;
                         }
                         for (int b = fb; b < e2; ++b) {
                             if (!L.core[b]) continue;
