@@ -1738,6 +1738,13 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     // ---- count (own points): a thread each when they fill a quarter of the workgroup, else
     // a wave each (64 candidates per step, ballot counts) ----
     int ncore = 0;
+    // the staged slots' LDS forest, and their core flags: the own ones from the count, the
+    // halo's after barrier 1
+    for (int p = tid; p < S; p += kBandT) {
+        L.par[p] = p;
+        L.core[p] = 0;
+    }
+    __syncthreads();
     // (a thread per point from 256 own points: 128, 64 and always measured within 1-4%)
     if (s1 - s0 >= kBandT / 4) {
         for (int p = s0 + tid; p < s1; p += kBandT) {
@@ -1745,6 +1752,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             const int v = (int)(L.info[p] >> 16);
             ba.core[v] = cc ? 1 : 0;
             ba.par[v] = v;
+            L.core[p] = cc ? 1 : 0;
             ncore += cc ? 1 : 0;
         }
     } else {
@@ -1754,52 +1762,20 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                 const int v = (int)(L.info[p] >> 16);
                 ba.core[v] = cc ? 1 : 0;
                 ba.par[v] = v;
+                L.core[p] = cc ? 1 : 0;
                 ncore += cc ? 1 : 0;
             }
         }
     }
-    SM_STAMP(8);
-    BAND_WG(1, wall_clock64());
-    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(9);
-    BAND_WG(2, wall_clock64());
-
-    // ---- union: the staged core flags, own cores' walks, the forest published ----
-    {
-        int tot = 0, occ = 0;
-        (void)sm_excl_scan(ncore, L.wsc, &tot);
-        (void)sm_excl_scan(occupied, L.wsc, &occ);
-        if (tid == 0) {
-            if (tot) atomicAdd(&ba.cnt[0], tot);
-            if (occ) atomicAdd(&ba.cnt[1], occ);
-        }
-    }
-    for (int p = tid; p < S; p += kBandT) {
-        L.core[p] = ba.core[L.info[p] >> 16];
-        L.par[p] = p;
-    }
-    if (tid == 0) L.meta[2] = 0;
+    // own quarters' chains and list, ahead of barrier 1 (they need only the own core flags)
     __syncthreads();
-    BAND_WG(6, wall_clock64());
     const bool quarters = L.G.clique != 0;
-    const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
-    const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy - (double)sa;  // (staged rows)
-    // Quarter-level unions (clique grids: a quarter cell's cores are one clique; the staged
-    // slots of a cell are grouped by quarter): each own core chained to the previous core of
-    // its quarter; then for each own quarter holding a core and each of the 12 quarters after
-    // it (quarter-grid offsets within 2, row-major order) a core pair within eps searched and
-    // united -- adjacent quarters first, then (after a barrier) the distance-2 ones, skipped
-    // when already in one set, their far cores pruned by the other quarter's box.  Every
-    // quarter pair is tested by the owner of its smaller quarter, which stages both.  Against
-    // the per-core stencil walks: 133 / 147 / 171 / 191 -> 112 / 138 / 155 / 178 us per kernel
-    // at 12k / 20k / 40k / 65k points (the walks repeat each quarter's work for every core).
-    bool walked = false;
+    uint32_t* qlist = L.rbits;  // (rbits and wrank are free until the numbering)
+    constexpr int kQMax = 2 * kBandWords;
+    static_assert(sizeof(L.rbits) + sizeof(L.wrank) == kQMax * sizeof(uint32_t) &&
+                      offsetof(BandLds, wrank) == offsetof(BandLds, rbits) + sizeof(L.rbits),
+                  "qlist spans rbits and wrank");
     if (quarters) {
-        uint32_t* qlist = L.rbits;  // (rbits and wrank are free until the numbering)
-        constexpr int kQMax = 2 * kBandWords;
-        static_assert(sizeof(L.rbits) + sizeof(L.wrank) == kQMax * sizeof(uint32_t) &&
-                          offsetof(BandLds, wrank) == offsetof(BandLds, rbits) + sizeof(L.rbits),
-                      "qlist spans rbits and wrank");
         if (tid == 0) L.meta[6] = 0;
         __syncthreads();
         // each own core chained to the previous core of its quarter (one union per thread), own
@@ -1832,6 +1808,41 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             }
         }
         __syncthreads();
+    }
+    SM_STAMP(8);
+    BAND_WG(1, wall_clock64());
+    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
+    SM_STAMP(9);
+    BAND_WG(2, wall_clock64());
+
+    // ---- union: the staged core flags, own cores' walks, the forest published ----
+    {
+        int tot = 0, occ = 0;
+        (void)sm_excl_scan(ncore, L.wsc, &tot);
+        (void)sm_excl_scan(occupied, L.wsc, &occ);
+        if (tid == 0) {
+            if (tot) atomicAdd(&ba.cnt[0], tot);
+            if (occ) atomicAdd(&ba.cnt[1], occ);
+        }
+    }
+    for (int p = tid; p < S; p += kBandT)
+        if (p < s0 || p >= s1) L.core[p] = ba.core[L.info[p] >> 16];
+    if (tid == 0) L.meta[2] = 0;
+    __syncthreads();
+    BAND_WG(6, wall_clock64());
+    const double reach_kx = (L.G.cx2 - L.G.xmin2) * L.G.invx;
+    const double reach_ky = (L.G.cy2 - L.G.ymin2) * L.G.invy - (double)sa;  // (staged rows)
+    // Quarter-level unions (clique grids: a quarter cell's cores are one clique; the staged
+    // slots of a cell are grouped by quarter): each own core chained to the previous core of
+    // its quarter; then for each own quarter holding a core and each of the 12 quarters after
+    // it (quarter-grid offsets within 2, row-major order) a core pair within eps searched and
+    // united -- adjacent quarters first, then (after a barrier) the distance-2 ones, skipped
+    // when already in one set, their far cores pruned by the other quarter's box.  Every
+    // quarter pair is tested by the owner of its smaller quarter, which stages both.  Against
+    // the per-core stencil walks: 133 / 147 / 171 / 191 -> 112 / 138 / 155 / 178 us per kernel
+    // at 12k / 20k / 40k / 65k points (the walks repeat each quarter's work for every core).
+    bool walked = false;
+    if (quarters) {
         const int nq = L.meta[6];
         BAND_WG(8, wall_clock64());
         BAND_WG(10, nq);
