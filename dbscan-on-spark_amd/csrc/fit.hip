@@ -3521,7 +3521,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         StageTimer t(prof, s, "small_fit");
         double* mirror = stats_mirror(ws);  // (LDS fits write their stats there: no copy back)
         // (from band_min points the band form: its cooperative staging and quarter unions
-        // measured faster than the spread form from ~3000 points, 133 -> 121 us at 8192)
+        // measured faster than the spread form from ~3000 points (133 -> 121 us at 8192) in its
+        // first form, from ~400 points since: 2000 / 600 points 77 / 64 us against 82 / 73)
         if (n >= a.band_min && n <= a.band_max && !a.batch &&
             band_fit_eligible(n, a.eps, a.mode, a.min_points))
             enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,

@@ -224,10 +224,10 @@ int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
 #define DBSCAN_BAND_DEFAULT_POINTS 65536
 int64_t dbscan_set_band_max(dbscan_handle* h, int64_t max_points);
 /* Fits inside the LDS fits' capacity of >= min_points points (default
- * DBSCAN_BAND_MIN_DEFAULT_POINTS; measured faster than the spread form from ~3000 points) take
- * the band form too, with the same eligibility (and up to the band maximum above).  Returns the
- * previous value. */
-#define DBSCAN_BAND_MIN_DEFAULT_POINTS 3072
+ * DBSCAN_BAND_MIN_DEFAULT_POINTS; measured faster than the one-workgroup and spread forms from
+ * ~400 points) take the band form too, with the same eligibility (and up to the band maximum
+ * above).  Returns the previous value. */
+#define DBSCAN_BAND_MIN_DEFAULT_POINTS 400
 int64_t dbscan_set_band_min(dbscan_handle* h, int64_t min_points);
 /* Test hook: the spread fit's barrier poll bound (default 2^21 polls, ~seconds); 0 makes every
  * barrier give up at once, so every spread fit takes the one-workgroup re-run.  Returns the

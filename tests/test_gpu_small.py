@@ -43,7 +43,7 @@ def _eq(got, ref, what=""):
 
 ONE_WG = 1 << 30  # dbscan_set_spread_min: every LDS fit on one workgroup
 NO_BAND = 1 << 30  # dbscan_set_band_min: no LDS-sized fit takes the band form
-BAND_MIN = 3072  # DBSCAN_BAND_MIN_DEFAULT_POINTS
+BAND_MIN = 400  # DBSCAN_BAND_MIN_DEFAULT_POINTS
 
 
 def _lds_forms(handle):

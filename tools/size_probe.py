@@ -1,6 +1,7 @@
 """Per-call latency (dbscan_fit_device, inputs resident; median of 20 calls after 3) over
 partition sizes, for comparing the LDS fit forms:
-    [DBSCAN_LIB_PATH=...] python tools/size_probe.py [m ...]"""
+    [DBSCAN_LIB_PATH=...] [BAND_MIN=n] python tools/size_probe.py [m ...]
+(BAND_MIN: the handle's dbscan_set_band_min, to time the band form below its default)"""
 import ctypes
 import os
 import sys
@@ -15,6 +16,8 @@ import dbscan_amd  # noqa: E402
 from dbscan_amd import device as D  # noqa: E402
 
 h = dbscan_amd.Handle(0)
+if os.environ.get("BAND_MIN"):
+    h.set_band_min(int(os.environ["BAND_MIN"]))
 L = dbscan_amd.load()
 sizes = [int(a) for a in sys.argv[1:]] or [600, 1200, 2000, 3000, 4096, 6000, 8192, 12000, 16000]
 out = []
