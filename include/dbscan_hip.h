@@ -208,7 +208,10 @@ int64_t dbscan_set_small_max(dbscan_handle* h, int64_t max_points);
  * work, e.g. many executors' spread fits at once) gives up its grid barrier after a bounded poll
  * instead of waiting forever, and the fit is then re-run by the one-workgroup kernel in the same
  * call (for dbscan_fit_device_async: in dbscan_sync), with the same results; the fit never
- * fails for it.  Such re-runs are counted (dbscan_spread_fallbacks). */
+ * fails for it.  Such re-runs are counted (dbscan_spread_fallbacks).  With the defaults the
+ * band form below takes every eligible fit from DBSCAN_BAND_MIN_DEFAULT_POINTS points, so the
+ * spread form serves the fits the band form does not take (minPoints <= 0, the float32-box
+ * Archery mode) or a handle whose dbscan_set_band_min is raised. */
 #define DBSCAN_SPREAD_DEFAULT_POINTS 512
 int64_t dbscan_set_spread_min(dbscan_handle* h, int64_t min_points);
 /* Full fits above the LDS fits' capacity (DBSCAN_SMALL_MAX_POINTS, with small_max at that
