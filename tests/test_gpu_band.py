@@ -1,9 +1,11 @@
-"""Partitions above the one-workgroup LDS capacity in ONE launch (small.hip band_fit_kernel):
-8192 < m <= 65536 points, up to 64 workgroups each staging a band of cell rows plus one row
-either side, four grid barriers, the clusters merged over input indices.  Every result must
-equal the oracle (LocalDBSCANNaive.scala:37-118 / LocalDBSCANArchery.scala:36-112 restated,
-visit order = array order) and the tiled pipeline (dbscan_set_band_max 0) bit for bit; bands
-over the staging capacity and barriers that give up fall back to the tiled pipeline."""
+"""Partitions in ONE launch of the band form (small.hip band_fit_kernel): 400 <= m <= 65536
+points by default (dbscan_set_band_min / _max), ~m/256 workgroups (16..64) each staging its own
+cell range's rows plus one row either side, six grid barriers, quarter-level unions (per-core
+walks on grown grids), the clusters merged over input indices.  Every result must equal the
+oracle (LocalDBSCANNaive.scala:37-118 / LocalDBSCANArchery.scala:36-112 restated, visit order =
+array order) and the tiled pipeline (dbscan_set_band_max 0) bit for bit; ranges over the
+staging capacity and barriers that give up fall back to the tiled pipeline.  (Sizes up to 8192
+run through this form in tests/test_gpu_small.py as well.)"""
 import numpy as np
 import pytest
 
@@ -108,6 +110,31 @@ def test_band_equals_tiled_and_edge_inputs(dm):
             refp = O.fit_grid(x[p], y[p], eps, mp, 0)
             _eq(dm.fit_arrays(x[p], y[p], eps, mp, 0, handle=h), refp, f"permuted m={m}")
             np.testing.assert_array_equal(refp[1] == 1, ref[1][p] == 1)  # core flags move along
+    finally:
+        h.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_band_grown_grid_per_core_walks(dm, mode):
+    """eps small against the extent: the band grid grows past eps cells, its quarter cells are
+    no cliques (stats clique 0) and the unions take the per-core stencil walks; pairs and
+    triples within eps make the clusters."""
+    rng = np.random.default_rng(77 + mode)
+    h = dm.Handle(0)
+    try:
+        for m in (3000, 20000):
+            x = rng.uniform(0, 1e4, m)
+            y = rng.uniform(0, 1e4, m)
+            k = m // 3
+            x[:k] = x[k:2 * k] + rng.uniform(-4e-4, 4e-4, k)
+            y[:k] = y[k:2 * k] + rng.uniform(-4e-4, 4e-4, k)
+            x[2 * k:2 * k + k // 2] = x[k:k + k // 2] + rng.uniform(-4e-4, 4e-4, k // 2)
+            y[2 * k:2 * k + k // 2] = y[k:k + k // 2] + rng.uniform(-4e-4, 4e-4, k // 2)
+            ref = O.fit_grid(x, y, 1e-3, 2, mode)
+            before = h.spread_fallbacks()
+            _eq(dm.fit_arrays(x, y, 1e-3, 2, mode, handle=h), ref, f"m={m}")
+            assert h.spread_fallbacks() == before  # (the band form itself ran ...)
+            assert h.stats()["clique"] == 0  # (... on a grid without quarter cliques)
     finally:
         h.close()
 
