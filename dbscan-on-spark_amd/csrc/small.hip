@@ -1466,17 +1466,30 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
     const bool gbad = L.G.bad != 0 || nf == 0;  // (bad: unreachable for finite bboxes)
     int prow = -1, pcol = 0, pquad = 0;
     if (fin && !gbad) cell_of(px, py, prow, pcol, pquad);
-    // the slice's row histogram (LDS), added to the global row counts
+    // the row histogram: of the whole partition in LDS (up to kBandFullBox points: no global
+    // row counts, no barrier), else of the slice, added to the global row counts
     if (!gbad) {
         for (int r = tid; r < ny; r += kBandT) L.info[r] = 0u;
         __syncthreads();
-        if (prow >= 0) atomicAdd(&L.info[prow], 1u);
-        __syncthreads();
-        for (int r = tid; r < ny; r += kBandT)
-            if (L.info[r]) atomicAdd(ba.rowcnt + r, L.info[r]);
+        if (fullbox) {
+            for (int i = tid; i < m; i += kBandT) {
+                const double a = x[i], b = y[i];
+                if (isfinite(a) && isfinite(b)) {
+                    int row, col, quad;
+                    cell_of(a, b, row, col, quad);
+                    atomicAdd(&L.info[row], 1u);
+                }
+            }
+        } else {
+            if (prow >= 0) atomicAdd(&L.info[prow], 1u);
+            __syncthreads();
+            for (int r = tid; r < ny; r += kBandT)
+                if (L.info[r]) atomicAdd(ba.rowcnt + r, L.info[r]);
+        }
     }
     SM_STAMP(3);
-    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
+    if (!fullbox) sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
+    __syncthreads();
     SM_STAMP(4);
 
     // ---- the bands: cell ranges of equal cost ----
@@ -1502,9 +1515,10 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
 #pragma unroll
             for (int k = 0; k < kRowsPer; ++k) {
                 const int r = tid * kRowsPer + k;
-                v[k] = r < ny ? (int)__hip_atomic_load(ba.rowcnt + r, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)
-                              : 0;
+                v[k] = r >= ny ? 0
+                       : fullbox ? (int)L.info[r]
+                                 : (int)__hip_atomic_load(ba.rowcnt + r, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
                 v[k] = min(max(v[k], 0), kBandMaxPoints);  // (a gave-up barrier: stay in bounds)
                 sum += v[k];
                 q += (int64_t)v[k] * ((int64_t)kBandC0 * nx + v[k]);
@@ -1559,10 +1573,11 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             L.meta[tid] = lo;
         }
         // each of the slice's rows: its piece of the row-sorted records claimed (info: cursor)
-        for (int r = tid; r < ny; r += kBandT) {
-            const uint32_t k = L.info[r];
-            if (k) L.info[r] = (uint32_t)L.par[r] + atomicAdd(ba.rowcur + r, k);
-        }
+        if (!fullbox)
+            for (int r = tid; r < ny; r += kBandT) {
+                const uint32_t k = L.info[r];
+                if (k) L.info[r] = (uint32_t)L.par[r] + atomicAdd(ba.rowcur + r, k);
+            }
         __syncthreads();
         ra = L.meta[0];
         rb = L.meta[1];  // (ny: the range runs to the end)
@@ -1577,7 +1592,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         c_rb = rb < ny ? C[rb] : T;
         p_rb = rb < ny ? L.par[rb + 1] - L.par[rb] : 0;
         // the slice's records to their rows' pieces
-        if (prow >= 0) {
+        if (!fullbox && prow >= 0) {
             const uint32_t k = atomicAdd(&L.info[prow], 1u);
             if (k < (uint32_t)L.par[prow + 1] && k < (uint32_t)m) {
                 ba.rxy[k] = make_double2(px, py);
@@ -1598,14 +1613,43 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     SM_STAMP(5);
-    sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
-    SM_STAMP(6);
-    // (every workgroup has read the row counts and claimed its pieces: this workgroup's share
-    // of them zeroed for the next launch)
-    for (int r = g * kBandT + tid; r < kBandCap; r += G * kBandT) {
-        ba.rowcnt[r] = 0u;
-        ba.rowcur[r] = 0u;
+    uint16_t* slist = reinterpret_cast<uint16_t*>(L.rbits);  // (fullbox: the staged points)
+    static_assert(sizeof(L.rbits) + sizeof(L.wrank) >= kBandCap * sizeof(uint16_t),
+                  "the staged list fits rbits + wrank");
+    if (!fullbox) {
+        sp_grid_sync(ba.bar, (++nbar) * (uint32_t)G, st, mirror, spin_limit);
+        // (every workgroup has read the row counts and claimed its pieces: this workgroup's
+        // share of them zeroed for the next launch)
+        for (int r = g * kBandT + tid; r < kBandCap; r += G * kBandT) {
+            ba.rowcnt[r] = 0u;
+            ba.rowcur[r] = 0u;
+        }
+    } else if (S > 0) {
+        // the staged rows' points listed by input index (one append per wave)
+        if (tid == 0) L.meta[8] = 0;
+        __syncthreads();
+        for (int i0 = 0; i0 < m; i0 += kBandT) {
+            const int i = i0 + tid;
+            bool in = false;
+            if (i < m) {
+                const double a = x[i], b = y[i];
+                if (isfinite(a) && isfinite(b)) {
+                    int row, col, quad;
+                    cell_of(a, b, row, col, quad);
+                    in = row >= sa && row < sb;
+                }
+            }
+            const uint64_t bl = __ballot(in);
+            int base = 0;
+            if (lane == 0 && bl) base = atomicAdd(&L.meta[8], __popcll(bl));
+            base = __shfl(base, 0, 64);
+            const int k = base + __popcll(bl & (lane ? (~0ull >> (64 - lane)) : 0ull));
+            if (in && k < kBandCap) slist[k] = (uint16_t)i;
+        }
+        __syncthreads();
+        S = min(S, min(L.meta[8], kBandCap));
     }
+    SM_STAMP(6);
 
     // ---- stage the rows [sa, sb): their records, a counting sort by staged cell ----
     const int srows = sb - sa, scells = srows * nx;
@@ -1622,8 +1666,8 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             sinf[k] = ~0u;
             srec[k] = make_float2(0.f, 0.f);
             if (j < S) {
-                const double2 r = ba.rxy[row0 + j];
-                const int i = ba.ridx[row0 + j];
+                const int i = fullbox ? (int)slist[j] : ba.ridx[row0 + j];
+                const double2 r = fullbox ? make_double2(x[i], y[i]) : ba.rxy[row0 + j];
                 if (i >= 0 && i < m && isfinite(r.x) && isfinite(r.y)) {
                     int row, col, quad;
                     cell_of(r.x, r.y, row, col, quad);
