@@ -2560,6 +2560,24 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 // not yet joined in LDS.  A found edge is one global union of the two tile components, so the
 // global union-find sees about one operation per component pair per tile side.
 constexpr int kEdgeNodes = 72;
+// DBSCAN_AB_EDGE_STOP (timing builds only): 1 ends each trip after the node loads, 2 after the
+// LDS pre-join, 3 skips the global unions
+#ifndef DBSCAN_AB_EDGE_STOP
+#define DBSCAN_AB_EDGE_STOP 0
+#endif
+// DBSCAN_AB_EDGE_COUNT (counting builds only): edge_union's pair-test outcomes, summed over the
+// fit, read back (and cleared) by dbscan_ab_edge_counts() (tools/edge_probe.py)
+#ifndef DBSCAN_AB_EDGE_COUNT
+#define DBSCAN_AB_EDGE_COUNT 0
+#endif
+#if DBSCAN_AB_EDGE_COUNT
+__device__ unsigned long long g_edge_cnt[8];
+#define EDGE_CNT(k) atomicAdd(&g_edge_cnt[(k)], 1ull)
+#else
+#define EDGE_CNT(k) \
+    do {            \
+    } while (0)
+#endif
 
 // edge_union's full pair test (the reps were not within eps) and its global union.
 __device__ __forceinline__ bool edge_pair_full(const double2* __restrict__ xy, int4 me, int4 o,
@@ -2567,6 +2585,7 @@ __device__ __forceinline__ bool edge_pair_full(const double2* __restrict__ xy, i
     const auto gcore = [core](int j) { return core[j] != 0; };
     double px[kQReg], py[kQReg];
     const int na = load_own(xy, me, 0, px, py);
+    EDGE_CNT(na >= 0 ? 3 : 4);
     return na >= 0 ? pair_found(px, py, na, xy, o.x, o.y, (uint32_t)o.w, gcore, 0, eps2)
                    : pair_found_generic(xy, 0, me, o, gcore, eps2);
 }
@@ -2650,27 +2669,56 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                 fnb[w][f + 1] = incl - cnt;
                 fne[w][f + 1] = incl;
             }
-            for (int j = 0; j < cnt; ++j) {
-                const int idx = incl - cnt + j;
-                nqi[w][idx] = qinfo[q0 + j];
-                const int4 gq = qg[q0 + j];
-                ngq[w][idx] = make_int2(gq.x, gq.y);
-                ncomp[w][idx] = qcomp[q0 + j];  // tile component rep (a member of the set)
+            // node -> quarter index in LDS (lp, free until the pre-join), then a lane per node:
+            // the quarter loads of all nodes in flight at once, not one cell's per trip
+            for (int j = 0; j < cnt; ++j) lp[incl - cnt + j] = q0 + j;
+            wave_sync();
+            for (int i = lane; i < ntot; i += 64) {
+                const int q = lp[i];
+                const int4 qi = qinfo[q];
+                const int4 gq = qg[q];
+                const int qc = qcomp[q];  // tile component rep (a member of the set)
+                nqi[w][i] = qi;
+                ngq[w][i] = make_int2(gq.x, gq.y);
+                ncomp[w][i] = qc;
             }
         }
         wave_sync();
-        for (int i = lane; i < ntot; i += 64) {  // pre-join nodes sharing a tile component
-            const int c = ncomp[w][i];
-            int r = i;
-            if (c >= 0)
-                for (int j = i < nA ? 0 : nA; j < i; ++j)
-                    if (ncomp[w][j] == c) {
-                        r = j;
-                        break;
-                    }
-            lp[i] = r;
+        if (lane == 0) EDGE_CNT(0);
+        if (lane == 0 && ntot > 64) EDGE_CNT(7);
+        if (DBSCAN_AB_EDGE_STOP == 1) continue;
+        {
+            // pre-join nodes sharing a tile component (own nodes among themselves, facing nodes
+            // among themselves): lp[i] = the first such node.  Nodes 0..63 sit in the lanes, one
+            // ballot per distinct component (a per-lane scan of the earlier nodes cost ~40 us of
+            // the launch at 10^7); nodes 64.. (corner quarters) against the lanes, then each other
+            const int c = lane < ntot ? ncomp[w][lane] : -1;
+            const bool own = lane < nA;
+            int r = lane;
+            unsigned long long todo = __ballot(c >= 0);
+            while (todo) {
+                const int ld = __builtin_ctzll(todo);
+                const int lc = __shfl(c, ld, 64);
+                const unsigned long long m = __ballot(c == lc && own == (ld < nA)) & todo;
+                if ((m >> lane) & 1ull) r = ld;
+                todo &= ~m;
+            }
+            if (lane < ntot) lp[lane] = r;
+            for (int i = 64; i < ntot; ++i) {  // (wave-uniform; node i >= nA: a facing node)
+                const int ci = ncomp[w][i];
+                const unsigned long long m = __ballot(ci >= 0 && c == ci && !own);
+                int ri = m ? __builtin_ctzll(m) : i;
+                if (!m && ci >= 0)
+                    for (int j = 64; j < i; ++j)
+                        if (ncomp[w][j] == ci) {
+                            ri = j;
+                            break;
+                        }
+                if (lane == 0) lp[i] = ri;
+            }
         }
         wave_sync();
+        if (DBSCAN_AB_EDGE_STOP == 2) continue;
         const int a = lane & 31, half = lane >> 5;  // two lanes per own-strip quarter
         if (a < nA) {
             const int4 me = nqi[w][a];
@@ -2710,12 +2758,17 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                         if (sb[c] < 0 || sd[c] != sweep) continue;
                         const int b = sb[c];
                         if (lfind(lp, a) == lfind(lp, b)) continue;
+                        EDGE_CNT(sweep);
                         if (!within_eps(pr.x, pr.y, po[c].x, po[c].y, eps2) &&
                             !edge_pair_full(xy, me, nqi[w][b], core, eps2))
                             continue;
+                        EDGE_CNT(5);
                         // one global union per merge of two LDS sets: a lane that finds its
                         // pair already joined (another lane's merge) leaves the global sets alone
-                        if (lunite(lp, a, b)) edge_unite(parent, perm, ncomp[w][a], ncomp[w][b]);
+                        if (lunite(lp, a, b) && DBSCAN_AB_EDGE_STOP != 3) {
+                            EDGE_CNT(6);
+                            edge_unite(parent, perm, ncomp[w][a], ncomp[w][b]);
+                        }
                     }
             }
         }
@@ -4114,5 +4167,15 @@ extern "C" int dbscan_ab_stamps(long long* out, int n) {
     const size_t want = sizeof(long long) * (size_t)n;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ab_stamps), want < bytes ? want : bytes) ==
                    hipSuccess ? 0 : -1;
+}
+#endif
+
+#if DBSCAN_AB_EDGE_COUNT
+// Counting builds: copies edge_union's eight counters into out and clears them.
+extern "C" int dbscan_ab_edge_counts(unsigned long long* out) {
+    using namespace dbscan;
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_edge_cnt), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_edge_cnt), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -31,3 +31,9 @@ mkdir -p gpurun_out/ev/profiles
 PROF_DEST=gpurun_out/ev/profiles python3 tools/pmc_summary.py gpurun_out/prof ${TAG:-round_ev} > gpurun_out/ev/pmc_summary.txt 2>&1 || exit 1
 cp gpurun_out/prof/trace.log gpurun_out/ev/profile_trace.log
 rm -rf gpurun_out/prof
+# the default bench once more with this run's counters in place (profiles/pmc_traffic.json on the
+# box is the snapshot's; the one just written is stamped with the running sources), so the
+# committed default line carries roofline.traffic
+cp gpurun_out/ev/profiles/pmc_traffic.json profiles/pmc_traffic.json || exit 1
+run bench_default_traffic 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+grep -h '"traffic"' gpurun_out/ev/bench_default_traffic.log | cut -c1-120 || true
