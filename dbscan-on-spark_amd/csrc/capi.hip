@@ -193,6 +193,7 @@ struct dbscan_handle {
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
     void* fpinned = nullptr;          // partition-sized dbscan_fit_h: pinned x|y and cluster|flag
+    char* fpinned_dev = nullptr;      // ... its device address (the LDS forms write labels there)
     size_t fpinned_bytes = 0;
     dbscan::DevBuf hxy, hclfl;        // ... and their device twins (one copy each way)
     hipEvent_t ready = nullptr;       // marks the root count inside a prepare call
@@ -216,6 +217,9 @@ namespace {
 // dbscan_fit_h fits of at most this many points stage through one pinned block (21 B/point)
 constexpr int64_t kPinnedFitMax = 65536;  // (250 / 2000 / 8192 points: 101 / 151 / 240 ->
                                           // 65 / 119 / 207 us per call, one thread)
+// ... of which fits of at most this many points taking an LDS form get their labels written into
+// that block by the kernel itself
+constexpr int64_t kDirectOutMax = 16384;
 
 template <class F>
 int32_t guarded(dbscan_handle* h, F&& f) {
@@ -474,6 +478,9 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
                 const size_t cap = 21 * (size_t)kPinnedFitMax;
                 DBSCAN_HIP_CHECK(hipHostMalloc(&h->fpinned, cap, hipHostMallocDefault));
                 h->fpinned_bytes = cap;
+                void* dev = nullptr;
+                DBSCAN_HIP_CHECK(hipHostGetDevicePointer(&dev, h->fpinned, 0));
+                h->fpinned_dev = static_cast<char*>(dev);
             }
             char* pin = static_cast<char*>(h->fpinned);
             memcpy(pin, x, 8 * (size_t)n);
@@ -488,12 +495,23 @@ int32_t dbscan_fit_h(dbscan_handle* h, const double* x, const double* y, int64_t
             a.spread_min = h->spread_min;
             a.band_max = h->band_max;
             a.band_min = h->band_min;
+            // the LDS forms write cluster|flag straight into the pinned block (no copy back) up
+            // to kDirectOutMax points (250 / 2000 / 8192 points 2 us less per call; 4 executor
+            // threads over the 1597 G(10^7) partitions 80 -> 74 us per partition); above it
+            // their scattered label writes over PCIe cost more than the copy (65536 points: 277
+            // -> 343 us per call)
+            if (n <= kDirectOutMax) {
+                a.cluster_host = reinterpret_cast<int32_t*>(h->fpinned_dev + in_b);
+                a.flag_host = reinterpret_cast<uint8_t*>(h->fpinned_dev + in_b + 4 * (size_t)n);
+            }
             h->prepared = false;
             dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
-            DBSCAN_HIP_CHECK(
-                hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
+            const bool direct = h->ws.out_direct;
+            if (!direct)
+                DBSCAN_HIP_CHECK(
+                    hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
             h->stats = dbscan::read_fit_stats(h->stream, h->ws, &h->prof);  // (synchronizes)
-            if (h->ws.spread_recovered) {  // the fit was re-run: its labels copied back again
+            if (h->ws.spread_recovered && !direct) {  // re-run fit: its labels copied back again
                 DBSCAN_HIP_CHECK(
                     hipMemcpyAsync(pin + in_b, dout, out_b, hipMemcpyDeviceToHost, h->stream));
                 DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));

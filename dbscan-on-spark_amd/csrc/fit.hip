@@ -3546,6 +3546,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                  SlabState* slab) {
     if (slab) slab->valid = false;
     ws.fit_mirrored = false;
+    ws.out_direct = false;
     ws.spread_recall.valid = false;
     ws.recall_band = false;
     const int64_t n = a.n;
@@ -3573,19 +3574,24 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         small_fit_eligible(n, a.eps, a.mode)) {
         StageTimer t(prof, s, "small_fit");
         double* mirror = stats_mirror(ws);  // (LDS fits write their stats there: no copy back)
+        // (and their labels into pinned host buffers when the caller passes them: one launch,
+        // no copy back; a recall re-runs into the same buffers)
+        ws.out_direct = a.cluster_host != nullptr;
+        int32_t* const cl = ws.out_direct ? a.cluster_host : a.cluster;
+        uint8_t* const fl = ws.out_direct ? a.flag_host : a.flag;
         // (from band_min points the band form: its cooperative staging and quarter unions
         // measured faster than the spread form from ~3000 points (133 -> 121 us at 8192) in its
         // first form, from ~400 points since: 2000 / 600 points 77 / 64 us against 82 / 73)
         if (n >= a.band_min && n <= a.band_max && !a.batch &&
             band_fit_eligible(n, a.eps, a.mode, a.min_points))
-            enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
-                             a.flag, gp, st, mirror);
+            enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, cl, fl, gp,
+                             st, mirror);
         else if (n >= a.spread_min)  // several workgroups, two grid barriers (spread_fit_kernel)
-            enqueue_spread_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
-                               a.flag, gp, st, mirror);
+            enqueue_spread_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, cl, fl, gp,
+                               st, mirror);
         else
             enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
-                               a.mode, a.cluster, a.flag, nullptr, gp, st, mirror);
+                               a.mode, cl, fl, nullptr, gp, st, mirror);
         ws.fit_mirrored = true;
         return;
     }
@@ -3594,8 +3600,10 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         band_fit_eligible(n, a.eps, a.mode, a.min_points)) {
         StageTimer t(prof, s, "band_fit");
         double* mirror = stats_mirror(ws);
-        enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, a.cluster,
-                         a.flag, gp, st, mirror);
+        ws.out_direct = a.cluster_host != nullptr;
+        enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode,
+                         ws.out_direct ? a.cluster_host : a.cluster,
+                         ws.out_direct ? a.flag_host : a.flag, gp, st, mirror);
         ws.fit_mirrored = true;
         return;
     }

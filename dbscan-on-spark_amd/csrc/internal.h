@@ -181,6 +181,7 @@ struct Workspace {
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
     double* stats_dev = nullptr;   // ... its device address (LDS fits write it directly)
     bool fit_mirrored = false;     // the last fit wrote its stats into stats_host itself
+    bool out_direct = false;       // ... and its labels into FitArgs::cluster_host / flag_host
     // The last spread fit's arguments (small.hip): when a grid barrier of it gave up
     // (st[kStError] == 2: its workgroups were not all resident), read_fit_stats re-runs the
     // fit through the one-workgroup kernel (no barrier; the same results bit for bit).
@@ -317,6 +318,10 @@ struct FitArgs {
     int64_t band_min = 0;  // (LDS-sized fits of >= band_min points also take the band form)
     // batched fit (n = the batch's span, cluster ids numbered per partition): see BatchFit
     const BatchFit* batch = nullptr;
+    // device pointers of pinned host buffers for cluster / flag: the LDS forms (one launch)
+    // write the labels there themselves, no copy back (Workspace::out_direct tells)
+    int32_t* cluster_host = nullptr;
+    uint8_t* flag_host = nullptr;
 };
 
 // What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).
