@@ -199,3 +199,32 @@ def test_band_from_concurrent_handles(dm):
         for hh in handles:
             hh.close()
     assert not errors, errors[0]
+
+
+def test_band_labels_written_into_pinned_block(dm):
+    """dbscan_fit_h up to 16384 points: the LDS kernels write cluster|flag into the handle's
+    pinned block themselves (capi.hip kDirectOutMax); above it the labels come back by copy.
+    Both sides of the limit, and the recalls that re-run such a fit through the tiled pipeline
+    into the same block (a staging overflow, a barrier that gives up), equal the oracle."""
+    rng = np.random.default_rng(16384)
+    h = dm.Handle(0)
+    try:
+        for m in (7000, 16384, 16385):
+            x, y = _set(rng, m)
+            _eq(dm.fit_arrays(x, y, 0.12, 6, 0, handle=h), O.fit_grid(x, y, 0.12, 6, 0),
+                f"m={m}")
+        before = h.spread_fallbacks()
+        m = 12000  # one thin strip: its row is over a band's staging capacity
+        x = rng.uniform(0, 50, m)
+        y = rng.uniform(0, 0.05, m)
+        _eq(dm.fit_arrays(x, y, 0.2, 10, 1, handle=h), O.fit_grid(x, y, 0.2, 10, 1), "strip")
+        assert h.spread_fallbacks() == before + 1
+        x2, y2 = _set(rng, 9000)
+        ref2 = O.fit_grid(x2, y2, 0.12, 6, 0)
+        h.set_spread_spin_limit(0)
+        _eq(dm.fit_arrays(x2, y2, 0.12, 6, 0, handle=h), ref2, "barrier give-up")
+        assert h.spread_fallbacks() == before + 2
+        h.set_spread_spin_limit(1 << 21)
+        _eq(dm.fit_arrays(x2, y2, 0.12, 6, 0, handle=h), ref2, "default bound")
+    finally:
+        h.close()
