@@ -2562,6 +2562,11 @@ __global__ __launch_bounds__(kBlock) void union_kernel(const double2* __restrict
 constexpr int kEdgeNodes = 72;
 // DBSCAN_AB_EDGE_STOP (timing builds only): 1 ends each trip after the node loads, 2 after the
 // LDS pre-join, 3 skips the global unions
+// edge_union_kernel's launch bound, waves per SIMD: 5 (96 VGPRs, no scratch) measured 0.166 ->
+// 0.153 ms at config 2 against 6 (80 VGPRs, 48 B of scratch); 4: 0.178
+#ifndef DBSCAN_AB_EDGE_W
+#define DBSCAN_AB_EDGE_W 5
+#endif
 #ifndef DBSCAN_AB_EDGE_STOP
 #define DBSCAN_AB_EDGE_STOP 0
 #endif
@@ -3892,7 +3897,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             StageTimer t(prof, s, "union_edge");
             // (+ union_kernel's blocks: a no-op on clique grids, the only union on the others)
             const unsigned ug = std::min(nblk(n), 2048u);
-            klaunch(prof, "edge_union", edge_union_kernel<6>, dim3(tile_grid + ug), dim3(kBlock), 0,
+            klaunch(prof, "edge_union", edge_union_kernel<DBSCAN_AB_EDGE_W>, dim3(tile_grid + ug), dim3(kBlock), 0,
                     s, xy, &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
                     (const uint8_t*)tcore, (int)tile_grid, cell, seg, nf_p);
             DBSCAN_HIP_CHECK(hipGetLastError());
