@@ -2567,6 +2567,11 @@ constexpr int kEdgeNodes = 72;
 #ifndef DBSCAN_AB_EDGE_W
 #define DBSCAN_AB_EDGE_W 5
 #endif
+// big_count_kernel's launch bound, waves per SIMD: 7 (71 VGPRs, no scratch) measured 0.113 ->
+// 0.103 ms at config 2 against 5 (81 VGPRs); 6: 0.111; 8 spills
+#ifndef DBSCAN_AB_BIGC_W
+#define DBSCAN_AB_BIGC_W 7
+#endif
 #ifndef DBSCAN_AB_EDGE_STOP
 #define DBSCAN_AB_EDGE_STOP 0
 #endif
@@ -3852,7 +3857,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
                         dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
                         a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
-                klaunch(prof, "big_count", big_count_kernel<5>, dim3(tile_grid), dim3(kBlock), 0,
+                klaunch(prof, "big_count", big_count_kernel<DBSCAN_AB_BIGC_W>, dim3(tile_grid), dim3(kBlock), 0,
                         s, xy, cell, seg, tstart, qidx, eps2, a.min_points, core,
                         block_cores + tile_grid, nbr, nbr_k, fa);
                 // one workgroup per big tile up to kTileGrid (a grid of 2048 gave the tiles past
