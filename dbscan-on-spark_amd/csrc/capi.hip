@@ -189,7 +189,6 @@ struct dbscan_handle {
     int64_t band_max = DBSCAN_BAND_DEFAULT_POINTS;      // band fits above the LDS capacity
     int64_t band_min = DBSCAN_BAND_MIN_DEFAULT_POINTS;  // ... and inside it from this many points
     bool pending = false;             // an asynchronous fit whose stats are not read yet
-    int32_t* pending_nk = nullptr;    // ... and the device word its cluster count went to
     bool prepared = false;            // dbscan_slab_roots_prepare_device ran since the slab fit
     void* pinned = nullptr;           // small pinned host block (stats, root count)
     void* fpinned = nullptr;          // partition-sized dbscan_fit_h: pinned x|y and cluster|flag
@@ -358,15 +357,18 @@ void* dbscan_stream(dbscan_handle* h) { return h ? (void*)h->stream : nullptr; }
 namespace {
 // Completes an asynchronous fit on the host side: waits for the stream, reads its stats
 // (raising a device-side error such as an unsizable grid) and accumulates the stage timers.
+// Every queued spread / band fit is checked (and re-run when a barrier gave up or a band
+// overflowed), not only the last one: each has its own stats block and recall record.
 void settle(dbscan_handle* h) {
-    if (!h->pending) return;
+    if (!h->pending) {
+        if (!h->ws.recalls.empty()) {  // (fits queued before a call that consumed the stats)
+            DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
+            dbscan::drain_recalls(h->stream, &h->prof, h->ws);
+        }
+        return;
+    }
     h->pending = false;
     h->stats = dbscan::read_fit_stats(h->stream, h->ws, &h->prof);
-    if (h->ws.spread_recovered && h->pending_nk) {  // (the re-run fit's count, like the first)
-        dbscan::write_nclusters(h->stream, h->ws, h->pending_nk);
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(h->stream));
-    }
-    h->pending_nk = nullptr;
     h->prof.flush();
 }
 }  // namespace
@@ -397,7 +399,9 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         std::lock_guard<std::mutex> lk(h->mu);
         check_fit_args(n, eps, mode, d_x, d_y, d_cluster, d_flag, true);
         if (h->pending && h->prof.pending.size() > 4096) settle(h);  // bound the event backlog
-        h->pending = false;  // a newer fit replaces the unread stats of an older one
+        // a newer fit replaces the unread stats of an older one; the older one's outcome stays
+        // in its own stats block and recall record (checked by dbscan_sync)
+        h->pending = false;
         dbscan::FitArgs a{d_x, d_y, nullptr, n, eps, min_points, mode, d_cluster, d_flag,
                           nullptr, nullptr};
         a.small_max = h->small_max;
@@ -408,7 +412,6 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
         h->pending = true;
-        h->pending_nk = d_n_clusters;
         return DBSCAN_OK;
     });
 }

@@ -87,6 +87,36 @@ __device__ long long g_ab_stamps[kTileGrid * kStamps];
     } while (0)
 #endif
 
+// DBSCAN_AB_CHECK (checking builds only, never the shipped library): edge_union's indices and
+// the pair tests' slot indices checked against their ranges; an index out of range is counted
+// per site (with the lowest and highest value seen) and clamped into range, so the checking
+// build never faults.  Read back (and cleared) by dbscan_ab_bounds() (tools/bounds_probe.py).
+// DBSCAN_AB_PAIR4 rebuilds the round-5 pair-test variant "the other quarter's cores four at a
+// time, their loads in flight together" (DESIGN_LOG round 5), the build that faulted once.
+#ifndef DBSCAN_AB_CHECK
+#define DBSCAN_AB_CHECK 0
+#endif
+#ifndef DBSCAN_AB_PAIR4
+#define DBSCAN_AB_PAIR4 0
+#endif
+#if DBSCAN_AB_CHECK
+constexpr int kChkSites = 12;
+__device__ unsigned long long g_chk_bad[kChkSites];
+#define CHK_12(v) {v, v, v, v, v, v, v, v, v, v, v, v}
+__device__ long long g_chk_lo[kChkSites] = CHK_12(INT64_MAX);
+__device__ long long g_chk_hi[kChkSites] = CHK_12(INT64_MIN);
+__device__ __forceinline__ int64_t chk_idx(int site, int64_t i, int64_t lo, int64_t hi) {
+    if (i >= lo && i < hi) return i;
+    atomicAdd(&g_chk_bad[site], 1ull);
+    atomicMin(&g_chk_lo[site], (long long)i);
+    atomicMax(&g_chk_hi[site], (long long)i);
+    return hi > lo ? (i < lo ? lo : hi - 1) : lo;
+}
+#define CHK(site, i, lo, hi) ((std::remove_reference_t<decltype(i)>)chk_idx((site), (int64_t)(i), (int64_t)(lo), (int64_t)(hi)))
+#else
+#define CHK(site, i, lo, hi) (i)
+#endif
+
 // DBSCANPoint.scala:26-30 as used at LocalDBSCANNaive.scala:77.  Two rounded subtractions,
 // two rounded multiplies, one rounded add, <=.  The whole library is built with
 // -ffp-contract=off; the pragma pins it here as well.
@@ -1142,10 +1172,33 @@ __device__ __forceinline__ bool pair_found(const double* px, const double* py, i
                                            uint32_t bmask, CoreF core, int boff, double eps2) {
     if (b1 - b0 <= 32) {
         uint32_t m = bmask;
+#if DBSCAN_AB_PAIR4
+        // (the round-5 variant: four cores per trip, loads in flight together; at a tail of
+        // fewer than four set bits __ffs(0) - 1 = -1 indexes the slot BEFORE the quarter)
+        while (m) {
+            int j[4];
+            double2 pb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                j[u] = __ffs(m) - 1;
+                m &= m - 1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pb[u] = src[b0 - boff + CHK(0, j[u], 0, b1 - b0)];
+            bool f = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < kQReg; ++k)
+                    f |= (j[u] >= 0) && (k < na) && within_eps(px[k], py[k], pb[u].x, pb[u].y, eps2);
+            if (f) return true;
+        }
+        return false;
+#endif
         while (m) {
             const int j = __ffs(m) - 1;
             m &= m - 1;
-            const double2 pb = src[b0 - boff + j];
+            const double2 pb = src[b0 - boff + CHK(0, j, 0, b1 - b0)];
             bool f = false;
 #pragma unroll
             for (int k = 0; k < kQReg; ++k) f |= (k < na) && within_eps(px[k], py[k], pb.x, pb.y, eps2);
@@ -1181,7 +1234,7 @@ __device__ __forceinline__ int load_own(const Src* __restrict__ src, int4 me, in
         if (m) {
             const int j = __ffs(m) - 1;
             m &= m - 1;
-            const double2 v = src[me.x - off + j];
+            const double2 v = src[me.x - off + CHK(1, j, 0, me.y - me.x)];
             px[k] = v.x;
             py[k] = v.y;
             na = k + 1;
@@ -2658,6 +2711,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             }
             int cnt = 0, q0 = 0;
             if (occ >= 0) {
+                occ = CHK(7, occ, 0, ntiles);
                 q0 = tq[(int64_t)occ * kTslot + l];
                 cnt = tq[(int64_t)occ * kTslot + l + 1] - q0;
             }
@@ -2684,7 +2738,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             for (int j = 0; j < cnt; ++j) lp[incl - cnt + j] = q0 + j;
             wave_sync();
             for (int i = lane; i < ntot; i += 64) {
-                const int q = lp[i];
+                const int q = lp[CHK(2, i, 0, kEdgeNodes)];
                 const int4 qi = qinfo[q];
                 const int4 gq = qg[q];
                 const int qc = qcomp[q];  // tile component rep (a member of the set)
@@ -2741,12 +2795,12 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                 int sb[6], sd[6];
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
-                    const int f = flo + (c >> 1);
+                    const int f = CHK(3, flo + (c >> 1) + 1, 0, 10) - 1;
                     const int b = fnb[w][f + 1] + half + 2 * (c & 1);
                     sb[c] = -1;
                     sd[c] = 0;
                     if (b < fne[w][f + 1]) {
-                        const int2 og = ngq[w][b];
+                        const int2 og = ngq[w][CHK(4, b, 0, ntot)];
                         const int d = max(abs(og.x - mg.x), abs(og.y - mg.y));
                         if (d <= 2 && nqi[w][b].z >= 0) {
                             sb[c] = b;
@@ -2756,11 +2810,11 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                 }
                 // each pair's first test: the two quarters' reps (cores), all loads in flight
                 // together; the full test only where the reps are not within eps
-                const double2 pr = xy[me.z];
+                const double2 pr = xy[CHK(5, me.z, 0, *nf_p)];
                 double2 po[6];
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
-                    po[c] = sb[c] >= 0 ? xy[nqi[w][sb[c]].z] : make_double2(0.0, 0.0);
+                    po[c] = sb[c] >= 0 ? xy[CHK(5, nqi[w][sb[c]].z, 0, *nf_p)] : make_double2(0.0, 0.0);
 #pragma unroll 1
                 for (int sweep = 1; sweep <= 2; ++sweep)
 #pragma unroll
@@ -2777,7 +2831,8 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                         // pair already joined (another lane's merge) leaves the global sets alone
                         if (lunite(lp, a, b) && DBSCAN_AB_EDGE_STOP != 3) {
                             EDGE_CNT(6);
-                            edge_unite(parent, perm, ncomp[w][a], ncomp[w][b]);
+                            edge_unite(parent, perm, CHK(6, ncomp[w][a], 0, *nf_p),
+                                       CHK(6, ncomp[w][b], 0, *nf_p));
                         }
                     }
             }
@@ -3540,25 +3595,61 @@ static const int32_t* resolve_box_pairs(hipStream_t s, Workspace& ws, int32_t* s
 // from the device bbox (no host readback), the radix sort skips the key digits the grid does
 // not use, and the clique (quarter-cell) and per-point union paths are both enqueued, each
 // exiting at once when the grid selects the other.
-// The handle's pinned stats block and its device address (allocated on first use).
-static double* stats_mirror(Workspace& ws) {
-    if (!ws.stats_host) {
+// The handle's pinned stats block (the tiled pipeline's stats are copied there).
+static void stats_block(Workspace& ws) {
+    if (!ws.stats_host)
         DBSCAN_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ws.stats_host),
-                                       kFitStatsDoubles * sizeof(double),
+                                       kFitStatsDoubles * sizeof(double), hipHostMallocDefault));
+}
+
+// A stats block of the ring for one LDS fit (Workspace::ring_host), its kStError cleared by the
+// host: the block belongs to this fit alone, and no earlier fit still queued can write it (a
+// block is reused only after the stream has drained since it was taken: a full ring drains
+// the stream and the queued fits' recalls first).  Returns the device address.
+static double* take_stat_block(hipStream_t s, Profiler* prof, Workspace& ws) {
+    if (!ws.ring_host) {
+        DBSCAN_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ws.ring_host),
+                                       (size_t)Workspace::kStatRing * Workspace::kStatBlock *
+                                           sizeof(double),
                                        hipHostMallocMapped | hipHostMallocCoherent));
-        DBSCAN_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ws.stats_dev),
-                                                 ws.stats_host, 0));
+        DBSCAN_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ws.ring_dev),
+                                                 ws.ring_host, 0));
+        ws.ring_next = ws.ring_used = 0;
     }
-    return ws.stats_dev;
+    if (ws.ring_used >= Workspace::kStatRing) {
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        drain_recalls(s, prof, ws);  // (resets ring_used)
+        ws.ring_used = 0;
+    }
+    const int k = ws.ring_next;
+    ws.ring_next = (k + 1) % Workspace::kStatRing;
+    ++ws.ring_used;
+    double* host = ws.ring_host + (size_t)k * Workspace::kStatBlock;
+    reinterpret_cast<int32_t*>(host + kMiscState)[kStError] = 0;
+    ws.fit_block = host;
+    return ws.ring_dev + (size_t)k * Workspace::kStatBlock;
 }
 
 void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                  SlabState* slab) {
+    // Which form: partition-sized full fits (the seam's usual call, DBSCAN.scala:150-155) take
+    // one launch with everything in LDS (small.hip), one workgroup or several; larger ones the
+    // tiled pipeline below.
+    const bool lds_small = !a.zone && a.n > 0 && a.n <= std::min<int64_t>(a.small_max, kSmallMaxPoints) &&
+                           small_fit_eligible(a.n, a.eps, a.mode);
+    const bool lds_band = !lds_small && !a.zone && !a.batch && a.n > 0 &&
+                          a.small_max >= kSmallMaxPoints && a.n <= a.band_max &&
+                          band_fit_eligible(a.n, a.eps, a.mode, a.min_points);
+    // Queued spread / band fits not yet checked are re-run (if they must be) in the tiled
+    // pipeline's buffers: settled before a tiled fit uses those buffers (its slab state must
+    // survive until the label phase).  (Mixing the forms on one handle without a sync is rare.)
+    if (!lds_small && !lds_band && !ws.recalls.empty()) {
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+        drain_recalls(s, prof, ws);
+    }
     if (slab) slab->valid = false;
     ws.fit_mirrored = false;
     ws.out_direct = false;
-    ws.spread_recall.valid = false;
-    ws.recall_band = false;
     const int64_t n = a.n;
     const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
     const int mode =
@@ -3578,42 +3669,47 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         return;
     }
     const int32_t* nf_p = &st[kStNf];
-    // partition-sized full fits (the seam's usual call, DBSCAN.scala:150-155): one launch,
-    // everything in LDS (small.hip), one workgroup or several; the kernel zeroes the fit state
-    if (!a.zone && n <= std::min<int64_t>(a.small_max, kSmallMaxPoints) &&
-        small_fit_eligible(n, a.eps, a.mode)) {
-        StageTimer t(prof, s, "small_fit");
-        double* mirror = stats_mirror(ws);  // (LDS fits write their stats there: no copy back)
-        // (and their labels into pinned host buffers when the caller passes them: one launch,
-        // no copy back; a recall re-runs into the same buffers)
-        ws.out_direct = a.cluster_host != nullptr;
-        int32_t* const cl = ws.out_direct ? a.cluster_host : a.cluster;
-        uint8_t* const fl = ws.out_direct ? a.flag_host : a.flag;
+    if (lds_small || lds_band) {
         // (from band_min points the band form: its cooperative staging and quarter unions
         // measured faster than the spread form from ~3000 points (133 -> 121 us at 8192) in its
         // first form, from ~400 points since: 2000 / 600 points 77 / 64 us against 82 / 73)
-        if (n >= a.band_min && n <= a.band_max && !a.batch &&
-            band_fit_eligible(n, a.eps, a.mode, a.min_points))
+        const bool band = lds_band || (n >= a.band_min && n <= a.band_max && !a.batch &&
+                                       band_fit_eligible(n, a.eps, a.mode, a.min_points));
+        const bool spread = !band && n >= a.spread_min;  // two grid barriers (spread_fit_kernel)
+        StageTimer t(prof, s, band ? "band_fit" : "small_fit");
+        // (LDS fits write their stats into a pinned block of their own: no copy back)
+        double* mirror = take_stat_block(s, prof, ws);
+        // (and their labels into pinned host buffers when the caller passes them: one launch,
+        // no copy back; a re-run writes the device twins and copies them there in one DMA)
+        ws.out_direct = a.cluster_host != nullptr;
+        int32_t* const cl = ws.out_direct ? a.cluster_host : a.cluster;
+        uint8_t* const fl = ws.out_direct ? a.flag_host : a.flag;
+        if (band || spread) {  // a grid barrier may give up, a band overflow: a recall record
+            Workspace::Recall r;
+            r.band = band;
+            r.x = a.x;
+            r.y = a.y;
+            r.n = n;
+            r.eps = a.eps;
+            r.min_points = a.min_points;
+            r.mode = a.mode;
+            r.cluster = cl;
+            r.flag = fl;
+            r.dev_cluster = ws.out_direct ? a.cluster : nullptr;
+            r.dev_flag = ws.out_direct ? a.flag : nullptr;
+            r.block_host = ws.fit_block;
+            r.block_dev = mirror;
+            ws.recalls.push_back(r);
+        }
+        if (band)
             enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, cl, fl, gp,
                              st, mirror);
-        else if (n >= a.spread_min)  // several workgroups, two grid barriers (spread_fit_kernel)
+        else if (spread)
             enqueue_spread_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode, cl, fl, gp,
                                st, mirror);
         else
             enqueue_small_fits(s, prof, a.x, a.y, nullptr, nullptr, 1, n, a.eps, a.min_points,
                                a.mode, cl, fl, nullptr, gp, st, mirror);
-        ws.fit_mirrored = true;
-        return;
-    }
-    // partitions above the LDS capacity (the seam's dense rectangles): one launch over bands
-    if (!a.zone && !a.batch && a.small_max >= kSmallMaxPoints && n <= a.band_max &&
-        band_fit_eligible(n, a.eps, a.mode, a.min_points)) {
-        StageTimer t(prof, s, "band_fit");
-        double* mirror = stats_mirror(ws);
-        ws.out_direct = a.cluster_host != nullptr;
-        enqueue_band_fit(s, prof, ws, a.x, a.y, n, a.eps, a.min_points, a.mode,
-                         ws.out_direct ? a.cluster_host : a.cluster,
-                         ws.out_direct ? a.flag_host : a.flag, gp, st, mirror);
         ws.fit_mirrored = true;
         return;
     }
@@ -4035,6 +4131,31 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     }
 }
 
+#if DBSCAN_AB_CHECK
+// checking builds: per site {count, lowest, highest} out-of-range indices since the last read
+extern "C" int dbscan_ab_bounds(long long* out) {
+    unsigned long long bad[kChkSites];
+    long long lo[kChkSites], hi[kChkSites];
+    if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_chk_bad), sizeof(bad)) != hipSuccess ||
+        hipMemcpyFromSymbol(lo, HIP_SYMBOL(g_chk_lo), sizeof(lo)) != hipSuccess ||
+        hipMemcpyFromSymbol(hi, HIP_SYMBOL(g_chk_hi), sizeof(hi)) != hipSuccess)
+        return -1;
+    for (int k = 0; k < kChkSites; ++k) {
+        out[3 * k] = (long long)bad[k];
+        out[3 * k + 1] = bad[k] ? lo[k] : 0;
+        out[3 * k + 2] = bad[k] ? hi[k] : 0;
+        bad[k] = 0;
+        lo[k] = INT64_MAX;
+        hi[k] = INT64_MIN;
+    }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_chk_bad), bad, sizeof(bad)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_chk_lo), lo, sizeof(lo)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_chk_hi), hi, sizeof(hi)) != hipSuccess)
+        return -1;
+    return kChkSites;
+}
+#endif
+
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
     if (ws.fit_n == 0) {
         DBSCAN_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(int32_t), s));
@@ -4043,25 +4164,85 @@ void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
     const int32_t* st = reinterpret_cast<const int32_t*>(static_cast<double*>(ws.misc.p) + kMiscState);
     hipLaunchKernelGGL(nclusters_kernel, dim3(1), dim3(1), 0, s, st, d_out);
     DBSCAN_HIP_CHECK(hipGetLastError());
+    // (a re-run of this fit rewrites the word: drain_recalls)
+    if (ws.fit_mirrored && !ws.recalls.empty() && ws.recalls.back().block_host == ws.fit_block)
+        ws.recalls.back().nk = d_out;
 }
 
 void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst) {
-    if (ws.fit_n == 0 || ws.fit_mirrored) return;  // (mirrored: parse reads stats_host)
+    if (ws.fit_n == 0 || ws.fit_mirrored) return;  // (mirrored: parse reads the fit's block)
     DBSCAN_HIP_CHECK(
         hipMemcpyAsync(dst, ws.misc.p, kFitStatsDoubles * sizeof(double), hipMemcpyDeviceToHost, s));
 }
 
+bool drain_recalls(hipStream_t s, Profiler* prof, Workspace& ws) {
+    ws.ring_used = 0;  // (the stream has drained: every block taken so far is free)
+    if (ws.recalls.empty()) return false;
+    std::vector<Workspace::Recall> list;
+    list.swap(ws.recalls);
+    // the last fit's state (a re-run below enqueues fits of its own)
+    const int64_t fit_n = ws.fit_n;
+    const int fit_mode = ws.fit_mode;
+    const bool mirrored = ws.fit_mirrored, direct = ws.out_direct;
+    double* const block = ws.fit_block;
+    bool last = false, any = false;
+    int32_t* const st = reinterpret_cast<int32_t*>(static_cast<double*>(ws.misc.p) + kMiscState);
+    GridParams* const gp = reinterpret_cast<GridParams*>(static_cast<double*>(ws.misc.p) + kMiscGrid);
+    for (const Workspace::Recall& r : list) {
+        const int32_t e = reinterpret_cast<const int32_t*>(r.block_host + kMiscState)[kStError];
+        if (!(e == 2 || (r.band && e == 3))) continue;
+        any = true;
+        int32_t* cl = r.dev_cluster ? r.dev_cluster : r.cluster;
+        uint8_t* fl = r.dev_cluster ? r.dev_flag : r.flag;
+        if (r.band) {  // the tiled pipeline (no LDS fit, no band fit); its stats to the block
+            FitArgs b{r.x, r.y, nullptr, r.n, r.eps, r.min_points, r.mode, cl, fl, nullptr,
+                      nullptr};
+            b.small_max = 0;
+            enqueue_fit(s, ws, prof, b, nullptr);
+            enqueue_fit_stats_copy(s, ws, r.block_host);
+        } else {  // the one-workgroup kernel: no grid barrier, every label and statistic
+            enqueue_small_fits(s, prof, r.x, r.y, nullptr, nullptr, 1, r.n, r.eps, r.min_points,
+                               r.mode, cl, fl, nullptr, gp, st, r.block_dev);
+        }
+        if (r.dev_cluster) {  // direct fits: the labels to the caller's pinned block, one DMA each
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(r.cluster, cl, (size_t)r.n * sizeof(int32_t),
+                                            hipMemcpyDeviceToDevice, s));
+            DBSCAN_HIP_CHECK(hipMemcpyAsync(r.flag, fl, (size_t)r.n, hipMemcpyDeviceToDevice, s));
+        }
+        if (r.nk) {
+            hipLaunchKernelGGL(nclusters_kernel, dim3(1), dim3(1), 0, s, st, r.nk);
+            DBSCAN_HIP_CHECK(hipGetLastError());
+        }
+        ++ws.spread_fallbacks;
+        if (r.block_host == block) last = true;
+    }
+    if (any) {
+        // (a barrier that gave up left the band scratch to its last workgroup's cleanup; zeroed
+        // again ahead of the next band fit all the same)
+        ws.band_ready = false;
+        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    ws.fit_n = fit_n;
+    ws.fit_mode = fit_mode;
+    ws.fit_mirrored = mirrored;
+    ws.out_direct = direct;
+    ws.fit_block = block;
+    ws.ring_used = 0;
+    return last;
+}
+
 FitStats read_fit_stats(hipStream_t s, Workspace& ws, Profiler* prof) {
-    stats_mirror(ws);  // (pinned: a pageable copy costs a staging pass per fit)
+    stats_block(ws);  // (pinned: a pageable copy costs a staging pass per fit)
     enqueue_fit_stats_copy(s, ws, ws.stats_host);
-    if (ws.fit_n != 0) DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-    // a spread fit whose workgroups were not all resident: re-run by one workgroup
-    ws.spread_recovered = recover_spread_fit(s, prof, ws);
+    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
+    // queued spread / band fits whose workgroups were not all resident (or whose band
+    // overflowed): re-run, each into its own outputs
+    ws.spread_recovered = drain_recalls(s, prof, ws);
     return parse_fit_stats(ws, ws.stats_host);
 }
 
 FitStats parse_fit_stats(const Workspace& ws, const double* buf) {
-    if (ws.fit_mirrored) buf = ws.stats_host;  // (an LDS fit wrote it; no copy was made)
+    if (ws.fit_mirrored) buf = ws.fit_block;  // (an LDS fit wrote it; no copy was made)
     FitStats stats;
     stats.n = ws.fit_n;
     stats.grid_mode = ws.fit_mode;

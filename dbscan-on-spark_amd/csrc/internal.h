@@ -179,32 +179,48 @@ struct Workspace {
         spread, band;
     bool spread_ready = false;  // spread.p holds zeroed barrier words (small.hip)
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
-    double* stats_dev = nullptr;   // ... its device address (LDS fits write it directly)
-    bool fit_mirrored = false;     // the last fit wrote its stats into stats_host itself
+    bool fit_mirrored = false;     // the last fit (an LDS form) wrote its stats into fit_block
     bool out_direct = false;       // ... and its labels into FitArgs::cluster_host / flag_host
-    // The last spread fit's arguments (small.hip): when a grid barrier of it gave up
-    // (st[kStError] == 2: its workgroups were not all resident), read_fit_stats re-runs the
-    // fit through the one-workgroup kernel (no barrier; the same results bit for bit).
-    struct SpreadRecall {
-        bool valid = false;
+    // Every LDS fit (small.hip: one-workgroup, spread and band forms) writes its statistics,
+    // kStError included, into a pinned block of its OWN, taken from a ring: fits queued back to
+    // back on the stream never share one, so each one's outcome survives until the host reads
+    // it.  A block is reused only after the stream has drained since it was taken.
+    static constexpr int kStatRing = 64;
+    // block stride, doubles: the misc block's layout up to the whole FitState (kStCount ints
+    // from kMiscState, which the LDS kernels zero: 320 B, past a 32-double copy's 256 B)
+    static constexpr int kStatBlock = 64;
+    double* ring_host = nullptr;   // kStatRing blocks of kStatBlock doubles
+    double* ring_dev = nullptr;    // ... their device address
+    int ring_next = 0;             // the next block to take
+    int ring_used = 0;             // blocks taken since the stream last drained
+    double* fit_block = nullptr;   // the last LDS fit's block (host address)
+    // A spread or band fit queued and not checked yet: when a grid barrier of it gave up
+    // (kStError 2: its workgroups were not all resident) or a band overflowed its staging (3),
+    // drain_recalls re-runs it (one-workgroup kernel / tiled pipeline: the same results bit for
+    // bit) into its own outputs.  Every queued fit has its own record, checked in stream order.
+    struct Recall {
+        bool band = false;
         const double *x = nullptr, *y = nullptr;
         int64_t n = 0;
         double eps = 0.0;
         int32_t min_points = 0, mode = 0;
-        int32_t* cluster = nullptr;
+        int32_t* cluster = nullptr;  // where the fit wrote its labels (may be host-mapped)
         uint8_t* flag = nullptr;
-        GridParams* gp = nullptr;
-        int32_t* st = nullptr;
-        double* mirror = nullptr;
-    } spread_recall;
-    bool recall_band = false;               // ... and it was a band fit (band_fit_kernel)
+        int32_t* dev_cluster = nullptr;  // direct fits: device twins a re-run writes into, then
+        uint8_t* dev_flag = nullptr;     // ... copied to cluster / flag in one DMA (or nullptr)
+        int32_t* nk = nullptr;           // device word its cluster count was copied to
+        double* block_host = nullptr;    // its stats block
+        double* block_dev = nullptr;
+    };
+    std::vector<Recall> recalls;
     bool band_ready = false;                // band.p holds zeroed barrier words (small.hip)
     uint32_t spread_spin_limit = 1u << 21;  // barrier polls before giving up (0: at once; tests)
-    int64_t spread_fallbacks = 0;           // spread fits re-run by the one-workgroup kernel
-    bool spread_recovered = false;          // the last read_fit_stats re-ran the fit
+    int64_t spread_fallbacks = 0;           // spread / band fits re-run (drain_recalls)
+    bool spread_recovered = false;          // the last read_fit_stats re-ran the last fit
     Workspace() = default;
     ~Workspace() {
         if (stats_host) (void)hipHostFree(stats_host);
+        if (ring_host) (void)hipHostFree(ring_host);
     }
     ScanState scan;
     BucketSort bucket;  // the bucketed sort's buffers (large fits only)
@@ -227,7 +243,10 @@ struct Workspace {
         band_ready = false;
         if (stats_host) (void)hipHostFree(stats_host);
         stats_host = nullptr;
-        stats_dev = nullptr;
+        if (ring_host) (void)hipHostFree(ring_host);
+        ring_host = ring_dev = fit_block = nullptr;
+        ring_next = ring_used = 0;
+        recalls.clear();
     }
 };
 
@@ -357,6 +376,10 @@ static_assert(sizeof(GridParams) <= (kMiscState - kMiscGrid) * sizeof(double),
               "GridParams overlaps the fit state");
 static_assert(kMiscState * sizeof(double) + kStTileBuckets * sizeof(int32_t) <=
                   kFitStatsDoubles * sizeof(double), "the stats copy must hold the states");
+// (an LDS fit writes the whole FitState into its stats block: the ring's stride must hold it)
+static_assert(kMiscState * sizeof(double) + kStCount * sizeof(int32_t) <=
+                  Workspace::kStatBlock * sizeof(double) &&
+              kFitStatsDoubles <= Workspace::kStatBlock, "LDS fits' stats blocks");
 void enqueue_fit_stats_copy(hipStream_t s, Workspace& ws, double* dst);
 FitStats parse_fit_stats(const Workspace& ws, const double* buf);
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out);
@@ -456,24 +479,27 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
                         int32_t* st, double* mirror = nullptr);
 // One fit of n <= kSmallMaxPoints points spread over several workgroups of one launch
 // (small.hip, spread_fit_kernel): the same results as the one-workgroup fit; statistics into
-// st / gp (the handle's fit state), st[kStError] = 2 if a grid barrier gave up.
+// st / gp (the handle's fit state) and the fit's own stats block `mirror` (whose kStError the
+// caller has cleared), kStError = 2 there if a grid barrier gave up.
 void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
                         const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
                         int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
-                        double* mirror = nullptr);
+                        double* mirror);
 // Partitions of kSmallMaxPoints < n <= kBandMaxPoints in ONE launch, each of G workgroups
-// staging a band of cell rows (small.hip band_fit_kernel); statistics into st / gp / mirror as
-// the spread fit, st[kStError] = 2 (barrier gave up) or 3 (a band over the staging capacity):
-// read_fit_stats then re-runs the fit through the tiled pipeline.
+// staging a band of cell rows (small.hip band_fit_kernel); statistics as the spread fit,
+// kStError = 2 (barrier gave up) or 3 (a band over the staging capacity): drain_recalls then
+// re-runs the fit through the tiled pipeline.
 constexpr int64_t kBandMaxPoints = 65536;
 bool band_fit_eligible(int64_t n, double eps, int32_t mode, int32_t min_points);
 void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double* x,
                       const double* y, int64_t n, double eps, int32_t min_points, int32_t mode,
                       int32_t* cluster, uint8_t* flag, GridParams* gp, int32_t* st,
-                      double* mirror = nullptr);
-// After the stream has drained: the last fit was a spread fit whose grid barrier gave up ->
-// re-run it through the one-workgroup kernel (synchronously), count it, return true.
-bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws);
+                      double* mirror);
+// After the stream has drained: every spread / band fit queued since the last check whose
+// barrier gave up or whose band overflowed is re-run, in stream order, into its own outputs
+// (its stats block and cluster-count word rewritten), synchronously; counted in
+// ws.spread_fallbacks.  Returns true when the LAST fit was re-run.
+bool drain_recalls(hipStream_t s, Profiler* prof, Workspace& ws);
 // DBSCAN.scala:116-137 on the host: the points every partition's outer rectangle (main grown
 // by eps, inclusive) holds, in input order (partition.hip)
 int64_t duplicate_points(const double* x, const double* y, int64_t n, const double* rects,

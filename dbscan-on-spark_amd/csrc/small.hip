@@ -829,6 +829,10 @@ __device__ __forceinline__ uint32_t sp_load(uint32_t* p) {
 // until `target` arrivals, and acquires (agent fence: this CU's stale lines dropped) before the
 // workgroup meets again and reads what the others published.  The poll gives up after ~2^21
 // rounds (seconds) and flags st[kStError] = 2: the fit then fails loudly instead of hanging.
+// A workgroup that gives up also raises the launch's abort word bar[2], which every poll reads
+// beside the count: once one barrier of a launch has failed, every later wait of every
+// workgroup ends at once (the result is discarded and re-run by the host) instead of spinning
+// to the bound again.  bar[2] is cleared by the last workgroup to leave.
 __device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st, double* mirror,
                              uint32_t spin_limit) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -839,8 +843,10 @@ __device__ void sp_grid_sync(uint32_t* bar, uint32_t target, int32_t* st, double
         __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (spin_limit 0: give up at once, the test of the fallback; the host re-runs the fit)
         for (uint32_t spins = 0; spin_limit == 0 || sp_load(bar) < target;) {
+            if (sp_load(bar + 2) != 0u) break;  // (another workgroup gave up: flagged already)
             __builtin_amdgcn_s_sleep(2);
             if (++spins > spin_limit) {
+                __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(st + kStError, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (mirror)
                     __hip_atomic_store(reinterpret_cast<int32_t*>(mirror + kMiscState) + kStError,
@@ -1142,6 +1148,7 @@ __global__ __launch_bounds__(kSmT, 1) void spread_fit_kernel(
             (uint32_t)G - 1) {
         __hip_atomic_store(sa.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sa.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sa.bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2164,11 +2171,27 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         *gp = gg;
         if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
     }
-    if (tid == 0 &&
-        __hip_atomic_fetch_add(ba.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            (uint32_t)G - 1) {
+    // The last workgroup to leave resets the barrier words.  After a barrier gave up (bar[2]
+    // raised) workgroups that were not resident added to the row counts after others had
+    // zeroed their shares: that workgroup zeroes them all (every other workgroup has left, and
+    // the acq_rel departure orders their writes before its own), so the next band fit on the
+    // handle starts from clean counters whatever this one's outcome.
+    if (tid == 0) {
+        const bool last = __hip_atomic_fetch_add(ba.bar + 1, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)G - 1;
+        L.meta[15] = last ? (sp_load(ba.bar + 2) != 0u ? 2 : 1) : 0;
+    }
+    __syncthreads();
+    const int leave = L.meta[15];
+    if (leave == 2 && !fullbox)
+        for (int r = tid; r < kBandCap; r += kBandT) {
+            __hip_atomic_store(ba.rowcnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ba.rowcur + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    if (leave && tid == 0) {
         __hip_atomic_store(ba.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(ba.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ba.bar + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2227,16 +2250,9 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     sa.core = reinterpret_cast<uint8_t*>(base + kSpreadHead);
     sa.pairs = reinterpret_cast<uint32_t*>(base + kSpreadHead + kSmN);
     const int G = (int)std::min<int64_t>(kSpreadMaxWG, std::max<int64_t>(1, n / kSpreadPer));
-    // kStError cleared ahead of the launch (the kernel never clears it): without waiting on
-    // the device, in the pinned mirror the host reads; in the device state only when there is
-    // no mirror (its host reads copy the device state then; a memset is one more GPU command
-    // per call: ~3 us)
-    if (mirror && ws.stats_host)
-        reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
-    else
-        DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
-    ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
-                                               gp, st, mirror};
+    // (kStError of the fit's own stats block `mirror` is cleared by the caller, enqueue_fit:
+    // the kernel never clears it, so a late workgroup 0 cannot erase another's barrier failure)
+    if (!mirror) throw ArgError{"spread fit without a stats block"};
     klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
             eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, sa,
             ws.spread_spin_limit);
@@ -2288,44 +2304,12 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     ba.par = reinterpret_cast<int32_t*>(q);
     q += (size_t)kBandMaxPoints * 4;
     ba.pairs = reinterpret_cast<uint32_t*>(q);
-    // kStError cleared ahead of the launch: in the pinned mirror, or the device state when
-    // there is no mirror (as enqueue_spread_fit)
-    if (mirror && ws.stats_host)
-        reinterpret_cast<int32_t*>(ws.stats_host + kMiscState)[kStError] = 0;
-    else
-        DBSCAN_HIP_CHECK(hipMemsetAsync(st + kStError, 0, sizeof(int32_t), s));
-    ws.spread_recall = Workspace::SpreadRecall{true, x, y, n, eps, min_points, mode, cluster, flag,
-                                               gp, st, mirror};
-    ws.recall_band = true;
+    // (kStError of the fit's own stats block: cleared by the caller, as for enqueue_spread_fit)
+    if (!mirror) throw ArgError{"band fit without a stats block"};
     klaunch(prof, "band_fit", band_fit_kernel, dim3(G), dim3(kBandT), 0, s, x, y, (int)n, eps,
             eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, ba,
             ws.spread_spin_limit);
     DBSCAN_HIP_CHECK(hipGetLastError());
-}
-
-bool recover_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws) {
-    Workspace::SpreadRecall& r = ws.spread_recall;
-    if (!ws.fit_mirrored || !r.valid || !ws.stats_host) return false;
-    int32_t* v = reinterpret_cast<int32_t*>(ws.stats_host + kMiscState);
-    if (ws.recall_band) {  // a band fit: barrier gave up (2) or a band overflowed (3)
-        if (v[kStError] != 2 && v[kStError] != 3) return false;
-        ws.band_ready = false;  // (a barrier that gave up may leave row counts: zeroed again)
-        FitArgs b{r.x, r.y, nullptr, r.n, r.eps, r.min_points, r.mode, r.cluster, r.flag,
-                  nullptr, nullptr};
-        b.small_max = 0;  // the tiled pipeline (no LDS fit, no band fit)
-        enqueue_fit(s, ws, prof, b, nullptr);
-        enqueue_fit_stats_copy(s, ws, ws.stats_host);
-        DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-        ++ws.spread_fallbacks;
-        return true;
-    }
-    if (v[kStError] != 2) return false;
-    // the one-workgroup kernel: no grid barrier, every label and statistic rewritten
-    enqueue_small_fits(s, prof, r.x, r.y, nullptr, nullptr, 1, r.n, r.eps, r.min_points, r.mode,
-                       r.cluster, r.flag, nullptr, r.gp, r.st, r.mirror);
-    DBSCAN_HIP_CHECK(hipStreamSynchronize(s));
-    ++ws.spread_fallbacks;
-    return true;
 }
 
 }  // namespace dbscan

@@ -228,3 +228,128 @@ def test_band_labels_written_into_pinned_block(dm):
         _eq(dm.fit_arrays(x2, y2, 0.12, 6, 0, handle=h), ref2, "default bound")
     finally:
         h.close()
+
+
+def test_async_queued_fits_all_recalled(dm):
+    """Three asynchronous fits of different data queued back to back on one handle (a band fit
+    over the one-box limit of 16384 points, a band fit below it in Archery mode, a spread fit),
+    every grid barrier giving up at once (spin limit 0), ONE dbscan_sync: each fit has its own
+    stats block and recall record, so all three are re-run and each equals the oracle, cluster
+    count included (dbscan_fit_device_async must never leave wrong labels, DBSCAN.scala:153-154).
+    Then the default bound: the same handle fits again with no re-run (the give-ups left no
+    dirty band counters behind)."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(606)
+    h = dm.Handle(0)
+    try:
+        assert h.set_spread_spin_limit(0) == 1 << 21
+        before = h.spread_fallbacks()
+        cases = [(20000, 0.2, 10, 0, None), (9000, 0.12, 6, 1, None), (5000, 0.2, 5, 0, "spread")]
+        outs = []
+        for m, eps, mp, mode, form in cases:
+            x, y = _set(rng, m)
+            if form == "spread":
+                h.set_band_min(1 << 30)
+                h.set_spread_min(0)
+            tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+            cl = torch.full((m,), -9, dtype=torch.int32, device="cuda")
+            fl = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+            nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            D.fit_tensors_async(tx, ty, eps, mp, mode, h, cl, fl, nk)
+            outs.append((x, y, eps, mp, mode, tx, ty, cl, fl, nk))
+        h.sync()
+        torch.cuda.synchronize()
+        assert h.spread_fallbacks() == before + 3
+        for x, y, eps, mp, mode, _, _, cl, fl, nk in outs:
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), int(nk.item())),
+                O.fit_grid(x, y, eps, mp, mode), f"queued m={x.size}")
+        h.set_spread_spin_limit(1 << 21)
+        h.set_band_min(400)
+        h.set_spread_min(512)
+        for m in (20000, 9000):  # (the seam's halo-grown shape: no staging overflow)
+            c = rng.uniform(0, 25 * 2.55, size=(6, 2))
+            pts = c[rng.integers(0, 6, m)] + rng.normal(0, 25 * 2.55 / 6, size=(m, 2))
+            x, y = pts[:, 0].copy(), pts[:, 1].copy()
+            _eq(dm.fit_arrays(x, y, 2.55, 10, 0, handle=h), O.fit_grid(x, y, 2.55, 10, 0),
+                f"after m={m}")
+        assert h.spread_fallbacks() == before + 3
+    finally:
+        h.close()
+
+
+def test_async_overflow_then_another_fit(dm):
+    """A queued band fit that overflows its staging (a 20000-point thin strip: kStError 3)
+    followed by two more queued fits, one dbscan_sync: the strip is re-run through the tiled
+    pipeline into its own outputs, the fits after it are untouched, all equal the oracle."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(707)
+    h = dm.Handle(0)
+    try:
+        before = h.spread_fallbacks()
+        sets = [(rng.uniform(0, 50, 20000), rng.uniform(0, 0.05, 20000), 0.2, 10, 0)]
+        for m in (9000, 3000):
+            x, y = _set(rng, m)
+            sets.append((x, y, 0.12, 6, m % 2))
+        outs = []
+        for x, y, eps, mp, mode in sets:
+            tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+            cl = torch.full((x.size,), -9, dtype=torch.int32, device="cuda")
+            fl = torch.full((x.size,), 9, dtype=torch.uint8, device="cuda")
+            nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            D.fit_tensors_async(tx, ty, eps, mp, mode, h, cl, fl, nk)
+            outs.append((tx, ty, cl, fl, nk))
+        h.sync()
+        torch.cuda.synchronize()
+        assert h.spread_fallbacks() == before + 1
+        for (x, y, eps, mp, mode), (_, _, cl, fl, nk) in zip(sets, outs):
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), int(nk.item())),
+                O.fit_grid(x, y, eps, mp, mode), f"queued m={x.size}")
+        st = h.stats()  # the last fit's
+        assert st["n"] == 3000
+    finally:
+        h.close()
+
+
+def test_async_fits_wrap_the_stats_ring(dm):
+    """150 asynchronous LDS fits (one-workgroup, spread and band forms) queued on one handle
+    without a sync: more than two turns of the 64-block stats ring, so the ring drains the
+    stream and checks the queued fits when it is full; one dbscan_sync; every fit's labels and
+    cluster count equal the oracle."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(150)
+    h = dm.Handle(0)
+    try:
+        h.set_spread_min(1000)
+        h.set_band_min(3000)
+        sets, outs = [], []
+        for i in range(150):
+            m = int(rng.choice([200, 700, 1500, 2500, 5000, 9000]))
+            x, y = _set(rng, m)
+            mode = i % 2
+            tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+            cl = torch.full((m,), -9, dtype=torch.int32, device="cuda")
+            fl = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+            nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+            sets.append((x, y, mode))
+            outs.append((tx, ty, cl, fl, nk))
+        torch.cuda.synchronize()
+        for (x, y, mode), (tx, ty, cl, fl, nk) in zip(sets, outs):
+            D.fit_tensors_async(tx, ty, 0.12, 6, mode, h, cl, fl, nk)
+        h.sync()
+        torch.cuda.synchronize()
+        for k, ((x, y, mode), (_, _, cl, fl, nk)) in enumerate(zip(sets, outs)):
+            _eq((cl.cpu().numpy(), fl.cpu().numpy(), int(nk.item())),
+                O.fit_grid(x, y, 0.12, 6, mode), f"fit {k} m={x.size}")
+    finally:
+        h.close()
