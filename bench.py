@@ -128,6 +128,9 @@ def parse(argv=None):
     ap.add_argument("--no-seam", action="store_true",
                     help="skip the seam leg (partition-sized fits and batches, N = 1)")
     ap.add_argument("--seam-only", action="store_true", help="only the seam leg (no timed fit)")
+    ap.add_argument("--plain-launch", action="store_true",
+                    help="seam leg: the spread / band forms by plain launches (barriers with a "
+                         "poll bound) instead of cooperative ones (dbscan_set_cooperative 0)")
     ap.add_argument("--launch-probe", action="store_true",
                     help="test hook: the ranks join the process group and report their devices")
     return ap.parse_args(argv)
@@ -643,8 +646,9 @@ def seam(args, h, threads):
     import dbscan_amd
     from dbscan_amd import device as D
 
-    out = {"per_call": {}}
+    out = {"per_call": {}, "cooperative": not args.plain_launch}
     eps, mp = args.eps, args.min_points
+    coop_prev = h.set_cooperative(not args.plain_launch)
     default_small = h.set_small_max(8192)  # (restored below: the handle's default cap)
     for m in (250, 2000, 8192, 65536):
         tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
@@ -693,18 +697,23 @@ def seam(args, h, threads):
     npart, total = len(sizes), int(offs[-1])
     cl = np.ones(total, np.int32)
     fl = np.ones(total, np.uint8)
-    # (a) one seam call per partition, one thread
+    # (a) one seam call per partition, one thread (recalls: partitions whose band fit
+    # overflowed its staging or whose grid barrier gave up, re-run through the tiled pipeline)
+    rec0 = h.spread_fallbacks()
     t0 = time.perf_counter()
     for p in range(npart):
         a, b = offs[p], offs[p + 1]
         dbscan_amd.fit_arrays(px[a:b], py[a:b], eps, mp, 0, handle=h, cluster_out=cl[a:b],
                               flag_out=fl[a:b])
     t_calls = time.perf_counter() - t0
+    recalls = h.spread_fallbacks() - rec0
     # (a') the same calls from 4 executor threads with a handle each (Spark local[4]: the box
     # gives a process 4 hardware queues), partitions dealt round-robin
     import threading
 
     hs = [dbscan_amd.Handle(h.device) for _ in range(4)]
+    for hh in hs:
+        hh.set_cooperative(not args.plain_launch)
 
     def worker(t):
         for p in range(t, npart, 4):
@@ -714,6 +723,7 @@ def seam(args, h, threads):
 
     for hh in hs:  # (each handle's workspace allocated before the clock starts)
         dbscan_amd.fit_arrays(px[:1000], py[:1000], eps, mp, 0, handle=hh)
+    rec4 = sum(hh.spread_fallbacks() for hh in hs)
     ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
     t0 = time.perf_counter()
     for th in ths:
@@ -721,6 +731,7 @@ def seam(args, h, threads):
     for th in ths:
         th.join()
     t_calls4 = time.perf_counter() - t0
+    recalls4 = sum(hh.spread_fallbacks() for hh in hs) - rec4
     for hh in hs:
         hh.close()
     # (b) one batch call, host arrays
@@ -754,10 +765,12 @@ def seam(args, h, threads):
                      f"{int((sizes > 8192).sum())} over the one-workgroup capacity)"),
         "partitions": npart, "points_with_halos": total,
         "per_partition_calls": {"seconds": round(t_calls, 4),
-                                "us_per_partition": round(t_calls / npart * 1e6, 2)},
+                                "us_per_partition": round(t_calls / npart * 1e6, 2),
+                                "recalled_partitions": int(recalls)},
         "per_partition_calls_4_threads": {"seconds": round(t_calls4, 4),
                                           "us_per_partition": round(t_calls4 / npart * 1e6, 2),
-                                          "points_per_s": round(total / t_calls4, 1)},
+                                          "points_per_s": round(total / t_calls4, 1),
+                                          "recalled_partitions": int(recalls4)},
         "batch_host": {"seconds": round(t_batch, 4),
                        "us_per_partition": round(t_batch / npart * 1e6, 3),
                        "points_per_s": round(total / t_batch, 1)},
@@ -778,6 +791,7 @@ def seam(args, h, threads):
             "what": ("LocalDBSCANNaive.fit O(m^2) restated in C (oracle/reference_pipeline.c) on "
                      "the same partitions, a thread pool of `threads`, stopped after an 8 s "
                      "budget (a sample of the partitions)")}
+    h.set_cooperative(coop_prev)
     return out
 
 

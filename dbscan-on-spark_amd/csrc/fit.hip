@@ -2653,10 +2653,36 @@ __device__ __forceinline__ bool edge_pair_full(const double2* __restrict__ xy, i
                    : pair_found_generic(xy, 0, me, o, gcore, eps2);
 }
 __device__ __forceinline__ void edge_unite(int32_t* __restrict__ parent,
-                                           const int32_t* __restrict__ perm, int ca, int cb) {
+                                           const int32_t* __restrict__ perm, int ca, int cb,
+                                           int nf) {
+#if DBSCAN_AB_CHECK
+    // (checking builds: every parent-chain index in [0, nf), checked and clamped)
+    const auto find = [&](int x) {
+        x = CHK(9, x, 0, nf);
+        for (int k = 0; k < (1 << 20); ++k) {
+            const int p = CHK(9, ld_par<0>(parent, x), 0, nf);
+            if (p == x) break;
+            x = p;
+        }
+        return x;
+    };
+    int ra = find(ca), rb = find(cb);
+    for (int k = 0; k < (1 << 20) && ra != rb; ++k) {
+        const bool swap = perm[ra] < perm[rb];
+        const int hi = swap ? rb : ra, lo = swap ? ra : rb;
+        int expected = hi;
+        if (__hip_atomic_compare_exchange_strong(parent + hi, &expected, lo, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+        ra = find(expected);
+        rb = find(lo);
+    }
+#else
+    (void)nf;
     const int ra = uf_find(parent, ca);
     const int rb = uf_find(parent, cb);
     if (ra != rb) uf_unite_roots(parent, perm, ra, rb);
+#endif
 }
 
 template <int MINW>
@@ -2738,7 +2764,8 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
             for (int j = 0; j < cnt; ++j) lp[incl - cnt + j] = q0 + j;
             wave_sync();
             for (int i = lane; i < ntot; i += 64) {
-                const int q = lp[CHK(2, i, 0, kEdgeNodes)];
+                const int q = CHK(8, lp[CHK(2, i, 0, kEdgeNodes)], 0,
+                                  ntiles_p[kStQuarters - kStTiles]);
                 const int4 qi = qinfo[q];
                 const int4 gq = qg[q];
                 const int qc = qcomp[q];  // tile component rep (a member of the set)
@@ -2823,6 +2850,15 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                         const int b = sb[c];
                         if (lfind(lp, a) == lfind(lp, b)) continue;
                         EDGE_CNT(sweep);
+#if DBSCAN_AB_CHECK
+                        {  // the two quarters' slot ranges inside [0, nf]
+                            const int4 ob = nqi[w][b];
+                            (void)CHK(10, me.x, 0, *nf_p + 1);
+                            (void)CHK(10, me.y, me.x, *nf_p + 1);
+                            (void)CHK(10, ob.x, 0, *nf_p + 1);
+                            (void)CHK(10, ob.y, ob.x, *nf_p + 1);
+                        }
+#endif
                         if (!within_eps(pr.x, pr.y, po[c].x, po[c].y, eps2) &&
                             !edge_pair_full(xy, me, nqi[w][b], core, eps2))
                             continue;
@@ -2832,7 +2868,7 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
                         if (lunite(lp, a, b) && DBSCAN_AB_EDGE_STOP != 3) {
                             EDGE_CNT(6);
                             edge_unite(parent, perm, CHK(6, ncomp[w][a], 0, *nf_p),
-                                       CHK(6, ncomp[w][b], 0, *nf_p));
+                                       CHK(6, ncomp[w][b], 0, *nf_p), *nf_p);
                         }
                     }
             }

@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/dbscan_hip.h"
+
 #include <string>
 #include <vector>
 
@@ -215,6 +217,7 @@ struct Workspace {
     std::vector<Recall> recalls;
     bool band_ready = false;                // band.p holds zeroed barrier words (small.hip)
     uint32_t spread_spin_limit = 1u << 21;  // barrier polls before giving up (0: at once; tests)
+    bool cooperative = DBSCAN_COOPERATIVE_DEFAULT != 0;  // spread / band: cooperative launches
     int64_t spread_fallbacks = 0;           // spread / band fits re-run (drain_recalls)
     bool spread_recovered = false;          // the last read_fit_stats re-ran the last fit
     Workspace() = default;
