@@ -589,6 +589,23 @@ int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double ep
     });
 }
 
+int32_t dbscan_train_node_shards(int32_t* device_out, int64_t* points_out, int64_t* shared_out,
+                                 int32_t max) {
+    return guarded(nullptr, [&]() -> int32_t {
+        if (max < 0) throw dbscan::ArgError{"max < 0"};
+        return dbscan::node_record(device_out, points_out, shared_out, max);
+    });
+}
+
+int32_t dbscan_selftest_node_plan(int32_t n_shards, int32_t ndev, int32_t fail_device,
+                                  int32_t* ran_on, int32_t* rc_of_device) {
+    return guarded(nullptr, [&]() -> int32_t {
+        if (n_shards < 1 || n_shards > 4096 || ndev < 1 || ndev > 64 || !ran_on || !rc_of_device)
+            throw dbscan::ArgError{"selftest: bad arguments"};
+        return dbscan::node_plan_selftest(n_shards, ndev, fail_device, ran_on, rc_of_device);
+    });
+}
+
 int32_t dbscan_selftest_worker_errors(int32_t* rcs, int32_t n) {
     return guarded(nullptr, [&]() -> int32_t {
         if (n < 0 || (n > 0 && !rcs)) throw dbscan::ArgError{"selftest: bad arguments"};

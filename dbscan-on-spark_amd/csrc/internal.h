@@ -438,6 +438,10 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                    int32_t mode, int32_t n_shards, int32_t* cluster_out, uint8_t* flag_out,
                    int64_t* n_clusters_out, std::string* err);
 int32_t worker_selftest(int32_t* rcs, int32_t n);
+// dbscan_train_node_shards / dbscan_selftest_node_plan (node.hip): see include/dbscan_hip.h.
+int32_t node_record(int32_t* device_out, int64_t* points_out, int64_t* shared_out, int32_t max);
+int32_t node_plan_selftest(int32_t n_shards, int32_t ndev, int32_t fail_device, int32_t* ran_on,
+                           int32_t* rc_of_device);
 // Node-path slab selection, label rows and scatter (node.hip): see include/dbscan_hip.h.
 int64_t select_slab(hipStream_t s, DevBuf& scratch, ScanState& scan, const double* x,
                     const double* y, int64_t n, const double* cuts, int32_t n_cuts, int32_t rank,

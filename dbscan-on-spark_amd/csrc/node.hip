@@ -615,7 +615,71 @@ bool run_workers(int nworkers, std::vector<WorkerStatus>& st, F&& f) {
     return true;
 }
 
+// dbscan_train_node's shard -> device plan: shard s runs on device s % ndev; one host worker per
+// device in use (nworkers = min(world, ndev)) runs its shards s = w, w + nworkers, ... in order.
+struct NodePlan {
+    int world = 0, nworkers = 0;
+    std::vector<std::vector<int>> shards_of;  // per worker (= device index)
+};
+NodePlan node_plan(int world, int ndev) {
+    NodePlan p;
+    p.world = std::max(0, world);
+    p.nworkers = std::max(0, std::min(p.world, ndev));
+    p.shards_of.resize((size_t)p.nworkers);
+    for (int s = 0; s < p.world && p.nworkers > 0; ++s) p.shards_of[(size_t)(s % p.nworkers)].push_back(s);
+    return p;
+}
+
+// The call's status from its workers': the first failed worker's (in device order), else OK.
+int32_t first_failure(const std::vector<WorkerStatus>& wst, std::string* err) {
+    for (const auto& d : wst)
+        if (d.rc != DBSCAN_OK) {
+            if (err) *err = d.err;
+            return d.rc;
+        }
+    return DBSCAN_OK;
+}
+
+// What the calling thread's last dbscan_train_node ran: per shard, the device its worker ran on
+// (read back from the worker's hipGetDevice), its points with halos and its shared points.
+struct NodeRecord {
+    std::vector<int32_t> device;
+    std::vector<int64_t> points, shared;
+};
+thread_local NodeRecord g_node_record;
+
 }  // namespace
+
+int32_t node_record(int32_t* device_out, int64_t* points_out, int64_t* shared_out, int32_t max) {
+    const NodeRecord& r = g_node_record;
+    const int32_t k = (int32_t)r.device.size();
+    for (int32_t s = 0; s < k && s < max; ++s) {
+        if (device_out) device_out[s] = r.device[(size_t)s];
+        if (points_out) points_out[s] = r.points[(size_t)s];
+        if (shared_out) shared_out[s] = r.shared[(size_t)s];
+    }
+    return k;
+}
+
+// The plan and the worker error path of dbscan_train_node on the host alone: ndev mocked
+// devices, the same node_plan and run_workers; worker w records the device it runs as for each
+// of its shards (ran_on[s]) and throws a HIP failure when w == fail_device; rc_of_device[w] is
+// each worker's status; returns the call's status as dbscan_train_node would.
+int32_t node_plan_selftest(int32_t n_shards, int32_t ndev, int32_t fail_device, int32_t* ran_on,
+                           int32_t* rc_of_device) {
+    const NodePlan plan = node_plan(n_shards, ndev);
+    std::vector<WorkerStatus> wst((size_t)plan.nworkers);
+    for (int s = 0; s < plan.world; ++s) ran_on[s] = -1;
+    run_workers(plan.nworkers, wst, [&](int w) {
+        for (int s : plan.shards_of[(size_t)w]) {
+            ran_on[s] = w;  // (train_node: the worker's hipSetDevice(w), read back per shard)
+            if (w == fail_device) throw HipFail{hipErrorInvalidValue, "selftest shard"};
+        }
+    });
+    for (int w = 0; w < plan.nworkers; ++w) rc_of_device[w] = wst[(size_t)w].rc;
+    std::string err;
+    return first_failure(wst, &err);
+}
 
 // The worker error mapping on the host alone (no device): worker w throws kind w (0 none,
 // 1 HipFail OOM, 2 HipFail other, 3 rc EARG, 4 HipError, 5 ArgError, 6 bad_alloc,
@@ -802,6 +866,9 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
     const std::vector<double> cuts = make_cuts(x, n, n_shards, eps);
     tr.mark("cuts");
     if (cuts.empty()) {  // one slab (or eps*eps not finite: all-pairs / no-pairs do not shard)
+        g_node_record.device.assign(1, 0);
+        g_node_record.points.assign(1, n);
+        g_node_record.shared.assign(1, 0);
         dbscan_handle* h = dbscan_create(0);
         if (!h) {
             *err = dbscan_last_error();
@@ -820,8 +887,13 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
     }
     const int world = (int)cuts.size() + 1;
     const std::vector<ZoneCut> zc = zone_cuts(world, cuts, reach(eps));
-    const int nworkers = std::min(world, ndev);
+    const NodePlan plan = node_plan(world, ndev);
+    const int nworkers = plan.nworkers;
     const bool shared_dev = world > nworkers;
+    NodeRecord& rec = g_node_record;
+    rec.device.assign((size_t)world, -1);
+    rec.points.assign((size_t)world, 0);
+    rec.shared.assign((size_t)world, 0);
     std::vector<DevShard> sh(world);
     std::vector<dbscan_handle*> hs(nworkers, nullptr);
     for (int w = 0; w < nworkers; ++w) {
@@ -877,8 +949,11 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                     int32_t* oh = cnt + 3 * nb;
                     int32_t* tot = cnt + 4 * nb;
                     dbscan::Workspace scratch;  // (the scans' look-back state)
-                    for (int r = w; r < world; r += nworkers) {
+                    for (int r : plan.shards_of[(size_t)w]) {
                         DevShard& s = sh[r];
+                        int dev = -1;
+                        hcheck(hipGetDevice(&dev), "hipGetDevice");
+                        rec.device[(size_t)r] = dev;
                         hipLaunchKernelGGL(plan_count_kernel, dim3((unsigned)nb), dim3(kBlock), 0,
                                            st, dx, n, r, world, zc[r], cs, ch);
                         hcheck(hipGetLastError(), "plan count");
@@ -890,6 +965,8 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                         hcheck(hipStreamSynchronize(st), "plan");
                         s.m = t2[0];
                         s.ns = t2[1];
+                        rec.points[(size_t)r] = s.m;
+                        rec.shared[(size_t)r] = s.ns;
                         const int64_t m = std::max<int64_t>(1, s.m);
                         hcheck(hipMalloc(&s.x, m * sizeof(double)), "shard");
                         hcheck(hipMalloc(&s.y, m * sizeof(double)), "shard");
@@ -959,7 +1036,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                                           hipMemcpyHostToDevice, st), "merge");
                     ccheck(dbscan_merge_union_device(d.ra, d.rb, nrec, d.parent, st));
                 }
-                for (int r = w; r < world; r += nworkers) {
+                for (int r : plan.shards_of[(size_t)w]) {
                     DevShard& s = sh[r];
                     if (s.m == 0) continue;
                     int64_t* own = nullptr;
@@ -1010,7 +1087,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
                     hcheck(hipMalloc(&d.out_cl, n * sizeof(int32_t)), "output");
                     hcheck(hipMalloc(&d.out_fl, n), "output");
                 }
-                for (int r = w; r < world; r += nworkers) {
+                for (int r : plan.shards_of[(size_t)w]) {
                     DevShard& s = sh[r];
                     if (s.m == 0) continue;
                     if (shared_dev) lean_fit(r, w);  // (the handle's last fit was another shard's)
@@ -1086,12 +1163,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         return true;
     }();
     if (!ok) {
-        for (auto& d : wst)
-            if (d.rc != DBSCAN_OK) {
-                rc = d.rc;
-                *err = d.err;
-                break;
-            }
+        rc = first_failure(wst, err);
         if (rc == DBSCAN_OK) rc = DBSCAN_EHIP;
     }
     for (int w = 0; w < nworkers; ++w) {
@@ -1100,7 +1172,7 @@ int32_t train_node(const double* x, const double* y, int64_t n, double eps, int3
         for (void* p : {(void*)d.parent, (void*)d.ra, (void*)d.rb, (void*)d.roots,
                         (void*)d.out_cl, (void*)d.out_fl})
             (void)hipFree(p);
-        for (int r = w; r < world; r += nworkers) sh[r].release();
+        for (int r : plan.shards_of[(size_t)w]) sh[r].release();
     }
     for (auto* h : hs) dbscan_destroy(h);
     if (rc == DBSCAN_OK) *n_clusters_out = nroots;

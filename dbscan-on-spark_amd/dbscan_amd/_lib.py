@@ -51,6 +51,8 @@ SIGNATURES = [
     ("dbscan_scala_range_count", _i64, [_d, _d, _d, _i32]),
     ("dbscan_train_node", _i32, [_vp, _vp, _i64, _d, _i32, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_selftest_worker_errors", _i32, [_vp, _i32]),
+    ("dbscan_train_node_shards", _i32, [_vp, _vp, _vp, _i32]),
+    ("dbscan_selftest_node_plan", _i32, [_i32, _i32, _i32, _vp, _vp]),
     ("dbscan_slab_fit_device", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),
     ("dbscan_slab_label_device", _i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     ("dbscan_slab_fit_device_async", _i32, [_vp, _vp, _vp, _vp, _i64, _d, _i32, _vp, _vp]),

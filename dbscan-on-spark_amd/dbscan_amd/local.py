@@ -185,6 +185,19 @@ def train_node(x, y, eps: float, min_points: int, mode: int = _lib.MODE_NAIVE,
     return cl, fl, int(k.value)
 
 
+def train_node_shards() -> List[dict]:
+    """What the calling thread's last train_node ran, per shard: the device its worker ran on
+    (shard s on device s % device_count), its points with eps halos, its shared points."""
+    L = _lib.load()
+    k = L.dbscan_train_node_shards(None, None, None, 0)
+    _lib.check(int(k) if k < 0 else _lib.DBSCAN_OK)
+    dev = (ctypes.c_int32 * max(1, k))()
+    pts = (ctypes.c_int64 * max(1, k))()
+    sh = (ctypes.c_int64 * max(1, k))()
+    L.dbscan_train_node_shards(dev, pts, sh, k)
+    return [{"device": int(dev[s]), "points": int(pts[s]), "shared": int(sh[s])} for s in range(k)]
+
+
 class _LocalDBSCAN:
     _mode = _lib.MODE_NAIVE
 

@@ -243,9 +243,12 @@ int64_t dbscan_spread_fallbacks(dbscan_handle* h);
  * hipLaunchCooperativeKernel, which refuses a grid that cannot be resident at once instead of
  * letting its grid barriers wait for workgroups that are not (the fallback re-run stays for a
  * band over its staging capacity and for a refused launch); 0 a plain launch, whose barriers
- * give up after their poll bound and re-run the fit.  Returns the previous setting (negative:
- * an error code). */
-#define DBSCAN_COOPERATIVE_DEFAULT 1
+ * give up after their poll bound and re-run the fit.  Measured (MI355X, ROCm 7.2, seam leg of
+ * bench.py): cooperative launches cost ~10 us more per call (2000 / 8192 points 80 / 116 ->
+ * 90 / 126 us) and are serialized across streams by the runtime, so four executor threads lose
+ * their overlap (72.8 -> 138.4 us per partition over the 1597 G(10^7) partitions): hence the
+ * plain default.  Returns the previous setting (negative: an error code). */
+#define DBSCAN_COOPERATIVE_DEFAULT 0
 int32_t dbscan_set_cooperative(dbscan_handle* h, int32_t on);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is
@@ -294,6 +297,20 @@ int32_t dbscan_train_node(const double* x, const double* y, int64_t n, double ep
  * an unknown type) and rcs[w] receives the status it maps to (DBSCAN_OK, EOOM, EHIP, EARG,
  * EHIP, EARG, EOOM, EHIP, EHIP) -- never a process abort. */
 int32_t dbscan_selftest_worker_errors(int32_t* rcs, int32_t n);
+/* What the calling thread's last dbscan_train_node ran, per shard s < the returned shard count
+ * (up to max entries written; any pointer may be NULL): device_out[s] the device its worker ran
+ * on (hipGetDevice inside the worker: s % device_count), points_out[s] its points with halos,
+ * shared_out[s] its points shared with a neighbouring slab.  Negative: an error code. */
+int32_t dbscan_train_node_shards(int32_t* device_out, int64_t* points_out, int64_t* shared_out,
+                                 int32_t max);
+/* Self-test of dbscan_train_node's shard plan and per-device status on the host alone (no
+ * device is touched): ndev mocked devices and n_shards shards through the same plan and worker
+ * pool; ran_on[s] = the device whose worker ran shard s; the worker of device fail_device (-1:
+ * none) fails with a HIP error on its first shard; rc_of_device[d] = each device worker's status
+ * (min(n_shards, ndev) entries).  Returns the call's status as dbscan_train_node would report it
+ * (the first failed device's, else DBSCAN_OK). */
+int32_t dbscan_selftest_node_plan(int32_t n_shards, int32_t ndev, int32_t fail_device,
+                                  int32_t* ran_on, int32_t* rc_of_device);
 
 /* ---------------------------------------------------------------------------------------
  * Slab fits for the multi-GPU node path (dbscan_amd/node.py).  The caller

@@ -144,3 +144,29 @@ def test_train_node_worker_errors_never_abort():
     want = [ok, eoom, ehip, earg, ehip, earg, eoom, ehip, ehip]
     assert list(rcs) == want * 2
     assert L.dbscan_selftest_worker_errors(None, 2) == earg
+
+
+@pytest.mark.parametrize("n_shards,ndev", [(8, 8), (8, 1), (8, 3), (3, 8), (16, 8), (1, 4)])
+def test_train_node_shard_plan_and_device_status(n_shards, ndev):
+    """dbscan_train_node's shard -> device plan with a mocked device count (host only, the same
+    plan and worker pool the call uses): shard s runs on device s % ndev, one worker per device
+    in use; a failing device's status is its own and becomes the call's (the first failed
+    device in device order), the other devices report OK (DBSCAN.scala:150-155 spreads the
+    partition fits over executors the same way)."""
+    L = _lib.load()
+    nw = min(n_shards, ndev)
+    ran = (ctypes.c_int32 * n_shards)()
+    rcd = (ctypes.c_int32 * nw)()
+    assert L.dbscan_selftest_node_plan(n_shards, ndev, -1, ran, rcd) == _lib.DBSCAN_OK
+    assert list(ran) == [s % ndev for s in range(n_shards)]
+    assert list(rcd) == [_lib.DBSCAN_OK] * nw
+    for fail in range(nw):
+        assert L.dbscan_selftest_node_plan(n_shards, ndev, fail, ran, rcd) == _lib.DBSCAN_EHIP
+        assert list(rcd) == [_lib.DBSCAN_EHIP if d == fail else _lib.DBSCAN_OK for d in range(nw)]
+        # the failing worker stopped at its first shard; every other shard ran on its device
+        for s in range(n_shards):
+            d = s % ndev
+            if d != fail:
+                assert ran[s] == d
+        assert ran[fail] == fail
+    assert L.dbscan_selftest_node_plan(0, ndev, -1, ran, rcd) == _lib.DBSCAN_EARG
