@@ -2620,6 +2620,13 @@ constexpr int kEdgeNodes = 72;
 #ifndef DBSCAN_AB_EDGE_W
 #define DBSCAN_AB_EDGE_W 5
 #endif
+// (launch bound 8 -- 64 VGPRs, 72 B of scratch -- is a broken build of this kernel: round 5's
+// four-at-a-time pair-test variant faulted with it once (illegal address), round 6's rebuild of
+// that variant faulted again, and the SHIPPED source at bound 8 with every global index checked
+// and clamped (DBSCAN_AB_CHECK, tools/bounds_probe.py) hung in its union loops, while the same
+// checked source at bound 5 ran configs 2, 3's share and 4 with 0 indices out of range: the
+// fault follows the 64-VGPR code generation, not the strip / quarter indexing.  DESIGN_LOG r6.)
+static_assert(DBSCAN_AB_EDGE_W <= 6, "edge_union_kernel misbehaves at launch bound 8");
 // big_count_kernel's launch bound, waves per SIMD: 7 (71 VGPRs, no scratch) measured 0.113 ->
 // 0.103 ms at config 2 against 5 (81 VGPRs); 6: 0.111; 8 spills
 #ifndef DBSCAN_AB_BIGC_W

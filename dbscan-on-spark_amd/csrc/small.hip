@@ -109,6 +109,7 @@ struct SmGrid {
     float lo, hi;                     // F <= lo: neighbour; F > hi: not; else exact fp64
     int nx, ny, ncells, nf, exact_only, bad;
     int clique;  // the side was not grown and <= |eps|*(1+2^-14): quarter cells are cliques
+    int swap;    // band grids: x and y exchanged (rows along the input's x axis)
 };
 
 // Workgroup exclusive scan of one int per thread; *total = the sum.  ws: kSmW + 1 ints.
@@ -1232,10 +1233,12 @@ struct BandArgs {
 
 // The band grid (one thread): sides as sm_make_grid, doubled along the axis over its share of
 // the limits until nx <= kBandCells / 3 and ny < kBandCap (row counts live in par) and the
-// whole grid holds <= 24 * kBandCells cells: with kBandMaxWG ranges of ~1/G of the cost below
-// (at most twice the points + cells) each range fits its tables with room for its halo rows
+// whole grid holds <= 24 * kBandCells * G / kBandMaxWG cells: with G ranges of ~1/G of the cost
+// below (at most twice the points + cells) each range fits its tables with room for its halo
+// rows (the bound scaled by G: sparse partitions of a few thousand points over hundreds of cells
+// per side, fitted by G = 16..20 workgroups, overflowed a fixed 24 * kBandCells)
 __device__ void band_make_grid(double xmin, double xmax, double ymin, double ymax, int nf,
-                               double eps, double eps2, SmGrid* g) {
+                               double eps, double eps2, int G, SmGrid* g) {
     g->nf = nf;
     g->bad = 0;
     g->exact_only = 0;
@@ -1250,7 +1253,8 @@ __device__ void band_make_grid(double xmin, double xmax, double ymin, double yma
         return floor((vmax * 0.5 - vmin * 0.5) * (2.0 / h)) + 1.0;
     };
     // (ny + 1 row counts live in par[kBandCap])
-    constexpr double kNx = kBandCells / 3, kNy = kBandCap - 1, kAll = 24.0 * kBandCells;
+    constexpr double kNx = kBandCells / 3, kNy = kBandCap - 1;
+    const double kAll = 24.0 * kBandCells * (double)G / (double)kBandMaxWG;
     bool ok = false;
     double cx = 1, cy = 1;
     for (int it = 0; it < 4096; ++it) {
@@ -1455,11 +1459,32 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         if (lane == 0) L.red[j][0] = v;
     }
     __syncthreads();
-    if (tid == 0)
+    if (tid == 0) {
         band_make_grid(L.red[0][0], L.red[1][0], L.red[2][0], L.red[3][0], (int)L.red[4][0], eps,
-                       eps2, &L.G);
+                       eps2, G, &L.G);
+        // rows along the axis that makes them shorter: a dense partition wider than tall (the
+        // strips EvenSplitPartitioner cuts out of a cluster's core) would stage rows of
+        // thousands of points and overflow (tools/band_overflow_sim.py: 6 of the 1597 G(10^7)
+        // partitions with rows along y alone, none this way).  Every geometric step below runs
+        // on (y, x); the exact predicate reads the input's own x, y by index, and
+        // fl(dx*dx) + fl(dy*dy) is the same sum either way round.
+        L.G.swap = 0;
+        if (!L.G.bad && L.G.nf > 0 && L.G.nx > L.G.ny) {
+            band_make_grid(L.red[2][0], L.red[3][0], L.red[0][0], L.red[1][0], (int)L.red[4][0],
+                           eps, eps2, G, &L.G);
+            L.G.swap = 1;
+        }
+    }
     __syncthreads();
     const int nf = L.G.nf, nx = L.G.nx, ny = L.G.ny;
+    const bool swp = L.G.swap != 0;
+    const double* X = swp ? y : x;  // (the geometry's coordinates)
+    const double* Y = swp ? x : y;
+    if (swp) {
+        const double t = px;
+        px = py;
+        py = t;
+    }
     // the cell of a finite point (quarter bits << 13 above the cell is the caller's)
     const auto cell_of = [&](double a, double b, int& row, int& col, int& quad) {
         int qx = (int)floor(2.0 * ((a * 0.5 - L.G.xmin2) * L.G.invx));
@@ -1480,7 +1505,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         __syncthreads();
         if (fullbox) {
             for (int i = tid; i < m; i += kBandT) {
-                const double a = x[i], b = y[i];
+                const double a = X[i], b = Y[i];
                 if (isfinite(a) && isfinite(b)) {
                     int row, col, quad;
                     cell_of(a, b, row, col, quad);
@@ -1639,7 +1664,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             const int i = i0 + tid;
             bool in = false;
             if (i < m) {
-                const double a = x[i], b = y[i];
+                const double a = X[i], b = Y[i];
                 if (isfinite(a) && isfinite(b)) {
                     int row, col, quad;
                     cell_of(a, b, row, col, quad);
@@ -1674,7 +1699,7 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
             srec[k] = make_float2(0.f, 0.f);
             if (j < S) {
                 const int i = fullbox ? (int)slist[j] : ba.ridx[row0 + j];
-                const double2 r = fullbox ? make_double2(x[i], y[i]) : ba.rxy[row0 + j];
+                const double2 r = fullbox ? make_double2(X[i], Y[i]) : ba.rxy[row0 + j];
                 if (i >= 0 && i < m && isfinite(r.x) && isfinite(r.y)) {
                     int row, col, quad;
                     cell_of(r.x, r.y, row, col, quad);
@@ -2166,8 +2191,10 @@ __global__ __launch_bounds__(kBandT, 1) void band_fit_kernel(
         sm_set_stat(st, mirror, kStCells, nf > 0 ? __hip_atomic_load(&ba.cnt[1], __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT)
                                                  : 0);
-        GridParams gg{L.G.xmin2, L.G.ymin2, L.G.invx, L.G.invy, (uint32_t)nx, (uint32_t)ny,
-                      1u, 1u, L.G.clique};
+        // (reported in the input's axes)
+        GridParams gg{swp ? L.G.ymin2 : L.G.xmin2, swp ? L.G.xmin2 : L.G.ymin2,
+                      swp ? L.G.invy : L.G.invx, swp ? L.G.invx : L.G.invy,
+                      (uint32_t)(swp ? ny : nx), (uint32_t)(swp ? nx : ny), 1u, 1u, L.G.clique};
         *gp = gg;
         if (mirror) *reinterpret_cast<GridParams*>(mirror + kMiscGrid) = gg;
     }

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from band_model import band_recall
 
 pytestmark = pytest.mark.gpu
 
@@ -54,6 +55,7 @@ def test_band_sizes_vs_oracle(dm, mode):
     h = dm.Handle(0)
     try:
         before = h.spread_fallbacks()
+        expect = before
         for m in (8193, 9000, 12345, 16384, 20000, 33333, 50000, 65535, 65536):
             x, y = _set(rng, m)
             eps, mp = (0.12, 6) if m % 2 else (0.2, 10)
@@ -62,9 +64,12 @@ def test_band_sizes_vs_oracle(dm, mode):
             tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
             cl, fl, k = D.fit_tensors(tx, ty, eps, mp, mode, h)
             _eq((cl.cpu().numpy(), fl.cpu().numpy(), k), ref, f"device m={m}")
-        # (the densest sets stage rows of > kBandCap / 3 points: those fits take the tiled
-        # recall; parity above covers both forms)
-        assert h.spread_fallbacks() - before <= 8
+            # the sets the band model says overflow a workgroup's staging (a row band of more
+            # than kBandCap points) take the tiled recall, both calls; no other fit does
+            expect += 2 * int(band_recall(x, y, eps))
+            assert h.spread_fallbacks() == expect, f"m={m}"
+        # (mode 1's 50000 / 65535-point sets: 4 recalls; mode 0: none)
+        assert expect - before == (0, 4)[mode]
     finally:
         h.close()
 
@@ -139,19 +144,32 @@ def test_band_grown_grid_per_core_walks(dm, mode):
         h.close()
 
 
+def _dense_square(rng, m):
+    """m points in a 0.5 x 0.5 square: at eps 0.2 every 3-row band holds all of them, whichever
+    axis the rows take (over a band's staging capacity)"""
+    return rng.uniform(0, 0.5, m), rng.uniform(0, 0.5, m)
+
+
 def test_band_overflow_and_barrier_fallbacks(dm):
-    """A row denser than a band's staging capacity (20000 points in one thin strip) and a
-    forced barrier give-up (poll bound 0) both re-run through the tiled pipeline in the same
-    call, counted, equal to the oracle."""
+    """Rows denser than a band's staging capacity (20000 points in a square of ~3 x 3 cells)
+    and a forced barrier give-up (poll bound 0) both re-run through the tiled pipeline in the
+    same call, counted, equal to the oracle.  A thin dense strip (rows along its length would
+    hold all of it) takes its rows across instead and needs no recall."""
     rng = np.random.default_rng(5)
     h = dm.Handle(0)
     try:
         m = 20000
         x = rng.uniform(0, 50, m)
         y = rng.uniform(0, 0.05, m)
-        ref = O.fit_grid(x, y, 0.2, 10, 0)
         before = h.spread_fallbacks()
-        _eq(dm.fit_arrays(x, y, 0.2, 10, 0, handle=h), ref, "dense strip")
+        _eq(dm.fit_arrays(x, y, 0.2, 10, 0, handle=h), O.fit_grid(x, y, 0.2, 10, 0),
+            "dense strip")
+        _eq(dm.fit_arrays(y, x, 0.2, 10, 0, handle=h), O.fit_grid(y, x, 0.2, 10, 0),
+            "dense strip, transposed")
+        assert h.spread_fallbacks() == before
+        x, y = _dense_square(rng, m)
+        ref = O.fit_grid(x, y, 0.2, 10, 0)
+        _eq(dm.fit_arrays(x, y, 0.2, 10, 0, handle=h), ref, "dense square")
         assert h.spread_fallbacks() == before + 1
         x2, y2 = _set(rng, 30000)
         ref2 = O.fit_grid(x2, y2, 0.12, 6, 1)
@@ -218,10 +236,8 @@ def test_band_labels_written_into_pinned_block(dm):
             _eq(dm.fit_arrays(x, y, 0.12, 6, 0, handle=h), O.fit_grid(x, y, 0.12, 6, 0),
                 f"m={m}")
         before = h.spread_fallbacks()
-        m = 12000  # one thin strip: its row is over a band's staging capacity
-        x = rng.uniform(0, 50, m)
-        y = rng.uniform(0, 0.05, m)
-        _eq(dm.fit_arrays(x, y, 0.2, 10, 1, handle=h), O.fit_grid(x, y, 0.2, 10, 1), "strip")
+        x, y = _dense_square(rng, 12000)  # every row band over a band's staging capacity
+        _eq(dm.fit_arrays(x, y, 0.2, 10, 1, handle=h), O.fit_grid(x, y, 0.2, 10, 1), "square")
         assert h.spread_fallbacks() == before + 1
         x2, y2 = _set(rng, 9000)
         ref2 = O.fit_grid(x2, y2, 0.12, 6, 0)
@@ -286,9 +302,10 @@ def test_async_queued_fits_all_recalled(dm):
 
 
 def test_async_overflow_then_another_fit(dm):
-    """A queued band fit that overflows its staging (a 20000-point thin strip: kStError 3)
-    followed by two more queued fits, one dbscan_sync: the strip is re-run through the tiled
-    pipeline into its own outputs, the fits after it are untouched, all equal the oracle."""
+    """A queued band fit that overflows its staging (20000 points in a square of ~3 x 3 cells:
+    kStError 3) followed by two more queued fits, one dbscan_sync: the square is re-run through
+    the tiled pipeline into its own outputs, the fits after it are untouched, all equal the
+    oracle."""
     import torch
 
     from dbscan_amd import device as D
@@ -297,7 +314,7 @@ def test_async_overflow_then_another_fit(dm):
     h = dm.Handle(0)
     try:
         before = h.spread_fallbacks()
-        sets = [(rng.uniform(0, 50, 20000), rng.uniform(0, 0.05, 20000), 0.2, 10, 0)]
+        sets = [_dense_square(rng, 20000) + (0.2, 10, 0)]
         for m in (9000, 3000):
             x, y = _set(rng, m)
             sets.append((x, y, 0.12, 6, m % 2))
