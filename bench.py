@@ -128,9 +128,6 @@ def parse(argv=None):
     ap.add_argument("--no-seam", action="store_true",
                     help="skip the seam leg (partition-sized fits and batches, N = 1)")
     ap.add_argument("--seam-only", action="store_true", help="only the seam leg (no timed fit)")
-    ap.add_argument("--plain-launch", action="store_true",
-                    help="seam leg: the spread / band forms by plain launches (barriers with a "
-                         "poll bound) instead of cooperative ones (dbscan_set_cooperative 0)")
     ap.add_argument("--launch-probe", action="store_true",
                     help="test hook: the ranks join the process group and report their devices")
     return ap.parse_args(argv)
@@ -646,9 +643,8 @@ def seam(args, h, threads):
     import dbscan_amd
     from dbscan_amd import device as D
 
-    out = {"per_call": {}, "cooperative": not args.plain_launch}
+    out = {"per_call": {}}
     eps, mp = args.eps, args.min_points
-    coop_prev = h.set_cooperative(not args.plain_launch)
     default_small = h.set_small_max(8192)  # (restored below: the handle's default cap)
     for m in (250, 2000, 8192, 65536):
         tx, ty = D.generate_blobs(m, 0.0, 1.0, 5, h)
@@ -712,8 +708,6 @@ def seam(args, h, threads):
     import threading
 
     hs = [dbscan_amd.Handle(h.device) for _ in range(4)]
-    for hh in hs:
-        hh.set_cooperative(not args.plain_launch)
 
     def worker(t):
         for p in range(t, npart, 4):
@@ -791,7 +785,6 @@ def seam(args, h, threads):
             "what": ("LocalDBSCANNaive.fit O(m^2) restated in C (oracle/reference_pipeline.c) on "
                      "the same partitions, a thread pool of `threads`, stopped after an 8 s "
                      "budget (a sample of the partitions)")}
-    h.set_cooperative(coop_prev)
     return out
 
 

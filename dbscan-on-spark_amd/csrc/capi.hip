@@ -1153,17 +1153,6 @@ int64_t dbscan_set_spread_spin_limit(dbscan_handle* h, int64_t polls) {
     return prev;
 }
 
-int32_t dbscan_set_cooperative(dbscan_handle* h, int32_t on) {
-    if (!h || on < 0 || on > 1) {
-        set_err(h ? "on must be 0 or 1" : "NULL handle");
-        return DBSCAN_EARG;
-    }
-    std::lock_guard<std::mutex> lk(h->mu);
-    const int32_t prev = h->ws.cooperative ? 1 : 0;
-    h->ws.cooperative = on != 0;
-    return prev;
-}
-
 int64_t dbscan_spread_fallbacks(dbscan_handle* h) {
     if (!h) {
         set_err("NULL handle");

@@ -217,7 +217,6 @@ struct Workspace {
     std::vector<Recall> recalls;
     bool band_ready = false;                // band.p holds zeroed barrier words (small.hip)
     uint32_t spread_spin_limit = 1u << 21;  // barrier polls before giving up (0: at once; tests)
-    bool cooperative = DBSCAN_COOPERATIVE_DEFAULT != 0;  // spread / band: cooperative launches
     int64_t spread_fallbacks = 0;           // spread / band fits re-run (drain_recalls)
     bool spread_recovered = false;          // the last read_fit_stats re-ran the last fit
     Workspace() = default;

@@ -2255,21 +2255,6 @@ void enqueue_small_fits(hipStream_t s, Profiler* prof, const double* x, const do
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 
-// A spread / band kernel through hipLaunchCooperativeKernel: the runtime launches the grid
-// only if all its workgroups can be resident at once, so the grid barriers never wait on a
-// workgroup that has not started.  A refused launch (hipErrorCooperativeLaunchTooLarge) leaves
-// the fit unrun: its stats block (ws.fit_block, this fit's alone) is flagged from the host like
-// a barrier that gave up, so drain_recalls re-runs it through a form without grid barriers.
-static void coop_launch(Workspace& ws, const void* kernel, dim3 grid, dim3 block, void** args,
-                        hipStream_t s) {
-    const hipError_t e = hipLaunchCooperativeKernel(kernel, grid, block, args, 0, s);
-    if (e == hipSuccess) return;
-    (void)hipGetLastError();
-    if (e != hipErrorCooperativeLaunchTooLarge || !ws.fit_block)
-        throw HipError(e, "hipLaunchCooperativeKernel", __FILE__, __LINE__);
-    reinterpret_cast<int32_t*>(ws.fit_block + kMiscState)[kStError] = 2;
-}
-
 // Workgroups of a spread fit: one per kSpreadPer points (at most kSpreadMaxWG; 128 and 512
 // measured within a few microseconds of 256 per call, round 4)
 constexpr int kSpreadPer = 256;
@@ -2295,19 +2280,6 @@ void enqueue_spread_fit(hipStream_t s, Profiler* prof, Workspace& ws, const doub
     // (kStError of the fit's own stats block `mirror` is cleared by the caller, enqueue_fit:
     // the kernel never clears it, so a late workgroup 0 cannot erase another's barrier failure)
     if (!mirror) throw ArgError{"spread fit without a stats block"};
-    if (ws.cooperative) {
-        const double* a0 = x;
-        const double* a1 = y;
-        int a2 = (int)n;
-        double a3 = eps, a4 = eps * eps;
-        int a5 = (int)min_points, a6 = (int)mode;
-        uint32_t a14 = ws.spread_spin_limit;
-        void* kp[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &cluster, &flag, &gp, &st, &mirror,
-                      &sa, &a14};
-        coop_launch(ws, reinterpret_cast<const void*>(spread_fit_kernel), dim3(G), dim3(kSmT), kp,
-                    s);
-        return;
-    }
     klaunch(prof, "spread_fit", spread_fit_kernel, dim3(G), dim3(kSmT), 0, s, x, y, (int)n, eps,
             eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, sa,
             ws.spread_spin_limit);
@@ -2361,19 +2333,6 @@ void enqueue_band_fit(hipStream_t s, Profiler* prof, Workspace& ws, const double
     ba.pairs = reinterpret_cast<uint32_t*>(q);
     // (kStError of the fit's own stats block: cleared by the caller, as for enqueue_spread_fit)
     if (!mirror) throw ArgError{"band fit without a stats block"};
-    if (ws.cooperative) {
-        const double* a0 = x;
-        const double* a1 = y;
-        int a2 = (int)n;
-        double a3 = eps, a4 = eps * eps;
-        int a5 = (int)min_points, a6 = (int)mode;
-        uint32_t a14 = ws.spread_spin_limit;
-        void* kp[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &cluster, &flag, &gp, &st, &mirror,
-                      &ba, &a14};
-        coop_launch(ws, reinterpret_cast<const void*>(band_fit_kernel), dim3(G), dim3(kBandT), kp,
-                    s);
-        return;
-    }
     klaunch(prof, "band_fit", band_fit_kernel, dim3(G), dim3(kBandT), 0, s, x, y, (int)n, eps,
             eps * eps, (int)min_points, (int)mode, cluster, flag, gp, st, mirror, ba,
             ws.spread_spin_limit);

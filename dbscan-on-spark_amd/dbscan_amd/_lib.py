@@ -72,7 +72,6 @@ SIGNATURES = [
     ("dbscan_set_band_min", _i64, [_vp, _i64]),
     ("dbscan_set_spread_spin_limit", _i64, [_vp, _i64]),
     ("dbscan_spread_fallbacks", _i64, [_vp]),
-    ("dbscan_set_cooperative", _i32, [_vp, _i32]),
     ("dbscan_fit_batch", _i32, [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
     ("dbscan_fit_batch_device_async", _i32,
      [_vp, _vp, _vp, _vp, _i32, _d, _i32, _i32, _vp, _vp, _vp]),
@@ -210,14 +209,6 @@ class Handle:
         if r < 0:
             check(int(r))
         return int(r)
-
-    def set_cooperative(self, on: bool) -> bool:
-        """Spread / band forms through hipLaunchCooperativeKernel (True) or a plain launch whose
-        grid barriers give up after their poll bound.  Returns the previous setting."""
-        r = load().dbscan_set_cooperative(self._h, 1 if on else 0)
-        if r < 0:
-            check(int(r))
-        return bool(r)
 
     def spread_fallbacks(self) -> int:
         """Spread fits of this handle re-run by the one-workgroup kernel so far."""

@@ -239,17 +239,6 @@ int64_t dbscan_set_spread_spin_limit(dbscan_handle* h, int64_t polls);
 /* Spread and band fits of this handle re-run by the fallback (the one-workgroup kernel, the
  * tiled pipeline) so far (negative: an error). */
 int64_t dbscan_spread_fallbacks(dbscan_handle* h);
-/* The spread and band forms' launch (default DBSCAN_COOPERATIVE_DEFAULT): 1 launches them with
- * hipLaunchCooperativeKernel, which refuses a grid that cannot be resident at once instead of
- * letting its grid barriers wait for workgroups that are not (the fallback re-run stays for a
- * band over its staging capacity and for a refused launch); 0 a plain launch, whose barriers
- * give up after their poll bound and re-run the fit.  Measured (MI355X, ROCm 7.2, seam leg of
- * bench.py): cooperative launches cost ~10 us more per call (2000 / 8192 points 80 / 116 ->
- * 90 / 126 us) and are serialized across streams by the runtime, so four executor threads lose
- * their overlap (72.8 -> 138.4 us per partition over the 1597 G(10^7) partitions): hence the
- * plain default.  Returns the previous setting (negative: an error code). */
-#define DBSCAN_COOPERATIVE_DEFAULT 0
-int32_t dbscan_set_cooperative(dbscan_handle* h, int32_t on);
 
 /* A batch of independent local fits -- an executor's partitions -- in one call: partition p is
  * points [offsets[p], offsets[p+1]) of x, y (host array offsets, n_parts + 1 non-decreasing

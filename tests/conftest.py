@@ -19,6 +19,15 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "dbscan-on-spar
 EPS_03F = float(np.float32(0.3))  # Scala `eps = 0.3F` widened to Double (SURVEY key fact 4b)
 
 
+if os.environ.get("DBSCAN_SEGV_TRACE") == "1":  # debug runs: native backtraces after finalize
+    import atexit
+    import ctypes
+
+    _segv = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools",
+                                     "segv_trace.so"))
+    atexit.register(_segv.segv_trace_install)  # (re-installed last: after torch's handlers)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
 

@@ -183,11 +183,9 @@ def test_band_overflow_and_barrier_fallbacks(dm):
         h.close()
 
 
-@pytest.mark.parametrize("coop", [False, True], ids=["plain", "cooperative"])
-def test_band_from_concurrent_handles(dm, coop):
+def test_band_from_concurrent_handles(dm):
     """Four executor threads, a handle each, band fits at once (4 x up to 64 workgroups of
-    one CU each), by plain and by cooperative launches (dbscan_set_cooperative): every fit
-    equals its oracle fit."""
+    one CU each): every fit equals its oracle fit."""
     import threading
 
     rng = np.random.default_rng(606)
@@ -197,8 +195,6 @@ def test_band_from_concurrent_handles(dm, coop):
         sets.append((x, y))
     refs = [O.fit_grid(x, y, 0.12, 6, 0) for x, y in sets]
     handles = [dm.Handle(0) for _ in range(4)]
-    for hh in handles:
-        hh.set_cooperative(coop)
     errors = []
 
     def worker(t):

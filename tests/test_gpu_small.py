@@ -254,13 +254,12 @@ def test_blob_partitions_batch(dm, handle):
     assert len(offs) - 1 > 100
 
 
-@pytest.mark.parametrize("coop", [False, True], ids=["plain", "cooperative"])
 @pytest.mark.parametrize("band_min", [BAND_MIN, NO_BAND])
-def test_spread_fits_from_concurrent_handles(dm, band_min, coop):
+def test_spread_fits_from_concurrent_handles(dm, band_min):
     """Four executor threads, a handle each, fitting partitions concurrently through the spread
     and band forms (each launch holds its workgroups at grid barriers while the other handles'
-    launches share the GPU; NO_BAND: the spread form alone), by plain and by cooperative
-    launches (dbscan_set_cooperative): every fit equals its oracle fit, no barrier times out."""
+    launches share the GPU; NO_BAND: the spread form alone): every fit equals its oracle fit,
+    no barrier times out."""
     import threading
 
     rng = np.random.default_rng(404)
@@ -272,7 +271,6 @@ def test_spread_fits_from_concurrent_handles(dm, band_min, coop):
     handles = [dm.Handle(0) for _ in range(4)]
     for hh in handles:
         hh.set_band_min(band_min)
-        hh.set_cooperative(coop)
     errors = []
 
     def worker(t):
