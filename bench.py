@@ -703,6 +703,21 @@ def seam(args, h, threads):
                               flag_out=fl[a:b])
     t_calls = time.perf_counter() - t0
     recalls = h.spread_fallbacks() - rec0
+    # (a'') the same calls as a JNI caller makes them: dbscan_fit_h straight through the C-ABI
+    # (ctypes with precomputed addresses: no numpy views or argument checks per call)
+    lib = dbscan_amd.load()
+    fit_h = lib.dbscan_fit_h
+    vp = ctypes.c_void_p
+    ax, ay, acl, afl = (int(a.ctypes.data) for a in (px, py, cl, fl))
+    kk = ctypes.c_int32(0)
+    pk = ctypes.byref(kk)
+    hp = h.ptr
+    calls = [(vp(ax + 8 * int(offs[p])), vp(ay + 8 * int(offs[p])), int(offs[p + 1] - offs[p]),
+              vp(acl + 4 * int(offs[p])), vp(afl + int(offs[p]))) for p in range(npart)]
+    t0 = time.perf_counter()
+    for cx_, cy_, m_, ccl, cfl in calls:
+        fit_h(hp, cx_, cy_, m_, float(eps), int(mp), 0, ccl, cfl, pk)
+    t_capi = time.perf_counter() - t0
     # (a') the same calls from 4 executor threads with a handle each (Spark local[4]: the box
     # gives a process 4 hardware queues), partitions dealt round-robin
     import threading
@@ -761,6 +776,10 @@ def seam(args, h, threads):
         "per_partition_calls": {"seconds": round(t_calls, 4),
                                 "us_per_partition": round(t_calls / npart * 1e6, 2),
                                 "recalled_partitions": int(recalls)},
+        "per_partition_capi_calls": {"seconds": round(t_capi, 4),
+                                     "us_per_partition": round(t_capi / npart * 1e6, 2),
+                                     "what": "dbscan_fit_h per partition through ctypes with "
+                                             "precomputed addresses, one thread"},
         "per_partition_calls_4_threads": {"seconds": round(t_calls4, 4),
                                           "us_per_partition": round(t_calls4 / npart * 1e6, 2),
                                           "points_per_s": round(total / t_calls4, 1),
