@@ -97,8 +97,13 @@ int32_t dbscan_fit_device(dbscan_handle* h, const double* d_x, const double* d_y
  * device).  The cluster count is written to DEVICE memory at d_n_clusters (may be NULL).
  * dbscan_sync waits for the stream, then makes the fit's statistics available and reports
  * device-side errors (an eps grid that cannot be sized) as DBSCAN_EARG.  Any synchronous entry
- * point on the same handle settles a pending asynchronous fit first.  bench.py times this form:
- * K fits back to back, one synchronization. */
+ * point on the same handle settles a pending asynchronous fit first.  Several fits may be queued
+ * back to back (inputs and outputs kept alive until dbscan_sync): each partition-sized fit
+ * (the LDS forms) records its outcome in a stats block of its own, and dbscan_sync re-runs, in
+ * order and into their own outputs and cluster-count words, every queued spread or band fit
+ * whose grid barrier gave up or whose band overflowed -- not only the last one -- so no queued
+ * fit ever keeps wrong labels; the statistics reported are the last fit's.  bench.py times this
+ * form: K fits back to back, one synchronization. */
 int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const double* d_y,
                                 int64_t n, double eps, int32_t min_points, int32_t mode,
                                 int32_t* d_cluster, uint8_t* d_flag, int32_t* d_n_clusters);

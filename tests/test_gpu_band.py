@@ -370,3 +370,30 @@ def test_async_fits_wrap_the_stats_ring(dm):
                 O.fit_grid(x, y, 0.12, 6, mode), f"fit {k} m={x.size}")
     finally:
         h.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_band_wide_and_tall_partitions(dm, mode):
+    """Partitions much wider than tall (the band grid then takes its rows across, on (y, x))
+    and much taller than wide (rows along y), sparse and dense, with non-finite points: each
+    equals the oracle, and fitting (y, x) gives the same labels as (x, y) (the predicate
+    dx*dx + dy*dy is symmetric, so every form must be too)."""
+    rng = np.random.default_rng(4242 + mode)
+    h = dm.Handle(0)
+    try:
+        before = h.spread_fallbacks()
+        for m, w, hgt, eps, mp in ((3000, 40.0, 2.0, 0.2, 5), (12000, 60.0, 1.0, 0.12, 6),
+                                   (20000, 200.0, 6.0, 0.3, 10), (50000, 300.0, 3.0, 0.15, 8)):
+            k = int(rng.integers(3, 12))
+            c = np.column_stack([rng.uniform(0, w, k), rng.uniform(0, hgt, k)])
+            pts = c[rng.integers(0, k, m)] + rng.normal(0, eps * 3, size=(m, 2))
+            x, y = pts[:, 0].copy(), pts[:, 1].copy()
+            x[::997] = np.nan
+            ref = O.fit_grid(x, y, eps, mp, mode)
+            _eq(dm.fit_arrays(x, y, eps, mp, mode, handle=h), ref, f"wide m={m}")
+            _eq(dm.fit_arrays(y, x, eps, mp, mode, handle=h), ref, f"tall m={m}")
+            expect = int(band_recall(x, y, eps)) + int(band_recall(y, x, eps))
+            assert h.spread_fallbacks() - before == expect, f"m={m}"
+            before += expect
+    finally:
+        h.close()
