@@ -99,6 +99,15 @@ __device__ long long g_ab_stamps[kTileGrid * kStamps];
 #ifndef DBSCAN_AB_PAIR4
 #define DBSCAN_AB_PAIR4 0
 #endif
+// DBSCAN_AB_COUNTDIV (counting builds only): count32's scan divergence -- per wave iteration
+// of the count loop, the longest lane's candidate batches against all lanes' (g_div, read by
+// dbscan_ab_countdiv(), tools/countdiv_probe.py)
+#ifndef DBSCAN_AB_COUNTDIV
+#define DBSCAN_AB_COUNTDIV 0
+#endif
+#if DBSCAN_AB_COUNTDIV
+__device__ unsigned long long g_div[8];
+#endif
 #if DBSCAN_AB_CHECK
 constexpr int kChkSites = 12;
 __device__ unsigned long long g_chk_bad[kChkSites];
@@ -1758,8 +1767,9 @@ template <bool REC, int STRIDE = kBlock, class ExactF>
 __device__ __forceinline__ bool scan_count32(const float2* __restrict__ buf, int b, int e,
                                              float2 me, F32Cut cut, int min_points, int& cnt,
                                              uint32_t* lst, int& nrec, int nbr_k, int tag,
-                                             ExactF exact) {
+                                             ExactF exact, int* nbatch = nullptr) {
     for (int j = b; j < e; j += kScanBatch) {
+        if (nbatch) ++*nbatch;
         const int nin = e - j;
         float2 qq[kScanBatch];
 #pragma unroll
@@ -2002,22 +2012,46 @@ __global__ __launch_bounds__(kBlock, MINW) void count_tile32_kernel(
                     };
                     int cnt = 0, nrec = 0;
                     const int k_rec = nbr_k;
+#if DBSCAN_AB_COUNTDIV
+                    int nbt = 0;
+                    int* const nbp = &nbt;
+#else
+                    int* const nbp = nullptr;
+#endif
                     bool done = scan_count32<true>(buf, rg.cs, rg.ce, me, cut, min_points, cnt,
-                                                   lst, nrec, k_rec, 0, exact);
+                                                   lst, nrec, k_rec, 0, exact, nbp);
 #pragma unroll
                     for (int k = 0; k < 3 && !done; ++k) {
                         const int lo = rg.b[k], hi = rg.e[k];
                         if (lo <= rg.cs && rg.ce <= hi) {
                             done = scan_count32<true>(buf, lo, rg.cs, me, cut, min_points, cnt,
-                                                      lst, nrec, k_rec, k, exact) ||
+                                                      lst, nrec, k_rec, k, exact, nbp) ||
                                    scan_count32<true>(buf, rg.ce, hi, me, cut, min_points, cnt,
-                                                      lst, nrec, k_rec, k, exact);
+                                                      lst, nrec, k_rec, k, exact, nbp);
                         } else {
                             done = scan_count32<true>(buf, lo, hi, me, cut, min_points, cnt, lst,
-                                                      nrec, k_rec, k, exact);
+                                                      nrec, k_rec, k, exact, nbp);
                         }
                     }
                     is_core = cnt >= min_points;
+#if DBSCAN_AB_COUNTDIV
+                    {  // per wave: the longest lane's batches, all lanes' batches, lanes, cores
+                        const uint64_t act = __ballot(1);
+                        int mx = nbt, sm = nbt;
+                        for (int o = 32; o > 0; o >>= 1) {
+                            mx = max(mx, __shfl_xor(mx, o, 64));
+                            sm += __shfl_xor(sm, o, 64);
+                        }
+                        const uint64_t cm = __ballot(is_core);
+                        if (__lane_id() == __builtin_ctzll(act)) {
+                            atomicAdd(&g_div[0], (unsigned long long)mx);
+                            atomicAdd(&g_div[1], (unsigned long long)sm);
+                            atomicAdd(&g_div[2], (unsigned long long)__popcll(act));
+                            atomicAdd(&g_div[3], (unsigned long long)__popcll(cm));
+                            atomicAdd(&g_div[4], 1ull);
+                        }
+                    }
+#endif
                     if (!is_core && k_rec > 0) {  // (a complete list: cnt < minPoints)
                         // the non-core's neighbours (self excluded), -1 terminated
                         int32_t* out = nbr + (int64_t)p * nbr_k;
@@ -4173,6 +4207,15 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         slab->nbr_k = nbr_k;
     }
 }
+
+#if DBSCAN_AB_COUNTDIV
+extern "C" int dbscan_ab_countdiv(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_div), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_div), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #if DBSCAN_AB_CHECK
 // checking builds: per site {count, lowest, highest} out-of-range indices since the last read
