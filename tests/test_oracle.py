@@ -212,3 +212,22 @@ def test_reference_train_labeled_csv(labeled_data):
     pairs = set(zip(r["cluster"].tolist(), lab.astype(int).tolist()))
     assert len(pairs) == 4 and len({a for a, _ in pairs}) == 4  # a bijection
     assert (0, 0) in pairs
+
+
+def test_band_model_shapes():
+    """tests/band_model.py (the host model of the band form's staging capacity that the band
+    tests take their exact recall counts from): a dense square overflows whichever axis the
+    rows take, a dense strip overflows with its rows along it and not across it, and the
+    shipped choice (rows along the axis with fewer cells per row) takes the strip across."""
+    import numpy as np
+
+    from band_model import band_overflows, band_recall
+
+    rng = np.random.default_rng(5)
+    x, y = rng.uniform(0, 50, 20000), rng.uniform(0, 0.05, 20000)
+    assert band_overflows(x, y, 0.2)[0]  # rows along the strip: one row of 20000 points
+    assert not band_recall(x, y, 0.2) and not band_recall(y, x, 0.2)
+    sx, sy = rng.uniform(0, 0.5, 20000), rng.uniform(0, 0.5, 20000)
+    assert band_recall(sx, sy, 0.2) and band_recall(sy, sx, 0.2)
+    bx, by = rng.normal(0, 5, 3000), rng.normal(0, 5, 3000)
+    assert not band_recall(bx, by, 0.3)
