@@ -397,3 +397,76 @@ def test_band_wide_and_tall_partitions(dm, mode):
             before += expect
     finally:
         h.close()
+
+
+def test_async_queue_fuzz(dm):
+    """A seeded mix of queued work on one handle -- single fits of every form (one-workgroup,
+    spread, band, tiled), batches of partitions, forced barrier give-ups switched on and off
+    between enqueues, syncs at random points -- and one final dbscan_sync: every queued fit's
+    labels and cluster counts equal the oracle, and the handle's re-run count equals the
+    number of queued spread / band fits that ran with the give-up forced or overflowed
+    (DBSCAN.scala:150-155: an executor's fits never come back wrong)."""
+    import torch
+
+    from dbscan_amd import device as D
+
+    rng = np.random.default_rng(2026)
+    h = dm.Handle(0)
+    try:
+        h.set_spread_min(1000)
+        h.set_band_min(2500)
+        before = h.spread_fallbacks()
+        expect = 0
+        jobs = []
+        for step in range(40):
+            give_up = bool(rng.random() < 0.5)
+            h.set_spread_spin_limit(0 if give_up else 1 << 21)
+            kind = rng.choice(["single", "single", "single", "batch", "sync"])
+            if kind == "sync":
+                h.sync()
+                continue
+            mode = int(rng.integers(0, 2))
+            eps, mp = (0.2, 10) if rng.random() < 0.5 else (0.12, 6)
+            if kind == "single":
+                m = int(rng.choice([300, 1500, 4000, 9000, 20000, 70000]))
+                if m <= 9000 and rng.random() < 0.3:  # (the oracle's cost grows as m^2 here)
+                    x, y = _dense_square(rng, m)
+                else:
+                    x, y = _set(rng, m)
+                tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+                cl = torch.full((m,), -9, dtype=torch.int32, device="cuda")
+                fl = torch.full((m,), 9, dtype=torch.uint8, device="cuda")
+                nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+                torch.cuda.synchronize()
+                D.fit_tensors_async(tx, ty, eps, mp, mode, h, cl, fl, nk)
+                jobs.append(("single", [(x, y)], eps, mp, mode, (tx, ty, cl, fl, nk)))
+                lds = m <= 65536 and m >= 1000  # (spread from 1000, band from 2500 points)
+                if lds and (give_up or (m >= 2500 and band_recall(x, y, eps))):
+                    expect += 1
+            else:
+                sizes = rng.integers(50, 3000, size=int(rng.integers(3, 12)))
+                parts = [_set(rng, int(s)) for s in sizes]
+                x = np.concatenate([p[0] for p in parts])
+                y = np.concatenate([p[1] for p in parts])
+                offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+                tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+                cl = torch.full((x.size,), -9, dtype=torch.int32, device="cuda")
+                fl = torch.full((x.size,), 9, dtype=torch.uint8, device="cuda")
+                nk = torch.full((len(sizes),), -1, dtype=torch.int32, device="cuda")
+                torch.cuda.synchronize()
+                D.fit_batch_tensors_async(tx, ty, offs, eps, mp, mode, h, cl, fl, nk)
+                jobs.append(("batch", parts, eps, mp, mode, (tx, ty, cl, fl, nk)))
+        h.sync()
+        torch.cuda.synchronize()
+        h.set_spread_spin_limit(1 << 21)
+        for k, (kind, parts, eps, mp, mode, (_, _, cl, fl, nk)) in enumerate(jobs):
+            cl, fl, nk = cl.cpu().numpy(), fl.cpu().numpy(), nk.cpu().numpy()
+            o = 0
+            for p, (x, y) in enumerate(parts):
+                m = x.size
+                _eq((cl[o:o + m], fl[o:o + m], int(nk[p])), O.fit_grid(x, y, eps, mp, mode),
+                    f"job {k} ({kind}) part {p} m={m}")
+                o += m
+        assert h.spread_fallbacks() - before == expect
+    finally:
+        h.close()
