@@ -334,6 +334,12 @@ void dbscan_destroy(dbscan_handle* h) {
     // default stream): synchronizing it is valid and waits for the handle's kernels there.
     (void)hipStreamSynchronize(h->stream);
     if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
+    if (!h->ws.recalls.empty()) {  // queued fits never synced: their re-runs still owed
+        try {
+            dbscan::drain_recalls(h->stream, &h->prof, h->ws);
+        } catch (...) {
+        }
+    }
     h->prof.destroy();
     h->ws.release();
     h->hx.release();
