@@ -183,9 +183,12 @@ def test_band_overflow_and_barrier_fallbacks(dm):
         h.close()
 
 
-def test_band_from_concurrent_handles(dm):
-    """Four executor threads, a handle each, band fits at once (4 x up to 64 workgroups of
-    one CU each): every fit equals its oracle fit."""
+@pytest.mark.parametrize("nt", [4, 8, 16])
+def test_band_from_concurrent_handles(dm, nt):
+    """nt executor threads, a handle each, band fits at once (nt x up to 64 workgroups of one
+    CU each; the process has 4 hardware queues on the box, so from 8 threads on more fits are
+    queued than can run): every fit equals its oracle fit, whether or not a grid barrier gave up
+    and the fit was re-run (tools/concurrency_probe.py: no give-ups at 4-16 threads)."""
     import threading
 
     rng = np.random.default_rng(606)
@@ -194,21 +197,21 @@ def test_band_from_concurrent_handles(dm):
         x, y = _set(rng, m)
         sets.append((x, y))
     refs = [O.fit_grid(x, y, 0.12, 6, 0) for x, y in sets]
-    handles = [dm.Handle(0) for _ in range(4)]
+    handles = [dm.Handle(0) for _ in range(nt)]
     errors = []
 
     def worker(t):
         try:
-            for rep in range(2):
-                for k in range(t, len(sets), 4):
-                    x, y = sets[k]
-                    _eq(dm.fit_arrays(x, y, 0.12, 6, 0, handle=handles[t]), refs[k],
-                        f"thread {t} set {k} rep {rep}")
+            for rep in range(2 * len(sets) // nt + 1):
+                k = (t + rep) % len(sets)
+                x, y = sets[k]
+                _eq(dm.fit_arrays(x, y, 0.12, 6, 0, handle=handles[t]), refs[k],
+                    f"thread {t} set {k} rep {rep}")
         except Exception as exc:
             errors.append(exc)
 
     try:
-        ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(nt)]
         for th in ths:
             th.start()
         for th in ths:
