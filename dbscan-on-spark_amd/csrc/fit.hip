@@ -2922,41 +2922,72 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
 // final_kernel is core -> rep -> root.  qlab (direct fits): also the root's visit index per
 // quarter, and the root flag (every root is a quarter rep: the rep of exactly one quarter), so
 // that final_kernel's grid cores only read their quarter's qlab.
+// Quarters per thread (quarter base + k * kBlock): their rep loads, then their parent chains one
+// step per trip with the steps' loads in flight together; 1 quarter per thread 0.035 ms per
+// 10^7 points, 4: 0.031 (A/B on one box, round 6).
+constexpr int kQrootPer = 4;  // (2 and 8: the same)
+
 __global__ __launch_bounds__(kBlock) void quarter_root_kernel(
     const int4* __restrict__ qinfo, const int32_t* __restrict__ nq_p,
     const GridParams* __restrict__ gp, int32_t* __restrict__ parent,
     const int32_t* __restrict__ perm, int32_t* __restrict__ qlab,
     unsigned long long* __restrict__ root_bits) {
     if (!gp->clique) return;
-    const int q = blockIdx.x * kBlock + threadIdx.x;
-    if (q >= *nq_p) return;
-    const int rep = qinfo[q].z;
-    if (rep < 0) return;
-    int r = rep;
-    for (int nx = parent[r]; nx != r; nx = parent[r]) r = nx;
-    parent[rep] = r;
+    constexpr int K = kQrootPer;
+    const int nq = *nq_p;
+    const int base = blockIdx.x * (K * kBlock) + threadIdx.x;
+    int rep[K], r[K], nx[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int q = base + k * kBlock;
+        rep[k] = q < nq ? qinfo[q].z : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        r[k] = rep[k];
+        nx[k] = rep[k] >= 0 ? parent[rep[k]] : rep[k];
+    }
+    for (;;) {  // every open chain one step per trip, their loads in flight together
+        bool open = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (nx[k] != r[k]) {
+                r[k] = nx[k];
+                nx[k] = parent[r[k]];
+                open = true;
+            }
+        if (!open) break;
+    }
+    int32_t o[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (rep[k] < 0) continue;
+        parent[rep[k]] = r[k];
+        if (qlab) o[k] = perm[r[k]];
+    }
     if (qlab) {
-        const int32_t o = perm[r];
-        qlab[q] = o;
-        if (r == rep) atomicOr(root_bits + (o >> 6), 1ull << (o & 63));
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (rep[k] < 0) continue;
+            qlab[base + k * kBlock] = o[k];
+            if (r[k] == rep[k]) atomicOr(root_bits + (o[k] >> 6), 1ull << (o[k] & 63));
+        }
     }
 }
 
 // qidx/qinfo (fused union: core parents were never written): a grid core's walk starts at its
 // quarter's rep (slots >= nf are outside the grid and their own parents).
-__global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t* __restrict__ nf_p,
-                                                       const GridParams* __restrict__ gp,
-                                                       const int32_t* __restrict__ perm,
-                                                       const uint8_t* __restrict__ core,
-                                                       const int32_t* __restrict__ parent,
-                                                       const int32_t* __restrict__ qidx,
-                                                       const int4* __restrict__ qinfo,
-                                                       int32_t* __restrict__ lab,
-                                                       unsigned long long* __restrict__ root_bits,
-                                                       int32_t* __restrict__ root_out,
-                                                       const int32_t* __restrict__ qlab) {
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= n) return;
+__device__ __forceinline__ void final_point(int64_t p, const int32_t* __restrict__ nf_p,
+                                            const GridParams* __restrict__ gp,
+                                            const int32_t* __restrict__ perm,
+                                            const uint8_t* __restrict__ core,
+                                            const int32_t* __restrict__ parent,
+                                            const int32_t* __restrict__ qidx,
+                                            const int4* __restrict__ qinfo,
+                                            int32_t* __restrict__ lab,
+                                            unsigned long long* __restrict__ root_bits,
+                                            int32_t* __restrict__ root_out,
+                                            const int32_t* __restrict__ qlab) {
     if (!core[p]) {
         lab[p] = -1;
         return;
@@ -2979,6 +3010,41 @@ __global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t*
     lab[p] = o;
     if (r == (int)p && root_bits) atomicOr(root_bits + (o >> 6), 1ull << (o & 63));
     if (r == (int)p && root_out) root_out[o] = o;  // lean slab output: the local roots
+}
+
+// Four consecutive slots per thread: on direct clique fits (every grid slot's label is its
+// quarter's root label, qlab) one 4-B core load, one 16-B quarter-index load, four qlab loads
+// in flight and one 16-B store; 0.040 -> 0.022 ms per 10^7 points (A/B on one box, round 6).
+constexpr int kFinalPer = 4;
+
+__global__ __launch_bounds__(kBlock) void final_kernel(int64_t n, const int32_t* __restrict__ nf_p,
+                                                       const GridParams* __restrict__ gp,
+                                                       const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ core,
+                                                       const int32_t* __restrict__ parent,
+                                                       const int32_t* __restrict__ qidx,
+                                                       const int4* __restrict__ qinfo,
+                                                       int32_t* __restrict__ lab,
+                                                       unsigned long long* __restrict__ root_bits,
+                                                       int32_t* __restrict__ root_out,
+                                                       const int32_t* __restrict__ qlab) {
+    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kFinalPer;
+    if (p0 >= n) return;
+    if (qlab && gp->clique && p0 + 3 < *nf_p) {
+        // four consecutive grid slots: core bytes and quarter indices by one load each, their
+        // quarters' root labels in flight together, one 16-B store
+        const uchar4 c = *reinterpret_cast<const uchar4*>(core + p0);
+        const int4 qi = *reinterpret_cast<const int4*>(qidx + p0);
+        int4 out;
+        out.x = c.x ? qlab[qi.x] : -1;
+        out.y = c.y ? qlab[qi.y] : -1;
+        out.z = c.z ? qlab[qi.z] : -1;
+        out.w = c.w ? qlab[qi.w] : -1;
+        *reinterpret_cast<int4*>(lab + p0) = out;
+        return;
+    }
+    for (int64_t p = p0; p < p0 + kFinalPer && p < n; ++p)
+        final_point(p, nf_p, gp, perm, core, parent, qidx, qinfo, lab, root_bits, root_out, qlab);
 }
 
 // Lean slab output for the listed (shared) slab points: core flag and local root.
@@ -3180,15 +3246,32 @@ __global__ __launch_bounds__(kBlock) void tile_part_kernel(const int32_t* __rest
 
 // Bucketed sort: input order from the labels at the padded places (pos: input -> place); pos
 // reads are coalesced, and a block's points read from the 256 bands' segments where they
-// stand in input order (runs that advance together).
+// stand in input order (runs that advance together).  kPermPer points per thread (point
+// base + k * kBlock): their pos loads, then their packed reads, in flight together.  One point
+// per thread: 0.059 ms per 10^7 points; 4: 0.058; 8: 0.052-0.053 (config 3's share 0.071 ->
+// 0.057); 16: 0.052 (A/B on one box, round 6).
+constexpr int kPermPer = 8;
 __global__ __launch_bounds__(kBlock) void permute_out_bucket_kernel(
     int64_t n, const int32_t* __restrict__ pos, const uint32_t* __restrict__ packed,
     int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t v = packed[pos[i]];
-    cluster_out[i] = (int32_t)(v >> 1);
-    flag_out[i] = v == 0 ? 2 : (uint8_t)(v & 1u);
+    const int64_t base = (int64_t)blockIdx.x * (kPermPer * kBlock) + threadIdx.x;
+    int32_t ps[kPermPer];
+#pragma unroll
+    for (int k = 0; k < kPermPer; ++k) {
+        const int64_t i = base + k * kBlock;
+        ps[k] = i < n ? pos[i] : 0;
+    }
+    uint32_t v[kPermPer];
+#pragma unroll
+    for (int k = 0; k < kPermPer; ++k)
+        if (base + k * kBlock < n) v[k] = packed[ps[k]];
+#pragma unroll
+    for (int k = 0; k < kPermPer; ++k) {
+        const int64_t i = base + k * kBlock;
+        if (i >= n) break;
+        cluster_out[i] = (int32_t)(v[k] >> 1);
+        flag_out[i] = v[k] == 0 ? 2 : (uint8_t)(v[k] & 1u);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3917,7 +4000,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             klaunch(prof, "inverse", inverse_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, perm,
                     inv);
         if (bucketed)  // (slab fits: zs from the records, inv only for the shared points)
-            klaunch(prof, "gather_bucket", gather_bucket_kernel, dim3(nblk(n)), dim3(kBlock), 0, s,
+            klaunch(prof, "gather_bucket", gather_bucket_kernel,
+                    dim3(nblk(n)), dim3(kBlock), 0, s,
                     n, (const int32_t*)ws.bucket.slot_place, (const double4*)ws.bucket.rec, nf_p,
                     perm, xy, zs, (a.zone && a.shared_idx) ? inv : (int32_t*)nullptr);
         else if (mode != kGridNoPairs)
@@ -4084,7 +4168,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         // direct fits (fused quarter unions): the roots' visit indices per quarter (into the
         // dead qcomp) and the root flags, for final_kernel
         // (qlab_bits: zeroed by heads_down)
-        klaunch(prof, "quarter_root", quarter_root_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, qinfo,
+        klaunch(prof, "quarter_root", quarter_root_kernel,
+                dim3((unsigned)((n + kQrootPer * kBlock - 1) / (kQrootPer * kBlock))), dim3(kBlock), 0, s, qinfo,
                 &st[kStQuarters], gp, parent, perm, qlab_bits ? qcomp : (int32_t*)nullptr,
                 reinterpret_cast<unsigned long long*>(qlab_bits));
         DBSCAN_HIP_CHECK(hipGetLastError());
@@ -4109,7 +4194,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             StageTimer t(prof, s, "final");
             if (!root_words)  // (eps grids: zeroed by heads_down)
                 DBSCAN_HIP_CHECK(hipMemsetAsync(root_bits, 0, nw * sizeof(uint64_t), s));
-            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
+            klaunch(prof, "final", final_kernel, dim3(nblk((n + kFinalPer - 1) / kFinalPer)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
                                reinterpret_cast<unsigned long long*>(root_bits), (int32_t*)nullptr,
                                qlab_bits ? (const int32_t*)qcomp : (const int32_t*)nullptr);
@@ -4129,7 +4214,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                     cell, seg, nf_p, n, a.eps, eps2, core, lab, root_bits, word_rank, cmap,
                     packed, bucketed ? (const int32_t*)ws.bucket.slot_place : nullptr);
             if (bucketed)
-                klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
+                klaunch(prof, "permute_out", permute_out_bucket_kernel,
+                        dim3((unsigned)((n + kPermPer * kBlock - 1) / (kPermPer * kBlock))), dim3(kBlock),
                         0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
                         a.flag);
             else
@@ -4155,7 +4241,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         (const uint64_t*)root_bits, (const int32_t*)word_rank,
                         (const int32_t*)st, a.batch->nclusters);
             } else if (bucketed) {
-                klaunch(prof, "permute_out", permute_out_bucket_kernel, dim3(nblk(n)), dim3(kBlock),
+                klaunch(prof, "permute_out", permute_out_bucket_kernel,
+                        dim3((unsigned)((n + kPermPer * kBlock - 1) / (kPermPer * kBlock))), dim3(kBlock),
                         0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
                         a.flag);
             } else {
@@ -4169,7 +4256,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
             StageTimer t(prof, s, "final");
             const bool lean = a.shared_idx != nullptr;
             if (lean) DBSCAN_HIP_CHECK(hipMemsetAsync(a.root_out, 0xFF, n * sizeof(int32_t), s));
-            klaunch(prof, "final", final_kernel, dim3(nblk(n)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
+            klaunch(prof, "final", final_kernel, dim3(nblk((n + kFinalPer - 1) / kFinalPer)), dim3(kBlock), 0, s, n, nf_p, gp, perm, core,
                                parent, fuse ? qidx : nullptr, qinfo, lab,
                                (unsigned long long*)nullptr, lean ? a.root_out : (int32_t*)nullptr,
                                (const int32_t*)nullptr);

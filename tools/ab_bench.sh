@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B the library variants built by tools/build_ab.sh on one GPU box, interleaved ROUNDS times:
 #   VARIANTS="base new" ROUNDS=3 BENCH_ARGS="..." bash tools/ab_bench.sh
-# "main" is the in-tree library.  Prints ms_per_step and the top kernels of every run.
+# "main" is the in-tree library.  Prints ms_per_step and the top kernels of every run (KERNELS="a b":
+# those kernels instead).
 set -o pipefail
 mkdir -p gpurun_out/ab
 ARGS="${BENCH_ARGS:---steps 20 --warmup 5} --no-cpu-baseline --e2e-steps 0"
@@ -14,7 +15,10 @@ for r in $(seq 1 ${ROUNDS:-2}); do
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 k = d["kernels_ms_per_step"]
-top = ", ".join(f"{a}={b:.3f}" for a, b in list(k.items())[:8])
+import os
+want = os.environ.get("KERNELS", "").split()
+top = ", ".join(f"{a}={b:.3f}" for a, b in (list(k.items())[:8] if not want else
+                                           [(w, k.get(w, float("nan"))) for w in want]))
 cnt = "+".join(f"{k.get(a, 0):.3f}" for a in ("count32", "count_wave", "count_tiny", "count_tiny16", "big_count"))
 print(f"{sys.argv[1]:10s} {d['ms_per_step']:.4f} ms  k={d['config']['clusters']}  count {cnt}  {top}")
 PY
