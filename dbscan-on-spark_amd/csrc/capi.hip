@@ -414,6 +414,7 @@ int32_t dbscan_fit_device_async(dbscan_handle* h, const double* d_x, const doubl
         a.spread_min = h->spread_min;
         a.band_max = h->band_max;
         a.band_min = h->band_min;
+        a.n_clusters_dev = d_n_clusters;
         h->prepared = false;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         if (d_n_clusters) dbscan::write_nclusters(h->stream, h->ws, d_n_clusters);
@@ -1277,6 +1278,7 @@ void batch_enqueue(dbscan_handle* h, const double* dx, const double* dy, const i
         dbscan::FitArgs a{dx + o, dy + o, nullptr, m, eps, min_points, mode, dcl + o, dfl + o,
                           nullptr, nullptr};
         a.small_max = 0;
+        a.n_clusters_dev = dnk + p;
         dbscan::enqueue_fit(h->stream, h->ws, &h->prof, a, &h->slab);
         dbscan::write_nclusters(h->stream, h->ws, dnk + p);
         h->pending = true;

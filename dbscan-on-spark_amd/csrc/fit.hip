@@ -3188,7 +3188,9 @@ template <bool SLAB>
 __global__ __launch_bounds__(kBlock) void permute_out_kernel(
     int64_t n, const int32_t* __restrict__ inv, const uint32_t* __restrict__ packed,
     const uint8_t* __restrict__ zone, int32_t* __restrict__ cluster_out,
-    uint8_t* __restrict__ flag_out) {
+    uint8_t* __restrict__ flag_out, const int32_t* __restrict__ nk_src,
+    int32_t* __restrict__ nk_out) {
+    if (nk_out && blockIdx.x == 0 && threadIdx.x == 0) *nk_out = *nk_src;  // (the cluster count)
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     if (SLAB && zone[i] != 0) return;
@@ -3253,7 +3255,9 @@ __global__ __launch_bounds__(kBlock) void tile_part_kernel(const int32_t* __rest
 constexpr int kPermPer = 8;
 __global__ __launch_bounds__(kBlock) void permute_out_bucket_kernel(
     int64_t n, const int32_t* __restrict__ pos, const uint32_t* __restrict__ packed,
-    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out) {
+    int32_t* __restrict__ cluster_out, uint8_t* __restrict__ flag_out,
+    const int32_t* __restrict__ nk_src, int32_t* __restrict__ nk_out) {
+    if (nk_out && blockIdx.x == 0 && threadIdx.x == 0) *nk_out = *nk_src;  // (the cluster count)
     const int64_t base = (int64_t)blockIdx.x * (kPermPer * kBlock) + threadIdx.x;
     int32_t ps[kPermPer];
 #pragma unroll
@@ -3810,6 +3814,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     if (slab) slab->valid = false;
     ws.fit_mirrored = false;
     ws.out_direct = false;
+    ws.nk_written = false;
     const int64_t n = a.n;
     const double eps2 = a.eps * a.eps;  // LocalDBSCANNaive.scala:33
     const int mode =
@@ -4217,11 +4222,13 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "permute_out", permute_out_bucket_kernel,
                         dim3((unsigned)((n + kPermPer * kBlock - 1) / (kPermPer * kBlock))), dim3(kBlock),
                         0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
-                        a.flag);
+                        a.flag, (const int32_t*)&st[kStClusters], a.n_clusters_dev);
             else
                 klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
-                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag,
+                        (const int32_t*)&st[kStClusters], a.n_clusters_dev);
             DBSCAN_HIP_CHECK(hipGetLastError());
+            ws.nk_written = a.n_clusters_dev != nullptr;
         } else {
             StageTimer t(prof, s, "output");
             uint32_t* packed = static_cast<uint32_t*>(
@@ -4244,12 +4251,14 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 klaunch(prof, "permute_out", permute_out_bucket_kernel,
                         dim3((unsigned)((n + kPermPer * kBlock - 1) / (kPermPer * kBlock))), dim3(kBlock),
                         0, s, n, (const int32_t*)ws.bucket.pos, (const uint32_t*)packed, a.cluster,
-                        a.flag);
+                        a.flag, (const int32_t*)&st[kStClusters], a.n_clusters_dev);
             } else {
                 klaunch(prof, "permute_out", permute_out_kernel<false>, dim3(nblk(n)), dim3(kBlock),
-                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag);
+                        0, s, n, inv, packed, (const uint8_t*)nullptr, a.cluster, a.flag,
+                        (const int32_t*)&st[kStClusters], a.n_clusters_dev);
             }
             DBSCAN_HIP_CHECK(hipGetLastError());
+            ws.nk_written = a.n_clusters_dev != nullptr && !a.batch;
         }
     } else {
         {
@@ -4330,6 +4339,7 @@ extern "C" int dbscan_ab_bounds(long long* out) {
 #endif
 
 void write_nclusters(hipStream_t s, Workspace& ws, int32_t* d_out) {
+    if (ws.nk_written) return;  // (the fit's output kernel wrote it: FitArgs::n_clusters_dev)
     if (ws.fit_n == 0) {
         DBSCAN_HIP_CHECK(hipMemsetAsync(d_out, 0, sizeof(int32_t), s));
         return;
@@ -4477,7 +4487,8 @@ void run_slab_label(hipStream_t s, Workspace& ws, Profiler* prof, const SlabStat
                        (const int32_t*)nullptr, zone, gid,
                        gs_of_root, label_of_root, packed, st.place);
     klaunch(prof, "permute_out", permute_out_kernel<true>, dim3(nblk(st.n)), dim3(kBlock), 0, s, st.n,
-                       st.to_packed, packed, zone, cluster, flag);
+                       st.to_packed, packed, zone, cluster, flag, (const int32_t*)nullptr,
+                       (int32_t*)nullptr);
     DBSCAN_HIP_CHECK(hipGetLastError());
 }
 

@@ -183,6 +183,7 @@ struct Workspace {
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
     bool fit_mirrored = false;     // the last fit (an LDS form) wrote its stats into fit_block
     bool out_direct = false;       // ... and its labels into FitArgs::cluster_host / flag_host
+    bool nk_written = false;       // ... and its cluster count into FitArgs::n_clusters_dev
     // Every LDS fit (small.hip: one-workgroup, spread and band forms) writes its statistics,
     // kStError included, into a pinned block of its OWN, taken from a ring: fits queued back to
     // back on the stream never share one, so each one's outcome survives until the host reads
@@ -343,6 +344,9 @@ struct FitArgs {
     // write the labels there themselves, no copy back (Workspace::out_direct tells)
     int32_t* cluster_host = nullptr;
     uint8_t* flag_host = nullptr;
+    // device word for the cluster count (asynchronous API): the tiled pipeline's output kernel
+    // writes it (Workspace::nk_written; write_nclusters then launches nothing)
+    int32_t* n_clusters_dev = nullptr;
 };
 
 // What a slab fit leaves on its handle for the label phase (dbscan_slab_label_device).
