@@ -1382,6 +1382,10 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
                                   int32_t* __restrict__ parent, UnionLds& u) {
     const int i = threadIdx.x;
     const auto is_core = [&](int j) { return core[j] != 0; };
+    // every quarter's slot range and its rep's coordinates in LDS: a pair's first test (the two
+    // reps, which most adjacent pairs pass) reads no global memory
+    __shared__ int qs[kMaxTileQ + 1];
+    __shared__ double2 rxy[kMaxTileQ];
     u.qmap[i] = 0xFFFF;
     u.cmin[i] = ~0ull;
     lds_barrier();
@@ -1398,11 +1402,31 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
         const int len = e - b;
         uint32_t mask = 0;
         int first = -1;
-        for (int j = 0; j < len && (j < 32 || first < 0); ++j)
-            if (is_core(b + j)) {
-                if (j < 32) mask |= 1u << j;
-                if (first < 0) first = j;
+        {
+            // the first 32 core flags by up to 9 aligned words, all loads in flight (a loop of
+            // byte loads waited for each one)
+            const int l32 = len < 32 ? len : 32;
+            const int a0 = b >> 2, sh = (b & 3) * 8;
+            const int last = l32 > 0 ? ((b + l32 - 1) >> 2) - a0 : -1;  // words needed: 0..last
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(core);
+            uint32_t w[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) w[k] = k <= last ? cw[a0 + k] : 0u;
+            // one bit per nonzero byte (bits 7, 15, 23, 31), packed to a nibble per word
+            uint64_t bits = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const uint32_t x = w[k];
+                const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+                const uint32_t nib = ((nz >> 7) & 1u) | ((nz >> 14) & 2u) | ((nz >> 21) & 4u) |
+                                     ((nz >> 28) & 8u);
+                bits |= (uint64_t)nib << (4 * k);
             }
+            mask = (uint32_t)(bits >> (sh >> 3)) & (l32 == 32 ? ~0u : ((1u << l32) - 1u));
+            first = mask ? __ffs(mask) - 1 : -1;
+            for (int j = 32; j < len && first < 0; ++j)
+                if (is_core(b + j)) first = j;
+        }
         if (first >= 0) {
             rep = b + first;
             best = fa.perm[rep];
@@ -1412,6 +1436,9 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
         u.lrange[i] = (rep >= 0 ? 0x80000000u : 0u) | ((uint32_t)lq << 22);
         u.lmask[i] = mask;
         u.qmap[lq] = (uint16_t)i;
+        qs[i] = b;
+        if (i == nq - 1) qs[nq] = e;
+        rxy[i] = rep >= 0 ? xy[rep] : make_double2(0.0, 0.0);
     }
     lds_barrier();
     // pair tests, one (quarter, offset) item per thread, adjacent quarters first so that most
@@ -1431,8 +1458,15 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
             if (!(rj >> 31)) continue;
             // (adjacent items run all at once: a find before each would rarely prune)
             if (sweep && lfind(u.lp, qi) == lfind(u.lp, j)) continue;
-            const int ab = fa.qstart[q0 + qi], ae = fa.qstart[q0 + qi + 1];
-            const int bb = fa.qstart[q0 + j], be = fa.qstart[q0 + j + 1];
+            {
+                const double2 pa = rxy[qi], pb = rxy[j];
+                if (within_eps(pa.x, pa.y, pb.x, pb.y, eps2)) {
+                    lunite(u.lp, qi, j);
+                    continue;
+                }
+            }
+            const int ab = qs[qi], ae = qs[qi + 1];
+            const int bb = qs[j], be = qs[j + 1];
             if (quarters_touch(xy, ab, ae, u.lmask[qi], bb, be, u.lmask[j], is_core, eps2))
                 lunite(u.lp, qi, j);
         }
