@@ -182,6 +182,32 @@ def test_argument_errors(dm, handle):
         == _lib.DBSCAN_OK and k.value == 0
 
 
+@pytest.mark.parametrize("n", [100_000, 9_000_000])
+def test_async_cluster_count_from_the_output_kernel(dm, handle, n):
+    """dbscan_fit_device_async on the tiled pipeline: the cluster count lands in the caller's
+    device word, written by the output kernel itself (FitArgs::n_clusters_dev; 100k points:
+    the plain sort's permute_out_kernel, 9M: the bucketed sort's permute_out_bucket_kernel), and
+    equals the synchronous fit's count and labels (the oracle digest of the full-size configs
+    pins those)."""
+    import torch
+    from dbscan_amd import device as D
+
+    x, y = D.generate_blobs(n, 0.1, 1.0, 11, handle)
+    cl = torch.empty(n, dtype=torch.int32, device="cuda")
+    fl = torch.empty(n, dtype=torch.uint8, device="cuda")
+    nk = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    D.fit_tensors_async(x, y, 2.55, 10, 0, handle, cl, fl, nk)
+    handle.sync()
+    cl2 = torch.empty_like(cl)
+    fl2 = torch.empty_like(fl)
+    _, _, k2 = D.fit_tensors(x, y, 2.55, 10, 0, handle, cl2, fl2)
+    torch.cuda.synchronize()
+    assert int(nk.item()) == int(k2) > 0
+    assert torch.equal(cl, cl2) and torch.equal(fl, fl2)
+    assert int(cl.max().item()) == int(k2)
+
+
 def test_async_fits_back_to_back(dm, handle):
     """dbscan_fit_device_async: several fits of different inputs (grid, all-pairs, no-finite)
     enqueued without any host synchronization, each output buffer equal to the oracle after
