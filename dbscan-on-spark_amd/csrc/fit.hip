@@ -1404,7 +1404,8 @@ __device__ void global_tile_union(int q0, int nq, int b, int e, uint32_t key, co
         int first = -1;
         {
             // the first 32 core flags by up to 9 aligned words, all loads in flight (a loop of
-            // byte loads waited for each one)
+            // byte loads waited for each one); the last word may reach 3 bytes past the
+            // quarter, inside the core array's 4 bytes of slack
             const int l32 = len < 32 ? len : 32;
             const int a0 = b >> 2, sh = (b & 3) * 8;
             const int last = l32 > 0 ? ((b + l32 - 1) >> 2) - a0 : -1;  // words needed: 0..last
@@ -3989,7 +3990,8 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* tslot =
         static_cast<int32_t*>(ws.tslot.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
     int2* tstage = static_cast<int2*>(ws.tstage.ensure((size_t)ntile_bound * 100 * sizeof(int2)));
-    uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n));
+    // (+4: big_union reads a quarter's first core flags as whole 4-B words)
+    uint8_t* core = static_cast<uint8_t*>(ws.core.ensure(n + 4));
     int32_t* parent = static_cast<int32_t*>(ws.parent.ensure(n * sizeof(int32_t)));
     int32_t* lab = static_cast<int32_t*>(ws.lab.ensure(n * sizeof(int32_t)));
     int32_t* tq = static_cast<int32_t*>(ws.tq.ensure((size_t)ntile_bound * kTslot * sizeof(int32_t)));
