@@ -2635,7 +2635,8 @@ __device__ __forceinline__ void union_body(int b, int nb, const double2* __restr
                                            int32_t* __restrict__ parent) {
     if (gp->clique) return;  // quarter-cell unions instead (a small grid: exits at once)
     const int64_t nf = *nf_p;
-    for (int64_t p = (int64_t)b * kBlock + threadIdx.x; p < nf; p += (int64_t)nb * kBlock) {
+    const int bs = (int)blockDim.x;
+    for (int64_t p = (int64_t)b * bs + threadIdx.x; p < nf; p += (int64_t)nb * bs) {
         if (!core[p]) continue;
         const double2 me = xy[p];
         const Seg s = load_seg(seg, cell[p]);
@@ -2704,6 +2705,11 @@ static_assert(DBSCAN_AB_EDGE_W <= 6, "edge_union_kernel misbehaves at launch bou
 #ifndef DBSCAN_AB_EDGE_STOP
 #define DBSCAN_AB_EDGE_STOP 0
 #endif
+// edge_union's waves per workgroup: 2 (or 1) measured 0.154 -> 0.146 ms at config 2 and 0.184 ->
+// 0.172 on config 3's share against 4: a workgroup's slot is freed only when its last wave ends
+#ifndef DBSCAN_AB_EDGE_WAVES
+#define DBSCAN_AB_EDGE_WAVES 2
+#endif
 // DBSCAN_AB_EDGE_COUNT (counting builds only): edge_union's pair-test outcomes, summed over the
 // fit, read back (and cleared) by dbscan_ab_edge_counts() (tools/edge_probe.py)
 #ifndef DBSCAN_AB_EDGE_COUNT
@@ -2761,8 +2767,10 @@ __device__ __forceinline__ void edge_unite(int32_t* __restrict__ parent,
 #endif
 }
 
-template <int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
+// WAVES: waves per workgroup, each on its own (tile, side) tasks.  (A workgroup's slot is freed
+// only when its last wave ends, so waves of uneven task lists hold each other's slots.)
+template <int MINW, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, MINW) void edge_union_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ ntiles_p,
     const int32_t* __restrict__ tq, const int4* __restrict__ tnb,
     const int4* __restrict__ qinfo, const int4* __restrict__ qg,
@@ -2779,19 +2787,19 @@ __global__ __launch_bounds__(kBlock, MINW) void edge_union_kernel(
         return;
     }
     if (!gp->clique) return;
-    __shared__ int4 nqi[kBlock / 64][kEdgeNodes];
-    __shared__ int2 ngq[kBlock / 64][kEdgeNodes];
-    __shared__ int ncomp[kBlock / 64][kEdgeNodes];
-    __shared__ int nlp[kBlock / 64][kEdgeNodes];
+    __shared__ int4 nqi[WAVES][kEdgeNodes];
+    __shared__ int2 ngq[WAVES][kEdgeNodes];
+    __shared__ int ncomp[WAVES][kEdgeNodes];
+    __shared__ int nlp[WAVES][kEdgeNodes];
     // facing nodes by position along the strip: facing cell f (0..7; the corner cell is f = 8
     // on side 0, f = -1 on side 1) holds nodes [fnb[f + 1], fne[f + 1])
-    __shared__ int fnb[kBlock / 64][10], fne[kBlock / 64][10];
+    __shared__ int fnb[WAVES][10], fne[WAVES][10];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ntiles = *ntiles_p;
     int* lp = nlp[w];
     // one (tile, side) per wave and loop trip: waves never wait for each other
-    for (int tw = xcd_block(edge_blocks) * (kBlock / 64) + w; tw < 2 * ntiles;
-         tw += edge_blocks * (kBlock / 64)) {
+    for (int tw = xcd_block(edge_blocks) * WAVES + w; tw < 2 * ntiles;
+         tw += edge_blocks * WAVES) {
         const int t = tw >> 1, side = tw & 1;
         int nA = 0, ntot = 0;
         {
@@ -4199,10 +4207,12 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
         {
             StageTimer t(prof, s, "union_edge");
             // (+ union_kernel's blocks: a no-op on clique grids, the only union on the others)
-            const unsigned ug = std::min(nblk(n), 2048u);
-            klaunch(prof, "edge_union", edge_union_kernel<DBSCAN_AB_EDGE_W>, dim3(tile_grid + ug), dim3(kBlock), 0,
-                    s, xy, &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm, core, parent, gp,
-                    (const uint8_t*)tcore, (int)tile_grid, cell, seg, nf_p);
+            constexpr int EW = DBSCAN_AB_EDGE_WAVES;
+            const unsigned ug = std::min(nblk(n), 2048u) * (kBlock / (64 * EW));
+            const unsigned eg = tile_grid * (kBlock / (64 * EW));  // (the same waves in all)
+            klaunch(prof, "edge_union", edge_union_kernel<DBSCAN_AB_EDGE_W, EW>, dim3(eg + ug),
+                    dim3(64 * EW), 0, s, xy, &st[kStTiles], tq, tnb, qinfo, qg, qcomp, eps2, perm,
+                    core, parent, gp, (const uint8_t*)tcore, (int)eg, cell, seg, nf_p);
             DBSCAN_HIP_CHECK(hipGetLastError());
         }
         StageTimer t(prof, s, "union_root");
