@@ -2167,8 +2167,8 @@ struct WaveTile {
 };
 
 // Walks the small-tile buckets [B0, B0 + NB) (tile_class_kernel), largest stages first.
-template <int MINW, int SEG, int SCAP, int B0, int NB>
-__global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
+template <int MINW, int SEG, int SCAP, int B0, int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, MINW) void count_wave_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ tstart,
     const int2* __restrict__ tstage, double eps2, int32_t min_points,
     uint8_t* __restrict__ core, int32_t* __restrict__ parent,
@@ -2176,8 +2176,8 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
     constexpr int NSEG = 64 / SEG, NQ = SCAP / SEG;
     static_assert(B0 + NB <= kSmallBuckets && 64 % SEG == 0 && SEG >= 8 && SCAP % SEG == 0,
                   "small-tile buckets / segments");
-    __shared__ WaveTile<SCAP, NSEG> wt[kBlock / 64];
-    __shared__ int wcores[kBlock / 64];
+    __shared__ WaveTile<SCAP, NSEG> wt[WAVES];
+    __shared__ int wcores[WAVES];
     const GridParams g = *fa.gp;
     const int lane = __lane_id(), w = threadIdx.x >> 6;
     const int sgi = lane / SEG, sl = lane - sgi * SEG;  // the lane's tile and its lane in it
@@ -2192,8 +2192,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
         const int32_t* lists = fa.tl.small + (int64_t)B0 * fa.tl.cap;
         const int nt = order.size();
         const int ngroups = (nt + NSEG - 1) / NSEG;
-        for (int kg = blockIdx.x * (kBlock / 64) + w; kg < ngroups;
-             kg += gridDim.x * (kBlock / 64)) {
+        for (int kg = blockIdx.x * WAVES + w; kg < ngroups; kg += gridDim.x * WAVES) {
             // a segment without a tile runs the same steps over an empty stage
             const int k = kg * NSEG + sgi;
             const bool live = k < nt;
@@ -2450,7 +2449,7 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
         int tot = 0;
-        for (int v = 0; v < kBlock / 64; ++v) tot += wcores[v];
+        for (int v = 0; v < WAVES; ++v) tot += wcores[v];
         block_cores[blockIdx.x] = tot;
     }
 }
@@ -2459,22 +2458,25 @@ __global__ __launch_bounds__(kBlock, MINW) void count_wave_kernel(
 // counts from global memory, spread over kBigChunks workgroups per tile (such tiles are the
 // dense cores of clusters: thousands of points each), then each tile's quarter union.
 constexpr int kBigChunks = 8;
-template <int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
+template <int MINW, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, MINW) void big_count_kernel(
     const double2* __restrict__ xy, const int32_t* __restrict__ cell,
     const Seg* __restrict__ seg, const int32_t* __restrict__ tstart,
     const int32_t* __restrict__ qidx, double eps2, int32_t min_points,
     uint8_t* __restrict__ core, int32_t* __restrict__ block_cores, int32_t* __restrict__ nbr,
     int nbr_k, FuseArgs fa) {
-    __shared__ int wcores[kBlock / 64];
+    // WAVES waves per workgroup: a tile's points in chunks of 64 * WAVES, kBigChunks * kBlock
+    // apart (the same coverage whatever WAVES)
+    constexpr int CS = 64 * WAVES, NC = kBigChunks * kBlock / CS;
+    __shared__ int wcores[WAVES];
     __shared__ TileStage st;  // (unused by the global-memory count)
     int mine = 0;
     if (fa.gp->clique) {
         const int nb = fa.tl.n[kTileBig];
-        for (int k = blockIdx.x; k < nb * kBigChunks; k += gridDim.x) {
-            const int t = fa.tl.big[k / kBigChunks], c = k % kBigChunks;
+        for (int k = blockIdx.x; k < nb * NC; k += gridDim.x) {
+            const int t = fa.tl.big[k / NC], c = k % NC;
             const int te = tstart[t + 1];
-            for (int p = tstart[t] + c * kBlock + (int)threadIdx.x; p < te;
+            for (int p = tstart[t] + c * CS + (int)threadIdx.x; p < te;
                  p += kBigChunks * kBlock) {
                 // a quarter cell is a clique on these grids: one holding minPoints points makes
                 // each of them core without a count (a third of the big tiles' points at 10^7)
@@ -2495,7 +2497,7 @@ __global__ __launch_bounds__(kBlock, MINW) void big_count_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
         int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += wcores[w];
+        for (int w = 0; w < WAVES; ++w) tot += wcores[w];
         block_cores[blockIdx.x] = tot;
     }
 }
@@ -2701,6 +2703,16 @@ static_assert(DBSCAN_AB_EDGE_W <= 6, "edge_union_kernel misbehaves at launch bou
 // 0.103 ms at config 2 against 5 (81 VGPRs); 6: 0.111; 8 spills
 #ifndef DBSCAN_AB_BIGC_W
 #define DBSCAN_AB_BIGC_W 7
+#endif
+// waves per workgroup of big_count and of count_wave / count_tiny (each wave on work of its own;
+// a workgroup's slot is released only when its last wave ends): big_count 1 wave 0.105 -> 0.099
+// ms at config 2, 0.44 -> 0.42 at config 4 (2 waves: 0.102, 0.428); count_wave 1 wave 0.058 ->
+// 0.057 ms at config 2, 0.124 -> 0.118 on config 3's share (round 6, A/B on one box)
+#ifndef DBSCAN_AB_BIGC_WAVES
+#define DBSCAN_AB_BIGC_WAVES 1
+#endif
+#ifndef DBSCAN_AB_CW_WAVES
+#define DBSCAN_AB_CW_WAVES 1
 #endif
 #ifndef DBSCAN_AB_EDGE_STOP
 #define DBSCAN_AB_EDGE_STOP 0
@@ -4131,11 +4143,17 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     // per-block core counts: (f32: count32 | big_count |) count (| f32: count_wave) |
     // count_rest, then their scan
     int32_t* block_cores = static_cast<int32_t*>(
-        ws.blockcnt.ensure(2 * ((size_t)5 * tile_grid + rest_grid + 1) * sizeof(int32_t)));
+        ws.blockcnt.ensure(2 * ((size_t)(2 + 4 / DBSCAN_AB_BIGC_WAVES + 8 / DBSCAN_AB_CW_WAVES) *
+                                    tile_grid + rest_grid + 1) * sizeof(int32_t)));
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
-    const int64_t nmain = (f32 ? 5 : 1) * (int64_t)tile_grid;
+    // per-block core counts: count32 [0, G), big_count [G, G + BG) (BG: its workgroups, smaller
+    // ones than kBlock), count (fp64) [G + BG, 2G + BG), count_wave, count_tiny; G = tile_grid
+    const int64_t big_grid = (int64_t)tile_grid * (4 / DBSCAN_AB_BIGC_WAVES);
+    const int64_t cw_grid = (int64_t)tile_grid * (4 / DBSCAN_AB_CW_WAVES);  // count_wave, _tiny
+    const int64_t nmain =
+        f32 ? 2 * (int64_t)tile_grid + big_grid + 2 * cw_grid : (int64_t)tile_grid;
     bool rest_done = false;  // count_rest's blocks ran inside the fp64 count launch
     {
         StageTimer t(prof, s, "count");
@@ -4151,19 +4169,22 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                 // lanes per tile over kTinyCap points; count_tiny: tiles packed 2 to a wave),
                 // medium one workgroup each (count32), big from global memory (big_count +
                 // big_union); other eps grids: count (fp64, exits at once on clique grids)
-                int32_t* bc = block_cores + 3 * tile_grid;
-                klaunch(prof, "count_wave", count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0>,
-                        dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
+                int32_t* bc = block_cores + 2 * tile_grid + big_grid;
+                constexpr int CW = DBSCAN_AB_CW_WAVES;
+                klaunch(prof, "count_wave",
+                        count_wave_kernel<5, 64, kSmallCap, 0, kTinyBucket0, CW>,
+                        dim3((unsigned)cw_grid), dim3(64 * CW), 0, s, xy, tstart, tstage, eps2,
                         a.min_points, core, parent, bc, nbr, nbr_k, fa);
                 klaunch(prof, "count_tiny",
                         count_wave_kernel<kTinyWaves, 32, kTinyCap, kTinyBucket0,
-                                          kSmallBuckets - kTinyBucket0>,
-                        dim3(tile_grid), dim3(kBlock), 0, s, xy, tstart, tstage, eps2,
-                        a.min_points, core, parent, bc + tile_grid, nbr, nbr_k, fa);
+                                          kSmallBuckets - kTinyBucket0, CW>,
+                        dim3((unsigned)cw_grid), dim3(64 * CW), 0, s, xy, tstart, tstage, eps2,
+                        a.min_points, core, parent, bc + cw_grid, nbr, nbr_k, fa);
                 klaunch(prof, "count32", count_tile32_kernel<kCap32, 6>, dim3(tile_grid),
                         dim3(kBlock), 0, s, xy, tstart, tstage, &st[kStTiles], eps2,
                         a.min_points, core, parent, block_cores, nbr, nbr_k, fa);
-                klaunch(prof, "big_count", big_count_kernel<DBSCAN_AB_BIGC_W>, dim3(tile_grid), dim3(kBlock), 0,
+                klaunch(prof, "big_count", big_count_kernel<DBSCAN_AB_BIGC_W, DBSCAN_AB_BIGC_WAVES>,
+                        dim3((unsigned)big_grid), dim3(64 * DBSCAN_AB_BIGC_WAVES), 0,
                         s, xy, cell, seg, tstart, qidx, eps2, a.min_points, core,
                         block_cores + tile_grid, nbr, nbr_k, fa);
                 // one workgroup per big tile up to kTileGrid (a grid of 2048 gave the tiles past
@@ -4172,7 +4193,7 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
                         (const uint8_t*)core, eps2, parent, fa);
                 klaunch(prof, "count", count_tile_kernel<1536, 5>, dim3(tile_grid + rest_grid),
                         dim3(kBlock), 0, s, xy, cell, seg, tstart, tstage, &st[kStTiles], eps2,
-                        a.min_points, core, parent, block_cores + 2 * tile_grid, nbr, nbr_k,
+                        a.min_points, core, parent, block_cores + tile_grid + big_grid, nbr, nbr_k,
                         (const GridParams*)gp, (int)tile_grid, nf_p, n, block_cores + nmain);
                 rest_done = true;
             } else {
