@@ -4148,8 +4148,9 @@ void enqueue_fit(hipStream_t s, Workspace& ws, Profiler* prof, const FitArgs& a,
     int32_t* nbr = nbr_k > 0
                        ? static_cast<int32_t*>(ws.nbr.ensure((size_t)n * nbr_k * sizeof(int32_t)))
                        : nullptr;
-    // per-block core counts: count32 [0, G), big_count [G, G + BG) (BG: its workgroups, smaller
-    // ones than kBlock), count (fp64) [G + BG, 2G + BG), count_wave, count_tiny; G = tile_grid
+    // per-block core counts: count32 [0, G), big_count [G, G + BG), count (fp64) [G + BG,
+    // 2G + BG), count_wave and count_tiny CG each after it; G = tile_grid, BG and CG the grids of
+    // the kernels whose workgroups are smaller than kBlock
     const int64_t big_grid = (int64_t)tile_grid * (4 / DBSCAN_AB_BIGC_WAVES);
     const int64_t cw_grid = (int64_t)tile_grid * (4 / DBSCAN_AB_CW_WAVES);  // count_wave, _tiny
     const int64_t nmain =

@@ -183,7 +183,7 @@ struct Workspace {
     double* stats_host = nullptr;  // pinned: the stats block read_fit_stats copies back
     bool fit_mirrored = false;     // the last fit (an LDS form) wrote its stats into fit_block
     bool out_direct = false;       // ... and its labels into FitArgs::cluster_host / flag_host
-    bool nk_written = false;       // ... and its cluster count into FitArgs::n_clusters_dev
+    bool nk_written = false;       // the last fit (tiled) wrote its count to FitArgs::n_clusters_dev
     // Every LDS fit (small.hip: one-workgroup, spread and band forms) writes its statistics,
     // kStError included, into a pinned block of its OWN, taken from a ring: fits queued back to
     // back on the stream never share one, so each one's outcome survives until the host reads
