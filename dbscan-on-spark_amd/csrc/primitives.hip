@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kOffThreads) void radix_offsets_kernel(
 template <int W>
 struct DownsweepSmem {
     static constexpr int RB = 1 << W;
-    int32_t cnt[kWaves][RB];  // per-wave digit counters -> wave offsets within a digit
+    uint16_t cnt[kWaves][RB];  // per-wave digit counters -> wave offsets within a digit
     uint32_t keys[kRTile];
     int32_t vals[kRTile];
     int32_t tile_start[RB + 1];
@@ -713,28 +713,22 @@ __global__ __launch_bounds__(1024) void bucket_offsets_kernel(const int32_t* __r
     }
 }
 
-// The MSD pass and the segmented LSD passes: radix_downsweep_kernel's ranking (one 2048-key
-// tile per workgroup, per-wave match-any ballots, the tile sorted in LDS, digit runs written
-// coalesced), with
-//   MODE 1 (MSD split, top 8 bits: shift = bits - 8 from the device): keys and records
-//          (x, y, input index, zone) written by digit run to the digit's padded segment
-//          (pshift[d]), pos[i] = the padded place.  The records are staged in LDS a quarter of
-//          the tile at a time (kMsdParts): each wave store then covers a few digit runs instead
-//          of 64 scattered 32-B records (0.186 -> 0.136 ms per 10^7 points; the whole tile
-//          staged at once: 0.183, its 64 KB of LDS leaving 2 workgroups per CU; eighths 0.147)
-//   MODE 2 (LSD within segments, bits = the low width, seg[kSegLBits]): payload = padded
-//          place (identity on the first pass); the last pass writes the dense order: key_fin
-//          and val_fin (slot -> padded place), pads dropped
+// The MSD pass: radix_downsweep_kernel's ranking (one 2048-key tile per workgroup, per-wave
+// match-any ballots, the tile sorted in LDS) on the top 8 bits (shift = bits - 8 from the
+// device); keys and records (x, y, input index, zone) written by digit run to the digit's
+// padded segment (pshift[d]), pos[i] = the padded place.  The records are staged in LDS a
+// quarter of the tile at a time (kMsdParts): each wave store then covers a few digit runs
+// instead of 64 scattered 32-B records (0.186 -> 0.136 ms per 10^7 points; the whole tile
+// staged at once: 0.183, its 64 KB of LDS leaving 2 workgroups per CU; eighths 0.147).
 struct BucketExtra {
     const double* x;
     const double* y;
-    double4* rec_out;  // MODE 1: (x, y, input index bits, zone | shared << 8) per padded place
+    double4* rec_out;  // (x, y, input index bits, zone | shared << 8) per padded place
     int32_t* pos;
-    const uint8_t* zone;  // MODE 1, slab fits: zone per input point (else nullptr)
-    const uint8_t* shm;   // MODE 1, lean slab fits: 1 for the listed shared points (or nullptr)
+    const uint8_t* zone;  // slab fits: zone per input point (else nullptr)
+    const uint8_t* shm;   // lean slab fits: 1 for the listed shared points (or nullptr)
     const int32_t* pshift;
-    const int2* tseg;
-    const GridParams* gp;  // MODE 1 with key == nullptr: bin x, y here (grid_key)
+    const GridParams* gp;  // key == nullptr: bin x, y here (grid_key)
 };
 
 constexpr int kMsdParts = 4;
@@ -743,48 +737,30 @@ struct MsdSmem : DownsweepSmem<W> {
     double2 xy[kRTile / kMsdParts];  // one part's coordinates in sorted order
     uint16_t zn[kRTile / kMsdParts];  // and zones
 };
-template <int W, int MODE>
-__global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
-    const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
-    uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, uint32_t* __restrict__ key_fin,
-    int32_t* __restrict__ val_fin, int64_t n, int shift, const int32_t* __restrict__ bits_p,
-    const int32_t* __restrict__ hist_off, BucketExtra ex) {
+template <int W>
+__global__ __launch_bounds__(kBlock) void bucket_msd_kernel(const uint32_t* __restrict__ key,
+                                                            uint32_t* __restrict__ key_out,
+                                                            int64_t n,
+                                                            const int32_t* __restrict__ bits_p,
+                                                            const int32_t* __restrict__ hist_off,
+                                                            BucketExtra ex) {
     constexpr int RB = 1 << W;
     constexpr int DPT = RB > kBlock ? RB / kBlock : 1;
-    __shared__ std::conditional_t<MODE == 1, MsdSmem<W>, DownsweepSmem<W>> sm;
+    __shared__ MsdSmem<W> sm;
     const int t = threadIdx.x, w = t >> 6, lane = lane_id();
     const int64_t tb = sort_tile();
     const int64_t base = tb * kRTile;
     const int tile_n = (int)((n - base) < kRTile ? (n - base) : kRTile);
-    bool last = false;
-    if constexpr (MODE == 1) {
-        const int bits = *bits_p;
-        shift = bits > 8 ? bits - 8 : 0;
-    } else {
-        const int bits = *bits_p;
-        if (bits == 0) {  // the MSD pass sorted everything: the dense copy (first pass only)
-            if (shift != 0) return;
-            const int2 ts = ex.tseg[tb];
-            for (int j = t; j < tile_n; j += kBlock) {
-                const int64_t gp = base + j;
-                if (gp >= ts.y) continue;
-                const int64_t g = gp - ts.x;
-                const int32_t v = val ? val[gp] : (int32_t)gp;
-                key_fin[g] = key[gp];
-                val_fin[g] = v;
-            }
-            return;
-        }
-        if (shift >= bits) return;
-        last = shift + W >= bits;
-    }
+    const int bits = *bits_p;
+    const int shift = bits > 8 ? bits - 8 : 0;
     for (int k = t; k < kWaves * RB; k += kBlock) (&sm.cnt[0][0])[k] = 0;
     __syncthreads();
 
+    // per item: the key, its coordinates, (digit | rank in the wave's digit << 10); the input
+    // index is rematerialised, not held in registers (96 VGPRs: 5 waves per SIMD)
     uint32_t k_r[kRItems];
-    int32_t v_r[kRItems];
     uint32_t dr[kRItems];
-    double2 c_r[MODE == 1 ? kRItems : 1];
+    double2 c_r[kRItems];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
 #pragma unroll
@@ -792,18 +768,11 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
         const int64_t i = wbase + r * 64 + lane;
         const bool valid = i < base + tile_n;
         uint32_t k = kSentinelKey;
-        // (MODE 1: no payload in, the input index: rematerialised, not held in registers)
-        const int32_t v = valid ? ((MODE != 1 && val) ? val[i] : (int32_t)i) : 0;
-        if constexpr (MODE == 1)
-        {
-            c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
-            if (valid)
-                k = key ? key[i]
-                        : grid_key(c_r[r].x, c_r[r].y, ex.gp->xmin2, ex.gp->ymin2, ex.gp->invx,
-                                   ex.gp->invy, ex.gp->nx, ex.gp->ny, ex.gp->ntx);
-        } else {
-            if (valid) k = key[i];
-        }
+        c_r[r] = valid ? make_double2(ex.x[i], ex.y[i]) : make_double2(0.0, 0.0);
+        if (valid)
+            k = key ? key[i]
+                    : grid_key(c_r[r].x, c_r[r].y, ex.gp->xmin2, ex.gp->ymin2, ex.gp->invx,
+                               ex.gp->invy, ex.gp->nx, ex.gp->ny, ex.gp->ntx);
         const uint32_t d = (k >> shift) & (RB - 1u);
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -820,7 +789,6 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
         }
         old = __shfl(old, leader, 64);
         k_r[r] = k;
-        v_r[r] = v;
         dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 10)) : 0xFFFFFFFFu;
     }
     __syncthreads();
@@ -853,9 +821,7 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
             const int dd = t * DPT + j;
             if (dd < RB) {
                 sm.tile_start[dd] = at;
-                int32_t go = hist_off[tb * RB + dd];
-                if constexpr (MODE == 1) go += ex.pshift[dd];
-                sm.gofs[dd] = go;
+                sm.gofs[dd] = hist_off[tb * RB + dd] + ex.pshift[dd];
             }
             at += tot[j];
         }
@@ -867,56 +833,185 @@ __global__ __launch_bounds__(kBlock) void bucket_downsweep_kernel(
             const uint32_t d = dr[r] & 1023u;
             const int within = sm.cnt[w][d] + (int)(dr[r] >> 10);
             const int lpos = sm.tile_start[d] + within;
+            const int32_t i = (int32_t)(wbase + r * 64 + lane);
             sm.keys[lpos] = k_r[r];
-            sm.vals[lpos] = v_r[r];
-            if constexpr (MODE == 1) ex.pos[v_r[r]] = sm.gofs[d] + within;  // the place
+            sm.vals[lpos] = i;
+            ex.pos[i] = sm.gofs[d] + within;  // the place
         }
     }
     __syncthreads();
-    if constexpr (MODE == 1) {  // keys and records by digit run, a part of the tile at a time
-        constexpr int PS = kRTile / kMsdParts;
-        for (int p = 0; p < kMsdParts; ++p) {
-            if (p) __syncthreads();
+    // keys and records by digit run, a part of the tile at a time
+    constexpr int PS = kRTile / kMsdParts;
+    for (int p = 0; p < kMsdParts; ++p) {
+        if (p) __syncthreads();
 #pragma unroll
-            for (int r = 0; r < kRItems; ++r) {
-                if (dr[r] == 0xFFFFFFFFu) continue;
-                const uint32_t d = dr[r] & 1023u;
-                const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 10) - p * PS;
-                if (lpos >= 0 && lpos < PS) {
-                    const int64_t i = wbase + r * 64 + lane;
-                    sm.xy[lpos] = c_r[r];
-                    sm.zn[lpos] =
-                        ex.zone ? (uint16_t)(ex.zone[i] | ((ex.shm && ex.shm[i]) ? 256u : 0u)) : 0;
-                }
+        for (int r = 0; r < kRItems; ++r) {
+            if (dr[r] == 0xFFFFFFFFu) continue;
+            const uint32_t d = dr[r] & 1023u;
+            const int lpos = sm.tile_start[d] + sm.cnt[w][d] + (int)(dr[r] >> 10) - p * PS;
+            if (lpos >= 0 && lpos < PS) {
+                const int64_t i = wbase + r * 64 + lane;
+                sm.xy[lpos] = c_r[r];
+                sm.zn[lpos] =
+                    ex.zone ? (uint16_t)(ex.zone[i] | ((ex.shm && ex.shm[i]) ? 256u : 0u)) : 0;
             }
-            __syncthreads();
-            const int je = tile_n < (p + 1) * PS ? tile_n : (p + 1) * PS;
-            for (int j = p * PS + t; j < je; j += kBlock) {
-                const uint32_t k = sm.keys[j];
-                const uint32_t d = (k >> shift) & (RB - 1u);
-                const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
-                key_out[g] = k;
-                const double2 c = sm.xy[j - p * PS];
-                ex.rec_out[g] = make_double4(c.x, c.y, __longlong_as_double((long long)sm.vals[j]),
-                                             __longlong_as_double((long long)sm.zn[j - p * PS]));
-            }
+        }
+        __syncthreads();
+        const int je = tile_n < (p + 1) * PS ? tile_n : (p + 1) * PS;
+        for (int j = p * PS + t; j < je; j += kBlock) {
+            const uint32_t k = sm.keys[j];
+            const uint32_t d = (k >> shift) & (RB - 1u);
+            const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
+            key_out[g] = k;
+            const double2 c = sm.xy[j - p * PS];
+            ex.rec_out[g] = make_double4(c.x, c.y, __longlong_as_double((long long)sm.vals[j]),
+                                         __longlong_as_double((long long)sm.zn[j - p * PS]));
+        }
+    }
+}
+
+// The LSD passes inside the segments (bits = the low width, seg[kSegLBits]): the same ranking,
+// payload = padded place (identity on the first pass); the last pass writes the dense order,
+// key_fin and val_fin (slot -> padded place), pads dropped.  16-bit digit counters, and the
+// tile's digit offsets written over them once the tile is ranked into LDS: 22.5 KB for 9-bit
+// digits instead of 28.7, and at most 72 VGPRs, so 7 workgroups per CU instead of 5 (0.104 ->
+// 0.090 ms per 10^7 points for the two 9-bit passes, 1.77 -> 1.55 at config 5's share).
+// Not kept: two tiles per workgroup ranked together (digit runs twice as long): 0.104 -> 0.144.
+template <int W>
+struct LsdSmem {
+    static constexpr int RB = 1 << W;
+    union {
+        uint16_t cnt[kWaves][RB];  // per-wave digit counters -> wave offsets within a digit
+        int32_t gofs[RB];          // then the tile's digit offsets in the output
+    } u;
+    uint32_t keys[kRTile];
+    int32_t vals[kRTile];
+    int32_t tile_start[RB + 1];
+    int32_t wsum[kWaves];
+};
+
+template <int W>
+__global__ __launch_bounds__(kBlock, 7) void bucket_lsd_kernel(
+    const uint32_t* __restrict__ key, const int32_t* __restrict__ val,
+    uint32_t* __restrict__ key_out, int32_t* __restrict__ val_out, uint32_t* __restrict__ key_fin,
+    int32_t* __restrict__ val_fin, int64_t n, int shift, const int32_t* __restrict__ bits_p,
+    const int32_t* __restrict__ hist_off, const int2* __restrict__ tseg) {
+    constexpr int RB = 1 << W;
+    constexpr int DPT = RB > kBlock ? RB / kBlock : 1;
+    __shared__ LsdSmem<W> sm;
+    const int t = threadIdx.x, w = t >> 6, lane = lane_id();
+    const int64_t tb = sort_tile();
+    const int64_t base = tb * kRTile;
+    const int tile_n = (int)((n - base) < kRTile ? (n - base) : kRTile);
+    const int bits = *bits_p;
+    if (bits == 0) {  // the MSD pass sorted everything: the dense copy (first pass only)
+        if (shift != 0) return;
+        const int2 ts = tseg[tb];
+        for (int j = t; j < tile_n; j += kBlock) {
+            const int64_t gp = base + j;
+            if (gp >= ts.y) continue;
+            key_fin[gp - ts.x] = key[gp];
+            val_fin[gp - ts.x] = val ? val[gp] : (int32_t)gp;
         }
         return;
     }
-    const int2 ts = (MODE == 2 && last) ? ex.tseg[tb] : make_int2(0, 0);
+    if (shift >= bits) return;
+    const bool last = shift + W >= bits;
+    for (int k = t; k < kWaves * RB; k += kBlock) (&sm.u.cnt[0][0])[k] = 0;
+    __syncthreads();
+
+    uint32_t k_r[kRItems];
+    int32_t v_r[kRItems];
+    uint32_t dr[kRItems];
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t wbase = base + (int64_t)w * (kRTile / kWaves);
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {
+        const int64_t i = wbase + r * 64 + lane;
+        const bool valid = i < base + tile_n;
+        const uint32_t k = valid ? key[i] : kSentinelKey;
+        const int32_t v = valid ? (val ? val[i] : (int32_t)i) : 0;
+        const uint32_t d = (k >> shift) & (RB - 1u);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < W; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        int old = 0;
+        if (valid && lane == leader) {
+            old = sm.u.cnt[w][d];
+            sm.u.cnt[w][d] = (uint16_t)(old + __popcll(peers));
+        }
+        old = __shfl(old, leader, 64);
+        k_r[r] = k;
+        v_r[r] = v;
+        dr[r] = valid ? (d | ((uint32_t)(old + __popcll(peers & lt_mask)) << 10)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    int32_t go[DPT];
+    {
+        int tot[DPT];
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            int running = 0;
+            if (dd < RB) {
+                go[j] = hist_off[tb * RB + dd];
+#pragma unroll
+                for (int k = 0; k < kWaves; ++k) {
+                    const int c = sm.u.cnt[k][dd];
+                    sm.u.cnt[k][dd] = (uint16_t)running;
+                    running += c;
+                }
+            }
+            tot[j] = running;
+            mine += running;
+        }
+        const int incl = wave_incl_scan(mine);
+        if (lane == 63) sm.wsum[w] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int q = 0; q < w; ++q) woff += sm.wsum[q];
+        int at = woff + incl - mine;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int dd = t * DPT + j;
+            if (dd < RB) sm.tile_start[dd] = at;
+            at += tot[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRItems; ++r) {
+        if (dr[r] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[r] & 1023u;
+            const int lpos = sm.tile_start[d] + sm.u.cnt[w][d] + (int)(dr[r] >> 10);
+            sm.keys[lpos] = k_r[r];
+            sm.vals[lpos] = v_r[r];
+        }
+    }
+    __syncthreads();  // the counters are done with: the digit offsets over them
+#pragma unroll
+    for (int j = 0; j < DPT; ++j)
+        if (t * DPT + j < RB) sm.u.gofs[t * DPT + j] = go[j];
+    __syncthreads();
+    const int2 ts = last ? tseg[tb] : make_int2(0, 0);
     for (int j = t; j < tile_n; j += kBlock) {
         const uint32_t k = sm.keys[j];
         const uint32_t d = (k >> shift) & (RB - 1u);
-        const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
+        const int64_t g = (int64_t)sm.u.gofs[d] + (j - sm.tile_start[d]);
         const int32_t v = sm.vals[j];
-        if (MODE == 2 && last) {
+        if (last) {
             if (g >= ts.y) continue;  // a pad (pads sort after the segment's keys)
-            const int64_t gd = g - ts.x;
-            key_fin[gd] = k;
-            val_fin[gd] = v;
+            key_fin[g - ts.x] = k;
+            val_fin[g - ts.x] = v;
         } else {
             key_out[g] = k;
-            if (MODE != 1) val_out[g] = v;
+            val_out[g] = v;
         }
     }
 }
@@ -1125,11 +1220,9 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
                 dim3((unsigned)(256 + kPadTailBlocks + (ntp + kBlock - 1) / kBlock)), dim3(kBlock),
                 0, s, (const int32_t*)seg, np, ka, ntp, tseg);
 
-        const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, nullptr, gp};
-        klaunch(prof, "bucket_msd", bucket_downsweep_kernel<8, 1>, dim3((unsigned)nb),
-                dim3(kBlock), 0, s, key, (const int32_t*)nullptr, ka, (int32_t*)nullptr,
-                (uint32_t*)nullptr,
-                (int32_t*)nullptr, n, 0, bits_dev, (const int32_t*)ho, ex);
+        const BucketExtra ex{x, y, b.rec, b.pos, zone, shm, pshift, gp};
+        klaunch(prof, "bucket_msd", bucket_msd_kernel<8>, dim3((unsigned)nb), dim3(kBlock), 0, s,
+                key, ka, n, bits_dev, (const int32_t*)ho, ex);
 
         DBSCAN_HIP_CHECK(hipGetLastError());
     }
@@ -1139,8 +1232,6 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
     const int32_t* vin = nullptr;  // the first pass generates the identity
     uint32_t* kout = kb;
     int32_t* vout = jb;
-    const BucketExtra ex{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tseg,
-                         nullptr};
     const auto pass = [&](auto wtag, int shift) {
         constexpr int W = decltype(wtag)::value;
         StageTimer st(prof, s, "sort_bucket");
@@ -1151,9 +1242,9 @@ void bucket_sort(hipStream_t s, const double* x, const double* y, const uint32_t
         klaunch(prof, W == 8 ? "bucket_offsets<8>" : "bucket_offsets<9>",
                 bucket_offsets_kernel<W>, dim3(257), dim3(1024), 0, s, (const int32_t*)h, ho,
                 (const int32_t*)seg, shift);
-        klaunch(prof, dn, bucket_downsweep_kernel<W, 2>, dim3((unsigned)ntp), dim3(kBlock), 0, s,
-                kin, vin, kout, vout, b.key_fin, b.slot_place, np, shift, lbits,
-                (const int32_t*)ho, ex);
+        klaunch(prof, dn, bucket_lsd_kernel<W>, dim3((unsigned)ntp), dim3(kBlock), 0, s, kin, vin,
+                kout, vout, b.key_fin, b.slot_place, np, shift, lbits, (const int32_t*)ho,
+                (const int2*)tseg);
         DBSCAN_HIP_CHECK(hipGetLastError());
         kin = kout;
         vin = vout;

@@ -59,9 +59,10 @@ def stage_of(sym):
     base = sym.split("<")[0]
     if base in STAGE_OF:
         return STAGE_OF[base]
-    if base == "bucket_downsweep_kernel":  # <W, 1>: the MSD pass; <W, 2>: the segmented passes
-        w, mode = (int(v) for v in sym[len(base) + 1:-1].split(","))
-        return "bucket_msd" if mode == 1 else f"bucket_lsd<{w}>"
+    if base == "bucket_msd_kernel":  # the MSD pass
+        return "bucket_msd"
+    if base == "bucket_lsd_kernel":  # the segmented passes, per digit width
+        return f"bucket_lsd<{sym[len(base) + 1:-1].strip()}>"
     if base == "count_wave_kernel":  # instances by lanes per tile: the library's profile names
         seg = int(sym[len(base) + 1:-1].split(",")[1])
         return {64: "count_wave", 32: "count_tiny", 16: "count_tiny16"}[seg]
