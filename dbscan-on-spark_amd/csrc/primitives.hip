@@ -732,8 +732,17 @@ struct BucketExtra {
 };
 
 constexpr int kMsdParts = 4;
+// 25.6 KB (the input index held as its offset in the tile: 29.7 KB with 32-bit indices, 0.135
+// -> 0.129 ms per 10^7 points)
 template <int W>
-struct MsdSmem : DownsweepSmem<W> {
+struct MsdSmem {
+    static constexpr int RB = 1 << W;
+    uint16_t cnt[kWaves][RB];  // per-wave digit counters -> wave offsets within a digit
+    uint32_t keys[kRTile];
+    uint16_t vals[kRTile];  // the input index - the tile's base
+    int32_t tile_start[RB + 1];
+    int32_t gofs[RB];
+    int32_t wsum[kWaves];
     double2 xy[kRTile / kMsdParts];  // one part's coordinates in sorted order
     uint16_t zn[kRTile / kMsdParts];  // and zones
 };
@@ -835,7 +844,7 @@ __global__ __launch_bounds__(kBlock) void bucket_msd_kernel(const uint32_t* __re
             const int lpos = sm.tile_start[d] + within;
             const int32_t i = (int32_t)(wbase + r * 64 + lane);
             sm.keys[lpos] = k_r[r];
-            sm.vals[lpos] = i;
+            sm.vals[lpos] = (uint16_t)(i - base);
             ex.pos[i] = sm.gofs[d] + within;  // the place
         }
     }
@@ -864,7 +873,8 @@ __global__ __launch_bounds__(kBlock) void bucket_msd_kernel(const uint32_t* __re
             const int64_t g = (int64_t)sm.gofs[d] + (j - sm.tile_start[d]);
             key_out[g] = k;
             const double2 c = sm.xy[j - p * PS];
-            ex.rec_out[g] = make_double4(c.x, c.y, __longlong_as_double((long long)sm.vals[j]),
+            const long long vi = base + sm.vals[j];
+            ex.rec_out[g] = make_double4(c.x, c.y, __longlong_as_double(vi),
                                          __longlong_as_double((long long)sm.zn[j - p * PS]));
         }
     }
